@@ -1,0 +1,163 @@
+"""ctypes binding of ``libnifty_amd.so`` (the C ABI declared in
+``include/nifty_amd.h``).
+
+PyTorch is plumbing only: it owns the device buffers (caching allocator) and
+the stream; every hot-path computation is a call into the HIP library.  There
+is no CPU fallback: calling a hot-path function on a CPU tensor, or on a
+machine where the library cannot be loaded, raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnifty_amd.so")
+
+# names and argument signatures of every exported symbol (kept in sync with
+# include/nifty_amd.h; tests/test_abi.py checks both directions)
+_i, _i64, _sz, _d, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_double, ctypes.c_void_p
+SIGNATURES = {
+    "nft_last_error": (ctypes.c_char_p, []),
+    "nft_release_caches": (None, []),
+    "nft_fft_prepare": (_i, [_i, _i]),
+    "nft_hartley_workspace": (_i, [_i, _p, _i, _p, _i, ctypes.POINTER(_sz)]),
+    "nft_hartley": (_i, [_p, _p, _i, _p, _i, _p, _i, _i, _d, _p, _sz, _p]),
+    "nft_fft_c2c": (_i, [_p, _p, _i, _p, _i, _p, _i, _i, _d, _p]),
+    "nft_reduce_workspace": (_sz, [_i64]),
+    "nft_dot": (_i, [_p, _p, _i64, _i, _p, _p, _p]),
+    "nft_scale": (_i, [_p, _i64, _i, _d, _p]),
+    "nft_cg_update": (_i, [_p, _p, _p, _p, _p, _i64, _i, _p, _p, _p]),
+    "nft_cg_direction": (_i, [_p, _p, _i64, _i, _p, _p]),
+    "nft_cg_residual": (_i, [_p, _p, _p, _p, _i64, _i, _p, _p, _p]),
+}
+
+CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD = range(8)
+CG_NSCALARS = 16
+
+_lib = None
+_load_error = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load(required=True):
+    """Load the shared library once.  Raises NativeError if it is missing."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is None:
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+        except OSError as e:
+            _load_error = f"cannot load {LIB_PATH}: {e} (run __graft_entry__.build())"
+        except AttributeError as e:
+            _load_error = f"{LIB_PATH} lacks a symbol: {e} (stale build?)"
+    if _lib is None and required:
+        raise NativeError(_load_error)
+    return _lib
+
+
+def _check(status):
+    if status != 0:
+        msg = _lib.nft_last_error().decode(errors="replace")
+        raise NativeError(f"nifty_amd native call failed ({status}): {msg}")
+
+
+def dtype_code(t):
+    if t in (torch.float64, torch.complex128):
+        return 0
+    if t in (torch.float32, torch.complex64):
+        return 1
+    raise TypeError(f"unsupported dtype {t}")
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise NativeError("nifty_amd hot-path ops run on the GPU only "
+                              f"(got a {t.device} tensor); no CPU fallback exists")
+        if not t.is_contiguous():
+            raise NativeError("nifty_amd hot-path ops need contiguous tensors")
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _shape_args(shape, axes):
+    nd = len(shape)
+    sh = (ctypes.c_int64 * max(nd, 1))(*shape)
+    ax = (ctypes.c_int * max(len(axes), 1))(*axes)
+    return nd, sh, len(axes), ax
+
+
+_ws_cache = {}
+
+
+def workspace(nbytes, device, tag="ws"):
+    """Grow-only per-(device, tag) scratch buffer owned by the torch allocator."""
+    key = (str(device), tag)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def hartley(x, axes, convention=0, scale=1.0, out=None):
+    """out = scale * genuine Hartley transform of real x over `axes`."""
+    lib = load()
+    require_device(x)
+    if x.is_complex():
+        raise TypeError("hartley expects a real tensor")
+    if out is None:
+        out = torch.empty_like(x)
+    nd, sh, na, ax = _shape_args(tuple(x.shape), tuple(axes))
+    dt = dtype_code(x.dtype)
+    nbytes = ctypes.c_size_t(0)
+    _check(lib.nft_hartley_workspace(nd, sh, na, ax, dt, ctypes.byref(nbytes)))
+    ws = workspace(nbytes.value, x.device, "hartley")
+    _check(lib.nft_hartley(ptr(x), ptr(out), nd, sh, na, ax, dt, int(convention), float(scale),
+                           ptr(ws), ctypes.c_size_t(ws.numel()), stream_ptr()))
+    return out
+
+
+def fft_c2c(z, axes, forward=True, scale=1.0, out=None):
+    lib = load()
+    require_device(z)
+    if not z.is_complex():
+        raise TypeError("fft_c2c expects a complex tensor")
+    if out is None:
+        out = torch.empty_like(z)
+    nd, sh, na, ax = _shape_args(tuple(z.shape), tuple(axes))
+    _check(lib.nft_fft_c2c(ptr(z), ptr(out), nd, sh, na, ax, dtype_code(z.dtype), int(bool(forward)),
+                           float(scale), stream_ptr()))
+    return out
+
+
+def dot(a, b, out=None):
+    """Device fp64 scalar sum(a*b) (real tensors, deterministic)."""
+    lib = load()
+    require_device(a, b)
+    if a.numel() != b.numel():
+        raise ValueError("dot: size mismatch")
+    if out is None:
+        out = torch.empty((), dtype=torch.float64, device=a.device)
+    n = a.numel()
+    ws = workspace(lib.nft_reduce_workspace(n), a.device, "reduce")
+    _check(lib.nft_dot(ptr(a), ptr(b), n, dtype_code(a.dtype), ptr(out), ptr(ws), stream_ptr()))
+    return out

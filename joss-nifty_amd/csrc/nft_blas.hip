@@ -1,0 +1,313 @@
+// Deterministic reductions and fused conjugate-gradient vector primitives.
+//
+// Replaces, for the CG hot loop:
+//   ducc_dispatch.vdot / Field.s_vdot   src/ducc_dispatch.py:53-58,81-86,
+//                                       src/field.py:296-347
+//   the vector algebra of ConjugateGradient.__call__
+//                                       src/minimization/conjugate_gradient.py:78-126
+//   QuadraticEnergy value bookkeeping   src/minimization/quadratic_energy.py:31-39
+//
+// All sums accumulate in fp64 (also for fp32 storage) with a fixed two-level
+// tree: per-workgroup partials (wave64 shuffles + LDS) written to a partials
+// buffer, then one workgroup folds the partials in index order.  Results are
+// bitwise reproducible run to run (no float atomics).
+//
+// CG scalars live on the device (so a whole iteration can be captured in a
+// hipGraph) in a small double array, see the CG_* indices in nifty_amd.h.
+#include "nft_api_internal.hpp"
+#include "../../include/nifty_amd.h"
+
+namespace nft {
+
+constexpr int RED_NT = 256;
+constexpr int RED_MAXBLOCKS = 1024;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+// block reduction of NV values per thread; result valid in thread 0
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double s = wave_sum(v[k]);
+    if (lane == 0) sh[k * (RED_NT / 64) + wid] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      double s = 0;
+      for (int w = 0; w < RED_NT / 64; ++w) s += sh[k * (RED_NT / 64) + w];
+      v[k] = s;
+    }
+  }
+}
+
+static int red_blocks(long long n) {
+  long long b = (n + (RED_NT * 8) - 1) / (RED_NT * 8);
+  if (b < 1) b = 1;
+  if (b > RED_MAXBLOCKS) b = RED_MAXBLOCKS;
+  return (int)b;
+}
+
+// ------------------------------------------------------------------ dot
+template <typename T>
+__global__ __launch_bounds__(RED_NT) void dot_partial(const T* __restrict__ a, const T* __restrict__ b,
+                                                      long long n, double* __restrict__ part) {
+  __shared__ double sh[RED_NT / 64];
+  double v[1] = {0.0};
+  const long long stride = (long long)gridDim.x * RED_NT;
+  for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride)
+    v[0] += (double)a[i] * (double)b[i];
+  block_sum<1>(v, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = v[0];
+}
+
+// fold `nb` partial vectors of width W (layout part[k*nb + b]) into out[k]
+template <int W>
+__global__ __launch_bounds__(RED_NT) void fold_partials(const double* __restrict__ part, int nb,
+                                                        double* __restrict__ out) {
+  __shared__ double sh[W * (RED_NT / 64)];
+  double v[W];
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    v[k] = 0.0;
+    for (int b = threadIdx.x; b < nb; b += RED_NT) v[k] += part[k * nb + b];
+  }
+  block_sum<W>(v, sh);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) out[k] = v[k];
+  }
+}
+
+int scale_real_impl(void* x, long long n, int dtype, double scale, hipStream_t s);
+
+// ------------------------------------------------------------------ scale
+template <typename T>
+__global__ void scale_kernel(T* __restrict__ x, long long n, T s) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
+}
+
+int scale_real(void* x, long long n, int dtype, double scale, hipStream_t s) {
+  if (n <= 0) return NFT_OK;
+  int nb = (int)std::min<long long>((n + 255) / 256, 4096);
+  if (dtype == 0) hipLaunchKernelGGL(scale_kernel<double>, dim3(nb), dim3(256), 0, s, (double*)x, n, scale);
+  else hipLaunchKernelGGL(scale_kernel<float>, dim3(nb), dim3(256), 0, s, (float*)x, n, (float)scale);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+// ------------------------------------------------------------------ CG
+// x -= alpha d ; r -= alpha q   with alpha = sc[GAMMA] / sc[CURV]
+// partial dots: r.r, x.r, x.b
+// A non-finite or non-positive curvature, or alpha < 0, leaves x and r
+// untouched (the host maps the flag to IterationController.ERROR, exactly
+// like conjugate_gradient.py:85-95 returns the previous energy).
+template <typename T>
+__global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T* __restrict__ r,
+                                                           const T* __restrict__ d,
+                                                           const T* __restrict__ q,
+                                                           const T* __restrict__ b, long long n,
+                                                           const double* __restrict__ sc,
+                                                           double* __restrict__ part) {
+  __shared__ double sh[3 * (RED_NT / 64)];
+  const double curv = sc[NFT_CG_CURV], gprev = sc[NFT_CG_GAMMA];
+  const double alpha = gprev / curv;
+  const bool ok = (curv == curv) && curv != 0.0 && (alpha >= 0.0) && (alpha == alpha);
+  const T al = (T)alpha;
+  double v[3] = {0.0, 0.0, 0.0};
+  const long long stride = (long long)gridDim.x * RED_NT;
+  for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
+    T xi = x[i], ri = r[i];
+    if (ok) {
+      xi = xi - al * d[i];
+      ri = ri - al * q[i];
+      x[i] = xi;
+      r[i] = ri;
+    }
+    const double bi = b ? (double)b[i] : 0.0;
+    v[0] += (double)ri * (double)ri;
+    v[1] += (double)xi * (double)ri;
+    v[2] += (double)xi * bi;
+  }
+  block_sum<3>(v, sh);
+  if (threadIdx.x == 0) {
+    const int nb = gridDim.x;
+    part[0 * nb + blockIdx.x] = v[0];
+    part[1 * nb + blockIdx.x] = v[1];
+    part[2 * nb + blockIdx.x] = v[2];
+  }
+}
+
+// one workgroup: fold the 3 partial vectors, shift gamma, record alpha/flags
+__global__ __launch_bounds__(RED_NT) void cg_finalize_kernel(const double* __restrict__ part, int nb,
+                                                             double* __restrict__ sc) {
+  __shared__ double sh[3 * (RED_NT / 64)];
+  double v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    v[k] = 0.0;
+    for (int b = threadIdx.x; b < nb; b += RED_NT) v[k] += part[k * nb + b];
+  }
+  block_sum<3>(v, sh);
+  if (threadIdx.x == 0) {
+    const double curv = sc[NFT_CG_CURV], gprev = sc[NFT_CG_GAMMA];
+    const double alpha = gprev / curv;
+    const bool ok = (curv == curv) && curv != 0.0 && (alpha >= 0.0) && (alpha == alpha);
+    sc[NFT_CG_ALPHA] = alpha;
+    sc[NFT_CG_FLAG] = ok ? 0.0 : 1.0;
+    if (ok) {
+      sc[NFT_CG_GPREV] = gprev;
+      sc[NFT_CG_GAMMA] = v[0];
+      sc[NFT_CG_XR] = v[1];
+      sc[NFT_CG_XB] = v[2];
+    }
+  }
+}
+
+// d = max(0, gamma/gprev) d + r
+template <typename T>
+__global__ void cg_dir_kernel(T* __restrict__ d, const T* __restrict__ r, long long n,
+                              const double* __restrict__ sc) {
+  double beta = sc[NFT_CG_GAMMA] / sc[NFT_CG_GPREV];
+  if (!(beta > 0.0)) beta = 0.0;
+  const T bt = (T)beta;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    d[i] = bt * d[i] + r[i];
+}
+
+// r = ax - b (exact residual refresh, conjugate_gradient.py:103-105 via
+// QuadraticEnergy.__init__) and partial dots r.r, x.r, x.b
+template <typename T>
+__global__ __launch_bounds__(RED_NT) void cg_residual_kernel(T* __restrict__ r, const T* __restrict__ ax,
+                                                             const T* __restrict__ x,
+                                                             const T* __restrict__ b, long long n,
+                                                             double* __restrict__ part) {
+  __shared__ double sh[3 * (RED_NT / 64)];
+  double v[3] = {0.0, 0.0, 0.0};
+  const long long stride = (long long)gridDim.x * RED_NT;
+  for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
+    const T bi = b ? b[i] : (T)0;
+    const T ri = ax[i] - bi;
+    r[i] = ri;
+    const double xi = (double)x[i];
+    v[0] += (double)ri * (double)ri;
+    v[1] += xi * (double)ri;
+    v[2] += xi * (double)bi;
+  }
+  block_sum<3>(v, sh);
+  if (threadIdx.x == 0) {
+    const int nb = gridDim.x;
+    part[0 * nb + blockIdx.x] = v[0];
+    part[1 * nb + blockIdx.x] = v[1];
+    part[2 * nb + blockIdx.x] = v[2];
+  }
+}
+
+__global__ void cg_residual_finalize(const double* __restrict__ part, int nb, double* __restrict__ sc) {
+  __shared__ double sh[3 * (RED_NT / 64)];
+  double v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    v[k] = 0.0;
+    for (int b = threadIdx.x; b < nb; b += RED_NT) v[k] += part[k * nb + b];
+  }
+  block_sum<3>(v, sh);
+  if (threadIdx.x == 0) {
+    sc[NFT_CG_GPREV] = sc[NFT_CG_GAMMA];
+    sc[NFT_CG_GAMMA] = v[0];
+    sc[NFT_CG_XR] = v[1];
+    sc[NFT_CG_XB] = v[2];
+  }
+}
+
+}  // namespace nft
+
+using namespace nft;
+
+extern "C" {
+
+size_t nft_reduce_workspace(int64_t n) { return (size_t)3 * red_blocks(n) * sizeof(double); }
+
+int nft_dot(const void* a, const void* b, int64_t n, int dtype, double* out, void* ws,
+            hipStream_t stream) {
+  if (n < 0 || !out || !ws) {
+    set_last_error("nft_dot: bad arguments");
+    return NFT_ERR_ARG;
+  }
+  int nb = red_blocks(n);
+  double* part = (double*)ws;
+  if (dtype == 0)
+    hipLaunchKernelGGL(dot_partial<double>, dim3(nb), dim3(RED_NT), 0, stream, (const double*)a,
+                       (const double*)b, (long long)n, part);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(dot_partial<float>, dim3(nb), dim3(RED_NT), 0, stream, (const float*)a,
+                       (const float*)b, (long long)n, part);
+  else {
+    set_last_error("nft_dot: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
+  hipLaunchKernelGGL(fold_partials<1>, dim3(1), dim3(RED_NT), 0, stream, part, nb, out);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_scale(void* x, int64_t n, int dtype, double scale, hipStream_t stream) {
+  return scale_real(x, n, dtype, scale, stream);
+}
+
+int nft_cg_update(void* x, void* r, const void* d, const void* q, const void* b, int64_t n, int dtype,
+                  double* sc, void* ws, hipStream_t stream) {
+  int nb = red_blocks(n);
+  double* part = (double*)ws;
+  if (dtype == 0)
+    hipLaunchKernelGGL(cg_update_kernel<double>, dim3(nb), dim3(RED_NT), 0, stream, (double*)x,
+                       (double*)r, (const double*)d, (const double*)q, (const double*)b, (long long)n,
+                       sc, part);
+  else
+    hipLaunchKernelGGL(cg_update_kernel<float>, dim3(nb), dim3(RED_NT), 0, stream, (float*)x,
+                       (float*)r, (const float*)d, (const float*)q, (const float*)b, (long long)n, sc,
+                       part);
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(RED_NT), 0, stream, part, nb, sc);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_direction(void* d, const void* r, int64_t n, int dtype, const double* sc,
+                     hipStream_t stream) {
+  int nb = (int)std::min<long long>((n + 255) / 256, 8192);
+  if (nb < 1) nb = 1;
+  if (dtype == 0)
+    hipLaunchKernelGGL(cg_dir_kernel<double>, dim3(nb), dim3(256), 0, stream, (double*)d,
+                       (const double*)r, (long long)n, sc);
+  else
+    hipLaunchKernelGGL(cg_dir_kernel<float>, dim3(nb), dim3(256), 0, stream, (float*)d,
+                       (const float*)r, (long long)n, sc);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_residual(void* r, const void* ax, const void* x, const void* b, int64_t n, int dtype,
+                    double* sc, void* ws, hipStream_t stream) {
+  int nb = red_blocks(n);
+  double* part = (double*)ws;
+  if (dtype == 0)
+    hipLaunchKernelGGL(cg_residual_kernel<double>, dim3(nb), dim3(RED_NT), 0, stream, (double*)r,
+                       (const double*)ax, (const double*)x, (const double*)b, (long long)n, part);
+  else
+    hipLaunchKernelGGL(cg_residual_kernel<float>, dim3(nb), dim3(RED_NT), 0, stream, (float*)r,
+                       (const float*)ax, (const float*)x, (const float*)b, (long long)n, part);
+  hipLaunchKernelGGL(cg_residual_finalize, dim3(1), dim3(RED_NT), 0, stream, part, nb, sc);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+}  // extern "C"

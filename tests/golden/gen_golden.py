@@ -1,0 +1,328 @@
+"""Generate golden fixtures by importing the reference (NIFTy 8.5) in the
+build container.
+
+This script is the ONLY place that touches ``/root/reference``.  It runs here
+(the survey/build container), never on the GPU box, and writes small ``.npz``
+files next to itself.  Only these data files are committed; the reference
+source never leaves the container.
+
+Usage:  python tests/golden/gen_golden.py
+
+Harness shim: ``np.asfarray`` was removed in NumPy 2 but is still called by the
+reference (``src/utilities.py:397``, ``src/operators/normal_operators.py:48``);
+it is monkey-patched before import.
+"""
+import os
+import sys
+
+import numpy as np
+
+np.asfarray = lambda a, dtype=np.float64: np.asarray(a, dtype=dtype)  # noqa: E731
+sys.path.insert(0, "/root/reference")
+import nifty8 as ift  # noqa: E402
+from nifty8 import ducc_dispatch  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+CF_ARGS = dict(offset_mean=0, offset_std=(1e-3, 1e-6), fluctuations=(1., 0.8),
+               loglogavgslope=(-3., 1), flexibility=(2, 1.), asperity=(0.5, 0.4))
+
+
+def _save(name, d):
+    np.savez_compressed(os.path.join(OUT, name), **d)
+    tot = sum(v.nbytes for v in d.values() if isinstance(v, np.ndarray))
+    print(f"{name}: {len(d)} arrays, {tot/1e6:.2f} MB raw")
+
+
+def _flat(mf):
+    """MultiField -> dict of arrays with 'key' prefix, sorted keys."""
+    return {k: np.asarray(mf[k].val) for k in sorted(mf.keys())}
+
+
+def gen_dispatch():
+    """ducc_dispatch.hartley/fftn/ifftn/vdot (src/ducc_dispatch.py:38-58)."""
+    rng = np.random.default_rng(1234)
+    cases = [((16,), (0,)), ((7,), (0,)), ((19,), (0,)), ((12, 46), (0, 1)),
+             ((12, 9), (0, 1)), ((15, 12), (0, 1)), ((1, 2, 3, 6), (0, 1, 2, 3)),
+             ((64, 64), (0, 1)), ((16, 16, 16), (0, 1, 2)), ((128, 128), (0, 1)),
+             ((32, 4, 4, 5, 6), (0,)), ((32, 4, 4, 5, 6), (1, 2)),
+             ((32, 4, 4, 5, 6), (3, 4)), ((6, 64), (1,)), ((64, 6), (0,)),
+             ((8, 12, 10), (0, 2)), ((30, 21), (0, 1)), ((256,), (0,)),
+             ((2, 1024), (1,)), ((48, 32, 8), (0, 1, 2))]
+    d = {}
+    for i, (shp, axes) in enumerate(cases):
+        x = rng.standard_normal(shp)
+        d[f"c{i}_shape"] = np.array(shp)
+        d[f"c{i}_axes"] = np.array(axes)
+        d[f"c{i}_x"] = x
+        ift.config.update("hartley_convention", "non_canonical_hartley")
+        d[f"c{i}_h_nc"] = ducc_dispatch.hartley(x, axes=axes)
+        ift.config.update("hartley_convention", "canonical_hartley")
+        d[f"c{i}_h_c"] = ducc_dispatch.hartley(x, axes=axes)
+        ift.config.update("hartley_convention", "non_canonical_hartley")
+        x32 = x.astype(np.float32)
+        d[f"c{i}_h32_nc"] = ducc_dispatch.hartley(x32, axes=axes)
+        z = x + 1j * rng.standard_normal(shp)
+        d[f"c{i}_z"] = z
+        d[f"c{i}_fft"] = ducc_dispatch.fftn(z, axes=axes)
+        d[f"c{i}_ifft"] = ducc_dispatch.ifftn(z, axes=axes)
+        y = rng.standard_normal(shp)
+        d[f"c{i}_y"] = y
+        d[f"c{i}_vdot"] = np.array(ducc_dispatch.vdot(x, y))
+    d["ncases"] = np.array(len(cases))
+    _save("dispatch.npz", d)
+
+
+def gen_geometry():
+    """RGSpace/PowerSpace (src/domains/rg_space.py:105-150, power_space.py:155-198)."""
+    spaces = [((32, 32), None), ((128, 128), None), ((16, 16, 16), None),
+              ((17, 38), (0.99, 1340)), ((64,), None), ((12, 46), (.2, .3)),
+              ((7,), 0.2), ((9, 10, 11), (0.5, 0.3, 0.2))]
+    d = {}
+    for i, (shp, dist) in enumerate(spaces):
+        h = ift.RGSpace(shp, distances=dist, harmonic=True)
+        ps = ift.PowerSpace(h)
+        d[f"s{i}_shape"] = np.array(shp)
+        d[f"s{i}_dist"] = np.array(h.distances)
+        d[f"s{i}_klen"] = h.get_k_length_array().val
+        d[f"s{i}_uniq"] = h.get_unique_k_lengths()
+        d[f"s{i}_pindex"] = ps.pindex
+        d[f"s{i}_k_lengths"] = ps.k_lengths
+        d[f"s{i}_dvol"] = ps.dvol
+        pos = h.get_default_codomain()
+        d[f"s{i}_pos_dist"] = np.array(pos.distances)
+        pd = ift.PowerDistributor(h, ps)
+        rng = np.random.default_rng(i)
+        v = rng.standard_normal(ps.shape)
+        g = rng.standard_normal(h.shape)
+        d[f"s{i}_pd_in"] = v
+        d[f"s{i}_pd_times"] = pd(ift.makeField(ps, v)).val
+        d[f"s{i}_pd_adj_in"] = g
+        d[f"s{i}_pd_adj"] = pd.adjoint(ift.makeField(h, g)).val
+    d["nspaces"] = np.array(len(spaces))
+    _save("geometry.npz", d)
+
+
+def _cf_case(shape, args, seed, prefix=""):
+    """SimpleCorrelatedField forward/Jacobian/adjoint at a fixed point
+    (src/library/correlated_fields_simple.py:38-170)."""
+    pos_space = ift.RGSpace(shape)
+    cf = ift.SimpleCorrelatedField(pos_space, **args, prefix=prefix)
+    d = {}
+    with ift.random.Context(seed):
+        x = ift.from_random(cf.domain, "normal")
+        t = ift.from_random(cf.domain, "normal")
+        g = ift.from_random(cf.target, "normal")
+    lin = cf(ift.Linearization.make_var(x))
+    for k, v in _flat(x).items():
+        d["x_" + k] = v
+    for k, v in _flat(t).items():
+        d["t_" + k] = v
+    d["g"] = g.val
+    d["val"] = lin.val.val
+    d["jt"] = lin.jac(t).val
+    for k, v in _flat(lin.jac.adjoint(g)).items():
+        d["ja_" + k] = v
+    d["amp"] = cf.amplitude.force(x).val
+    d["pspec"] = cf.power_spectrum.force(x).val
+    return d, cf, x
+
+
+def gen_cf():
+    d, _, _ = _cf_case((128, 128), CF_ARGS, 11)
+    _save("cf128.npz", d)
+    args = dict(offset_mean=1.5, offset_std=None, fluctuations=(0.5, 0.2),
+                loglogavgslope=(-2., 0.5), flexibility=None, asperity=None)
+    d, _, _ = _cf_case((32, 32), args, 12, prefix="p_")
+    _save("cf32_noflex.npz", d)
+    args = dict(CF_ARGS)
+    args["asperity"] = None
+    d, _, _ = _cf_case((16, 16, 16), args, 13)
+    _save("cf16cube.npz", d)
+    d, _, _ = _cf_case((48, 20), CF_ARGS, 14)
+    _save("cf48x20.npz", d)
+
+
+def _gaussian_problem(n, seed=27, noise=0.01):
+    pos_space = ift.RGSpace((n, n))
+    cf = ift.SimpleCorrelatedField(pos_space, **CF_ARGS)
+    R = ift.GeometryRemover(pos_space)
+    sr = R @ cf
+    N = ift.ScalingOperator(R.target, noise, np.float64)
+    ift.random.push_sseq_from_seed(seed)
+    mock = ift.from_random(sr.domain, "normal")
+    data = sr(mock) + N.draw_sample()
+    lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ sr
+    pos = 0.1 * ift.from_random(sr.domain, "normal")
+    ift.random.pop_sseq()
+    return cf, lh, data, mock, pos
+
+
+def gen_metric_and_cg():
+    """Sampling metric 1 + J^T N^-1 J and CG traces
+    (kl_energies.py:115-123, conjugate_gradient.py:48-126)."""
+    from nifty8.minimization.quadratic_energy import QuadraticEnergy
+    cf, lh, data, mock, pos = _gaussian_problem(128)
+    d = {"data": data.val}
+    for k, v in _flat(mock).items():
+        d["mock_" + k] = v
+    for k, v in _flat(pos).items():
+        d["pos_" + k] = v
+    dtype, f_lh = lh.get_transformation()
+    fl = f_lh(ift.Linearization.make_var(pos))
+    met = ift.SandwichOperator.make(fl.jac, ift.ScalingOperator(f_lh.target, 1., dtype)) \
+        + ift.ScalingOperator(fl.domain, 1., float)
+    with ift.random.Context(99):
+        v = ift.from_random(fl.domain, "normal")
+        b = ift.from_random(fl.domain, "normal")
+    for k, val in _flat(v).items():
+        d["v_" + k] = val
+    for k, val in _flat(b).items():
+        d["b_" + k] = val
+    for k, val in _flat(met(v)).items():
+        d["mv_" + k] = val
+    d["flval"] = fl.val.val
+    # CG from x0 = 0, fixed iteration counts (nreset crossing at 20)
+    for k_it in (1, 5, 25):
+        ic = ift.GradientNormController(iteration_limit=k_it)
+        ic.enable_logging()
+        en = QuadraticEnergy(0 * b, met, b)
+        en, st = ift.ConjugateGradient(ic)(en)
+        for kk, val in _flat(en.position).items():
+            d[f"cg{k_it}_" + kk] = val
+        d[f"cg{k_it}_value"] = np.array(en.value)
+        d[f"cg{k_it}_status"] = np.array(st)
+        d[f"cg{k_it}_hist"] = np.array(ic.history._lst)
+    _save("metric128.npz", d)
+
+
+def gen_draw_samples():
+    """MGVI draw for config C1 (128^2, Gaussian, n_samples=2 mirrored, seed 27)
+    and a small geoVI draw (kl_energies.py:90-158)."""
+    cf, lh, data, mock, pos = _gaussian_problem(128)
+    d = {}
+    for name, ic in (("fixed", ift.GradientNormController(iteration_limit=20)),
+                     ("absdelta", ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=100))):
+        ic.enable_logging()
+        H = ift.StandardHamiltonian(lh, ic)
+        ift.random.push_sseq_from_seed(27)
+        sl = ift.minimization.kl_energies.draw_samples(pos, H, None, 2, True)
+        ift.random.pop_sseq()
+        for i, (r, neg) in enumerate(zip(sl._r, sl._n)):
+            for k, v in _flat(r).items():
+                d[f"{name}_r{i}_" + k] = v
+            d[f"{name}_neg{i}"] = np.array(neg)
+        d[f"{name}_niter"] = np.array(len(ic.history._lst))
+    _save("mgvi128.npz", d)
+
+    # geoVI on 32x32 (small, exercises NewtonCG + line search)
+    cf, lh, data, mock, pos = _gaussian_problem(32)
+    dd = {"data": data.val}
+    for k, v in _flat(pos).items():
+        dd["pos_" + k] = v
+    ic = ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=100)
+    H = ift.StandardHamiltonian(lh, ic)
+    mini = ift.NewtonCG(ift.AbsDeltaEnergyController(deltaE=0.5, convergence_level=2,
+                                                     iteration_limit=5))
+    ift.random.push_sseq_from_seed(27)
+    sl = ift.minimization.kl_energies.draw_samples(pos, H, mini, 1, True)
+    ift.random.pop_sseq()
+    for i, r in enumerate(sl._r):
+        for k, v in _flat(r).items():
+            dd[f"r{i}_" + k] = v
+    _save("geovi32.npz", dd)
+
+
+def gen_poisson():
+    """Config C2 flavour (exp(cf), Poisson counts) at 64^2
+    (energy_operators.py:586-625)."""
+    pos_space = ift.RGSpace((64, 64))
+    cf = ift.SimpleCorrelatedField(pos_space, **CF_ARGS)
+    sig = cf.exp()
+    ift.random.push_sseq_from_seed(27)
+    mock = ift.from_random(sig.domain, "normal")
+    lam = sig(mock).val
+    counts = ift.random.current_rng().poisson(lam).astype(np.int64)
+    data = ift.makeField(pos_space, counts)
+    lh = ift.PoissonianEnergy(data) @ sig
+    pos = 0.1 * ift.from_random(sig.domain, "normal")
+    ift.random.pop_sseq()
+    d = {"counts": counts}
+    for k, v in _flat(pos).items():
+        d["pos_" + k] = v
+    dtype, f_lh = lh.get_transformation()
+    fl = f_lh(ift.Linearization.make_var(pos))
+    d["flval"] = fl.val.val
+    met = ift.SandwichOperator.make(fl.jac, ift.ScalingOperator(f_lh.target, 1., dtype)) \
+        + ift.ScalingOperator(fl.domain, 1., float)
+    with ift.random.Context(5):
+        v = ift.from_random(fl.domain, "normal")
+    for k, val in _flat(v).items():
+        d["v_" + k] = val
+    for k, val in _flat(met(v)).items():
+        d["mv_" + k] = val
+    d["energy"] = np.array(lh(pos).val)
+    ic = ift.GradientNormController(iteration_limit=10)
+    H = ift.StandardHamiltonian(lh, ic)
+    ift.random.push_sseq_from_seed(3)
+    sl = ift.minimization.kl_energies.draw_samples(pos, H, None, 1, True)
+    ift.random.pop_sseq()
+    for i, r in enumerate(sl._r):
+        for k, val in _flat(r).items():
+            d[f"r{i}_" + k] = val
+    _save("poisson64.npz", d)
+
+
+def gen_los():
+    """LOSResponse construction + matvec/rmatvec (los_response.py:34-233)."""
+    d = {}
+    for i, (shp, nlos) in enumerate((((64, 64), 200), ((40, 24), 50), ((12, 10, 8), 30))):
+        space = ift.RGSpace(shp)
+        rng = np.random.default_rng(100 + i)
+        starts = rng.random((len(shp), nlos))
+        ends = rng.random((len(shp), nlos))
+        R = ift.LOSResponse(space, starts=list(starts), ends=list(ends))
+        coo = R._smat.A  # the underlying scipy coo_matrix
+        x = rng.standard_normal(shp)
+        y = rng.standard_normal(nlos)
+        d[f"l{i}_shape"] = np.array(shp)
+        d[f"l{i}_starts"] = starts
+        d[f"l{i}_ends"] = ends
+        d[f"l{i}_row"] = coo.row.astype(np.int32)
+        d[f"l{i}_col"] = coo.col.astype(np.int32)
+        d[f"l{i}_wgt"] = coo.data
+        d[f"l{i}_x"] = x
+        d[f"l{i}_y"] = y
+        d[f"l{i}_Rx"] = R(ift.makeField(space, x)).val
+        d[f"l{i}_Rty"] = R.adjoint(ift.makeField(R.target, y)).val
+    _save("los.npz", d)
+
+
+def gen_random():
+    """RNG stream order: from_random on a MultiDomain draws keys in sorted
+    order (multi_field.py:103-127); spawn_sseq children (random.py:114-133)."""
+    dom = ift.makeDomain({"zeta": ift.RGSpace(5), "alpha": ift.RGSpace((2, 3)),
+                          "mid": ift.DomainTuple.scalar_domain()})
+    d = {}
+    with ift.random.Context(7):
+        mf = ift.from_random(dom, "normal", std=2.)
+    for k, v in _flat(mf).items():
+        d["mf_" + k] = v
+    ift.random.push_sseq_from_seed(27)
+    ss = ift.random.spawn_sseq(3)
+    for i, s in enumerate(ss):
+        with ift.random.Context(s):
+            d[f"child{i}"] = ift.random.current_rng().standard_normal(4)
+    ift.random.pop_sseq()
+    _save("random.npz", d)
+
+
+if __name__ == "__main__":
+    gen_dispatch()
+    gen_geometry()
+    gen_cf()
+    gen_metric_and_cg()
+    gen_draw_samples()
+    gen_poisson()
+    gen_los()
+    gen_random()
