@@ -92,6 +92,20 @@ int nft_cg_direction(void* d, const void* r, int64_t n, int dtype, const double*
 int nft_cg_residual(void* r, const void* ax, const void* x, const void* b, int64_t n, int dtype,
                     double* sc, void* ws, hipStream_t stream);
 
+/* ---- power-bin distributor -------------------------------------------- */
+/* out[p,i,q] = in[p, pindex[i], q]; in: [pre, nbins, post], out: [pre, npix, post] */
+int nft_bin_gather(const void* in, const int* pindex, void* out, int64_t pre, int64_t npix,
+                   int64_t nbins, int64_t post, int dtype, hipStream_t stream);
+/* out[p,b,q] = sum_{j in [offsets[b], offsets[b+1])} in[p, perm[j], q], summed in
+ * ascending j (perm = stable argsort of pindex: np.bincount order, bit-exact) */
+int nft_bin_scatter(const void* in, const int* perm, const int* offsets, void* out, int64_t pre,
+                    int64_t npix, int64_t nbins, int64_t post, int dtype, hipStream_t stream);
+
+/* ---- sparse LOS response --------------------------------------------- */
+/* y[r] = scale * sum_j weights[j] * x[indices[j]], j in [indptr[r], indptr[r+1]) */
+int nft_spmv_csr(const int64_t* indptr, const int* indices, const float* weights, const void* x,
+                 void* y, int64_t nrows, int dtype, double scale, int64_t nnz, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,6 +30,9 @@ SIGNATURES = {
     "nft_cg_update": (_i, [_p, _p, _p, _p, _p, _i64, _i, _p, _p, _p]),
     "nft_cg_direction": (_i, [_p, _p, _i64, _i, _p, _p]),
     "nft_cg_residual": (_i, [_p, _p, _p, _p, _i64, _i, _p, _p, _p]),
+    "nft_bin_gather": (_i, [_p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
+    "nft_bin_scatter": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
+    "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
 }
 
 CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD = range(8)
@@ -161,3 +164,28 @@ def dot(a, b, out=None):
     ws = workspace(lib.nft_reduce_workspace(n), a.device, "reduce")
     _check(lib.nft_dot(ptr(a), ptr(b), n, dtype_code(a.dtype), ptr(out), ptr(ws), stream_ptr()))
     return out
+
+
+def bin_gather(src, pindex, out, pre, npix, nbins, post):
+    lib = load()
+    require_device(src, pindex, out)
+    _check(lib.nft_bin_gather(ptr(src), ptr(pindex), ptr(out), pre, npix, nbins, post,
+                              dtype_code(src.dtype), stream_ptr()))
+    return out
+
+
+def bin_scatter(src, perm, offsets, out, pre, npix, nbins, post):
+    lib = load()
+    require_device(src, perm, offsets, out)
+    _check(lib.nft_bin_scatter(ptr(src), ptr(perm), ptr(offsets), ptr(out), pre, npix, nbins, post,
+                               dtype_code(src.dtype), stream_ptr()))
+    return out
+
+
+def spmv_csr(indptr, indices, weights, x, y, scale=1.0):
+    lib = load()
+    require_device(indptr, indices, weights, x, y)
+    nrows = indptr.numel() - 1
+    _check(lib.nft_spmv_csr(ptr(indptr), ptr(indices), ptr(weights), ptr(x), ptr(y), nrows,
+                            dtype_code(x.dtype), float(scale), indices.numel(), stream_ptr()))
+    return y

@@ -1,0 +1,355 @@
+"""SimpleCorrelatedField as one fused device model
+(src/library/correlated_fields_simple.py:38-170).
+
+    s(xi, theta) = offset_mean + c_h * HT[ A(theta)[pindex] * xi ]
+
+with the non-parametric amplitude A(theta) of correlated_fields.py
+(_TwoLogIntegrations, _SlopeRemover, _Normalization, fluctuation scaling,
+zero-mode insertion, total-volume scaling) and HT the harmonic->position
+Hartley transform with harmonic volume factor c_h.
+
+Instead of the reference's operator tree (~40 nodes, each a separate pass
+over its array) the model is one Operator whose Linearization carries a
+single fused Jacobian node, CFJacobian:
+
+    J [dxi, dtheta] = c_h HT[ A_full * dxi + xi0 * (dA(dtheta))[pindex] ]
+    J^T g           = ( A_full * v ,  dA^T( bins(xi0 * v) ) ),  v = c_h HT g
+
+whose grid work runs in the native kernels (Hartley passes, power-bin
+gather/scatter) and whose B-sized amplitude Jacobian is a short sequence of
+device tensor ops.  CFJacobian also implements ``sandwich_apply`` /
+``metric_flat`` so that SandwichOperator and the fused CG can evaluate
+J^T W J without materialising the operator tree."""
+import numpy as np
+import torch
+
+from .. import _native, config
+from ..domain_tuple import DomainTuple
+from ..domains import PowerSpace, UnstructuredDomain
+from ..ducc_dispatch import hartley
+from ..field import Field
+from ..linearization import Linearization
+from ..multi_domain import MultiDomain
+from ..multi_field import MultiField
+from ..operators.distributors import BinIndex
+from ..operators.linear_operator import LinearOperator
+from ..operators.operator import Operator
+from ..packing import PackedLayout
+from ..utilities import lognormal_moments
+from .correlated_fields import (_log_vol, _relative_log_k_lengths, mode_multiplicity, slope_remove,
+                                slope_remove_adjoint, twolog, twolog_adjoint)
+
+
+def _t(a):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=config.device())
+
+
+class _AmplitudeModel:
+    """Amplitude A(theta) on the PowerSpace, its JVP and VJP (B-sized math)."""
+
+    def __init__(self, target, harmonic_partner, offset_std, fluctuations, flexibility, asperity,
+                 loglogavgslope, prefix):
+        self.pspace = PowerSpace(harmonic_partner)
+        self.B = self.pspace.shape[0]
+        self.prefix = prefix
+        p = prefix
+        self.k_fl, self.k_sl = p + "fluctuations", p + "loglogavgslope"
+        self.k_flex, self.k_asp = p + "flexibility", p + "asperity"
+        self.k_spec, self.k_zm = p + "spectrum", p + "zeromode"
+        self.has_flex = flexibility is not None
+        self.has_asp = asperity is not None
+        self.has_zm = offset_std is not None
+        self.lm_f, self.ls_f = (float(v) for v in lognormal_moments(*fluctuations))
+        self.mu_s, self.sig_s = float(loglogavgslope[0]), float(loglogavgslope[1])
+        if self.has_flex:
+            self.lm_x, self.ls_x = (float(v) for v in lognormal_moments(*flexibility))
+        if self.has_asp:
+            self.lm_a, self.ls_a = (float(v) for v in lognormal_moments(*asperity))
+        if self.has_zm:
+            self.lm_o, self.ls_o = (float(v) for v in lognormal_moments(*offset_std))
+        self.total_vol = float(target.total_volume)
+        self.vslope = _t(_relative_log_k_lengths(self.pspace))
+        rl = _relative_log_k_lengths(self.pspace)
+        self.sc = _t(rl / float(rl[-1]))
+        self.mult = _t(mode_multiplicity(self.pspace))
+        if self.has_flex:
+            lv = _log_vol(self.pspace)
+            self.lv = _t(lv)
+            self.sqrt_lv = _t(np.sqrt(lv))
+            self.shift0 = _t(lv ** 2 / 12.)
+        dom = {self.k_fl: DomainTuple.scalar_domain(), self.k_sl: DomainTuple.scalar_domain()}
+        if self.has_flex:
+            dom[self.k_flex] = DomainTuple.scalar_domain()
+            dom[self.k_spec] = DomainTuple.make(UnstructuredDomain((2, self.B - 2)))
+        if self.has_asp:
+            dom[self.k_asp] = DomainTuple.scalar_domain()
+        if self.has_zm:
+            dom[self.k_zm] = DomainTuple.scalar_domain()
+        self.domain_dict = dom
+
+    # ------------------------------------------------------------- forward
+    def forward(self, lat):
+        """lat: dict key -> device tensor.  Returns (a, cache)."""
+        c = {}
+        fl = torch.exp(self.lm_f + self.ls_f * lat[self.k_fl])
+        avgsl = self.mu_s + self.sig_s * lat[self.k_sl]
+        apre = self.vslope * avgsl
+        if self.has_flex:
+            flex = torch.exp(self.lm_x + self.ls_x * lat[self.k_flex])
+            sf = self.sqrt_lv * flex
+            if self.has_asp:
+                asp = torch.exp(self.lm_a + self.ls_a * lat[self.k_asp])
+                sq0 = torch.sqrt(self.shift0 + asp)
+                c["asp"] = asp
+            else:
+                sq0 = torch.sqrt(self.shift0)
+            xs = lat[self.k_spec]
+            at0 = xs[0] * sf * sq0
+            at1 = xs[1] * sf
+            apre = apre + slope_remove(twolog(at0, at1, self.lv), self.sc)
+            c.update(flex=flex, sf=sf, sq0=sq0, xs=xs)
+        spec = torch.exp(apre)
+        S = torch.sum(self.mult * spec)
+        An = torch.sqrt(spec * (1. / S))
+        a = fl * An
+        a = torch.cat([a.new_zeros(1), a[1:]])
+        if self.has_zm:
+            zm = torch.exp(self.lm_o + self.ls_o * lat[self.k_zm])
+            a = a + torch.cat([zm.reshape(1), a.new_zeros(self.B - 1)])
+            c["zm"] = zm
+        a = a * self.total_vol
+        c.update(fl=fl, spec=spec, S=S, An=An)
+        return a, c
+
+    def jvp(self, c, t):
+        dfl = c["fl"] * self.ls_f * t[self.k_fl]
+        dapre = self.vslope * (self.sig_s * t[self.k_sl])
+        if self.has_flex:
+            dsf = c["sf"] * (self.ls_x * t[self.k_flex])
+            xs, ts, sf, sq0 = c["xs"], t[self.k_spec], c["sf"], c["sq0"]
+            dat0 = ts[0] * sf * sq0 + xs[0] * dsf * sq0
+            if self.has_asp:
+                dsq0 = c["asp"] * self.ls_a * t[self.k_asp] / (2. * sq0)
+                dat0 = dat0 + xs[0] * sf * dsq0
+            dat1 = ts[1] * sf + xs[1] * dsf
+            dapre = dapre + slope_remove(twolog(dat0, dat1, self.lv), self.sc)
+        spec, S, An = c["spec"], c["S"], c["An"]
+        dS = torch.sum(self.mult * spec * dapre)
+        dAn = An * (dapre / 2. - dS / (2. * S))
+        da = dfl * An + c["fl"] * dAn
+        da = torch.cat([da.new_zeros(1), da[1:]])
+        if self.has_zm:
+            dzm = c["zm"] * self.ls_o * t[self.k_zm]
+            da = da + torch.cat([dzm.reshape(1), da.new_zeros(self.B - 1)])
+        return da * self.total_vol
+
+    def vjp(self, c, g):
+        """g: (B,) cotangent of a.  Returns dict key -> cotangent tensors."""
+        out = {}
+        g = g * self.total_vol
+        if self.has_zm:
+            out[self.k_zm] = c["zm"] * self.ls_o * g[0]
+        gm = torch.cat([g.new_zeros(1), g[1:]])
+        An, spec, S = c["An"], c["spec"], c["S"]
+        out[self.k_fl] = c["fl"] * self.ls_f * torch.sum(gm * An)
+        gAn = c["fl"] * gm
+        gapre = An * gAn / 2. - self.mult * spec * (torch.sum(gAn * An) / (2. * S))
+        out[self.k_sl] = self.sig_s * torch.sum(self.vslope * gapre)
+        if self.has_flex:
+            gtl = slope_remove_adjoint(gapre, self.sc)
+            g0, g1 = twolog_adjoint(gtl, self.lv)
+            xs, sf, sq0 = c["xs"], c["sf"], c["sq0"]
+            out[self.k_spec] = torch.stack([g0 * sf * sq0, g1 * sf])
+            gsf = g0 * xs[0] * sq0 + g1 * xs[1]
+            out[self.k_flex] = c["flex"] * self.ls_x * torch.sum(gsf * self.sqrt_lv)
+            if self.has_asp:
+                gsq0 = g0 * xs[0] * sf
+                out[self.k_asp] = c["asp"] * self.ls_a * torch.sum(gsq0 / (2. * sq0))
+        return out
+
+
+class _AmplitudeJacobian(LinearOperator):
+    def __init__(self, amp, cache, domain, target):
+        self._amp, self._c = amp, cache
+        self._domain, self._target = domain, target
+        self._capability = self.TIMES | self.ADJOINT_TIMES
+
+    def apply(self, x, mode):
+        self._check_input(x, mode)
+        if mode == self.TIMES:
+            return Field(self._target, self._amp.jvp(self._c, {k: x[k].val for k in x.keys()}))
+        g = self._amp.vjp(self._c, x.val)
+        return MultiField(self._domain, tuple(Field(self._domain[k], g[k]) for k in self._domain.keys()))
+
+
+class _AmplitudeOperator(Operator):
+    """`op.amplitude` of the reference: latent (without xi) -> PowerSpace."""
+
+    def __init__(self, amp, power=1):
+        self._amp = amp
+        self._domain = MultiDomain.make(amp.domain_dict)
+        self._target = DomainTuple.make(amp.pspace)
+        self._power = power
+
+    def apply(self, x):
+        self._check_input(x)
+        lin = x.jac is not None
+        v = x.val if lin else x
+        a, c = self._amp.forward({k: v[k].val for k in self._domain.keys()})
+        res = Field(self._target, a if self._power == 1 else a ** 2)
+        if not lin:
+            return res
+        jac = _AmplitudeJacobian(self._amp, c, self._domain, self._target)
+        if self._power == 2:
+            from ..sugar import makeOp
+            jac = makeOp(Field(self._target, 2. * a)) @ jac
+        return x.new(res, jac)
+
+    def force(self, x):
+        return self.apply(x.extract(self._domain))
+
+
+class CFJacobian(LinearOperator):
+    """Fused Jacobian of the correlated field at an expansion point."""
+
+    def __init__(self, model, cache, a, afull, xi0):
+        self._m = model
+        self._c = cache
+        self._a = a
+        self._afull = afull
+        self._xi0 = xi0
+        self._domain = model.domain
+        self._target = model.target
+        self._capability = self.TIMES | self.ADJOINT_TIMES
+        self.device = afull.device
+
+    @property
+    def layout(self):
+        return self._m.layout
+
+    # ---------------------------------------------------------- primitives
+    def _times_t(self, t):
+        """t: dict key->tensor tangent.  Returns position-space grid tensor."""
+        m = self._m
+        da = m.amp.jvp(self._c, t)
+        dafull = torch.empty_like(self._afull)
+        b = m.bins
+        _native.bin_gather(da, b.pindex, dafull, 1, b.npix, b.nbin, 1)
+        u = self._afull * t[m.k_xi] + self._xi0 * dafull
+        return hartley(u, scale=m.c_h)
+
+    def _adjoint_t(self, g, out=None):
+        """g: grid tensor.  Returns dict key->tensor (or fills `out` views)."""
+        m = self._m
+        v = hartley(g.contiguous(), scale=m.c_h)
+        gxi = self._afull * v
+        ga = torch.empty(m.amp.B, dtype=v.dtype, device=v.device)
+        b = m.bins
+        _native.bin_scatter((self._xi0 * v).contiguous(), b.perm, b.offsets, ga, 1, b.npix, b.nbin, 1)
+        res = m.amp.vjp(self._c, ga)
+        res[m.k_xi] = gxi
+        return res
+
+    def apply(self, x, mode):
+        self._check_input(x, mode)
+        if mode == self.TIMES:
+            return Field(self._target, self._times_t({k: x[k].val for k in x.keys()}))
+        res = self._adjoint_t(x.val)
+        return MultiField(self._domain, tuple(Field(self._domain[k], res[k].reshape(self._domain[k].shape))
+                                              for k in self._domain.keys()))
+
+    def sandwich_apply(self, x, W):
+        """J^T W J x for a latent MultiField x, W a grid tensor."""
+        s = self._times_t({k: x[k].val for k in x.keys()})
+        res = self._adjoint_t(s * W)
+        return MultiField(self._domain, tuple(Field(self._domain[k], res[k].reshape(self._domain[k].shape))
+                                              for k in self._domain.keys()))
+
+    def metric_flat(self, d, q, W, shift):
+        """q = shift * d + J^T W J d on packed latent buffers (fused CG)."""
+        lay = self.layout
+        dv = lay.views(d)
+        s = self._times_t(dv)
+        res = self._adjoint_t(s * W)
+        qv = lay.views(q)
+        for k in lay.keys:
+            r = res[k].reshape(qv[k].shape)
+            if shift != 0.0:
+                torch.add(r, dv[k], alpha=shift, out=qv[k])
+            else:
+                qv[k].copy_(r)
+
+
+class _CorrelatedFieldModel(Operator):
+    def __init__(self, target, harmonic_partner, offset_mean, offset_std, fluctuations, flexibility,
+                 asperity, loglogavgslope, prefix):
+        self.amp = _AmplitudeModel(target, harmonic_partner, offset_std, fluctuations, flexibility,
+                                   asperity, loglogavgslope, prefix)
+        self.k_xi = prefix + "xi"
+        dom = dict(self.amp.domain_dict)
+        dom[self.k_xi] = DomainTuple.make(harmonic_partner)
+        self._domain = MultiDomain.make(dom)
+        self._target = DomainTuple.make(target)
+        self.harmonic_partner = harmonic_partner
+        self.c_h = float(harmonic_partner.scalar_dvol)
+        self.offset_mean = None if offset_mean is None else float(offset_mean)
+        self.bins = BinIndex.get(self.amp.pspace.pindex, self.amp.B, config.device())
+        self._layout = None
+        self.amplitude = _AmplitudeOperator(self.amp)
+        self.power_spectrum = _AmplitudeOperator(self.amp, power=2)
+
+    @property
+    def layout(self):
+        if self._layout is None:
+            self._layout = PackedLayout(self._domain)
+        return self._layout
+
+    def _value(self, lat):
+        a, c = self.amp.forward(lat)
+        afull = torch.empty(self.harmonic_partner.shape, dtype=a.dtype, device=a.device)
+        b = self.bins
+        _native.bin_gather(a, b.pindex, afull, 1, b.npix, b.nbin, 1)
+        s = hartley(afull * lat[self.k_xi], scale=self.c_h)
+        if self.offset_mean is not None:
+            s = s + self.offset_mean
+        return s, a, c, afull
+
+    def apply(self, x):
+        self._check_input(x)
+        lin = x.jac is not None
+        v = x.val if lin else x
+        lat = {k: v[k].val for k in self._domain.keys()}
+        s, a, c, afull = self._value(lat)
+        res = Field(self._target, s)
+        if not lin:
+            return res
+        jac = CFJacobian(self, c, a, afull, lat[self.k_xi])
+        return x.new(res, jac)
+
+    def __repr__(self):
+        return f"SimpleCorrelatedField (fused) {self._target.shape}"
+
+
+def SimpleCorrelatedField(target, offset_mean, offset_std, fluctuations, flexibility, asperity,
+                          loglogavgslope, prefix="", harmonic_partner=None):
+    """Same signature and latent keys as the reference
+    (correlated_fields_simple.py:38-48)."""
+    target = DomainTuple.make(target)
+    if len(target) != 1:
+        raise ValueError
+    target = target[0]
+    if harmonic_partner is None:
+        harmonic_partner = target.get_default_codomain()
+    else:
+        target.check_codomain(harmonic_partner)
+        harmonic_partner.check_codomain(target)
+    for kk in (fluctuations, loglogavgslope):
+        if len(kk) != 2:
+            raise TypeError
+    for kk in (offset_std, flexibility, asperity):
+        if not (kk is None or len(kk) == 2):
+            raise TypeError
+    if flexibility is None and asperity is not None:
+        raise ValueError
+    return _CorrelatedFieldModel(target, harmonic_partner, offset_mean, offset_std, fluctuations,
+                                 flexibility, asperity, loglogavgslope, prefix)

@@ -1,0 +1,86 @@
+"""DescentMinimizer / NewtonCG (src/minimization/descent_minimizers.py:24-206);
+the geoVI nonlinear sample refinement runs NewtonCG on
+GaussianEnergy(m) @ transformation (kl_energies.py:147-155)."""
+from ..logger import logger
+from .conjugate_gradient import ConjugateGradient
+from .iteration_controllers import AbsDeltaEnergyController, GradientNormController
+from .line_search import LineSearch
+from .minimizer import Minimizer
+from .quadratic_energy import QuadraticEnergy
+
+
+class DescentMinimizer(Minimizer):
+    def __init__(self, controller, line_searcher=LineSearch()):
+        self._controller = controller
+        self.line_searcher = line_searcher
+
+    def __call__(self, energy):
+        f_k_minus_1 = None
+        controller = self._controller
+        status = controller.start(energy)
+        if status != controller.CONTINUE:
+            return energy, status
+        while True:
+            if energy.gradient_norm == 0:
+                return energy, controller.CONVERGED
+            new_energy, success = self.line_searcher.perform_line_search(
+                energy=energy, pk=self.get_descent_direction(energy, f_k_minus_1), f_k_minus_1=f_k_minus_1)
+            if not success:
+                self.reset()
+            f_k_minus_1 = energy.value
+            if new_energy.value > energy.value:
+                logger.error("Error: Energy has increased")
+                return energy, controller.ERROR
+            if new_energy.value == energy.value:
+                logger.warning("Warning: Energy has not changed. Assuming convergence...")
+                return new_energy, controller.CONVERGED
+            energy = new_energy
+            status = self._controller.check(energy)
+            if status != controller.CONTINUE:
+                return energy, status
+
+    def reset(self):
+        pass
+
+    def get_descent_direction(self, energy, old_value=None):
+        raise NotImplementedError
+
+
+class SteepestDescent(DescentMinimizer):
+    def get_descent_direction(self, energy, _=None):
+        return -energy.gradient
+
+
+class NewtonCG(DescentMinimizer):
+    def __init__(self, controller, napprox=0, line_searcher=None, name=None, nreset=20,
+                 max_cg_iterations=200, energy_reduction_factor=0.1, enable_logging=False):
+        if line_searcher is None:
+            line_searcher = LineSearch(preferred_initial_step_size=1.)
+        super().__init__(controller=controller, line_searcher=line_searcher)
+        self._napprox = napprox
+        self._name = name
+        self._nreset = nreset
+        self._max_cg_iterations = max_cg_iterations
+        self._alpha = energy_reduction_factor
+        from .iteration_controllers import EnergyHistory
+        self._history = EnergyHistory() if enable_logging else None
+
+    def get_descent_direction(self, energy, old_value=None):
+        if old_value is None:
+            ic = GradientNormController(iteration_limit=5)
+        else:
+            ediff = self._alpha * (old_value - energy.value)
+            ic = AbsDeltaEnergyController(ediff, iteration_limit=self._max_cg_iterations, name=self._name)
+        if self._history is not None:
+            ic.enable_logging()
+        e = QuadraticEnergy(0 * energy.position, energy.metric, energy.gradient)
+        e, conv = ConjugateGradient(ic, nreset=self._nreset)(e, None)
+        if self._history is not None:
+            self._history += ic.history
+        if conv == ic.ERROR:
+            raise ValueError("Cannot find descent direction")
+        return -e.position
+
+    @property
+    def inversion_history(self):
+        return self._history

@@ -1,0 +1,177 @@
+"""Fused conjugate gradient for sampling metrics  M = shift * 1 + J^T W J.
+
+Same algorithm as ConjugateGradient.__call__ (src/minimization/
+conjugate_gradient.py:48-126), on packed device vectors:
+
+  q = M d                       fused model pipeline (core.metric_flat)
+  curv = d.q                    nft_dot            -> sc[CURV]
+  x -= a d ; r -= a q           nft_cg_update      -> sc[GAMMA]=r.r, x.r, x.b
+  (every nreset-th step: r = M x - b exactly, nft_cg_residual)
+  host: guards + controller on (curv, gamma, value = (x.r - x.b)/2)
+  d = max(0, g/g_prev) d + r    nft_cg_direction
+
+All scalars stay on the device; one 16-double D2H read per iteration feeds the
+host-side controller, exactly as the reference decides on host floats.
+"""
+import math
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..logger import logger
+from ..packing import PackedLayout
+
+
+def fusable_metric(A):
+    """(core, W, shift) if A = shift*1 + Sandwich(fused core, W), else None."""
+    from ..operators.sandwich_operator import SandwichOperator
+    from ..operators.scaling_operator import ScalingOperator
+    from ..operators.sum_operator import SumOperator
+    if isinstance(A, SandwichOperator):
+        if A.fused is None:
+            return None
+        return A.fused[0], A.fused[1], 0.0
+    if isinstance(A, SumOperator):
+        sand, shift = None, 0.0
+        for op, neg in zip(A._ops, A._neg):
+            if isinstance(op, SandwichOperator) and op.fused is not None and not neg and sand is None:
+                sand = op
+            elif isinstance(op, ScalingOperator) and complex(op._factor).imag == 0:
+                shift += (-1 if neg else 1) * complex(op._factor).real
+            else:
+                return None
+        if sand is None:
+            return None
+        return sand.fused[0], sand.fused[1], shift
+    return None
+
+
+class _State:
+    """Energy-like view of the fused iterate for IterationControllers."""
+
+    def __init__(self, value, gnorm, lazy):
+        self.value = value
+        self.gradient_norm = gnorm
+        self._lazy = lazy
+
+    @property
+    def position(self):
+        return self._lazy()[0]
+
+    @property
+    def gradient(self):
+        return self._lazy()[1]
+
+
+def fused_cg_or_none(energy, controller, nreset):
+    from .quadratic_energy import QuadraticEnergy
+    if type(energy) is not QuadraticEnergy:
+        return None
+    spec = fusable_metric(energy.metric)
+    if spec is None:
+        return None
+    core, W, shift = spec
+    if energy.position.domain is not core.domain or not core.device.type == "cuda":
+        return None
+    return FusedCG(core, W, shift, controller, nreset).run(energy)
+
+
+class FusedCG:
+    def __init__(self, core, W, shift, controller, nreset=20):
+        self.core, self.W, self.shift = core, W, float(shift)
+        self.controller = controller
+        self.nreset = nreset
+        self.layout = core.layout
+        self.niter = 0
+
+    def _energy(self, A, b, x, r):
+        from .quadratic_energy import QuadraticEnergy
+        lay = self.layout
+        return QuadraticEnergy(lay.unpack(x), A, b, _grad=lay.unpack(r))
+
+    def run(self, energy):
+        ctl = self.controller
+        status = ctl.start(energy)
+        if status != ctl.CONTINUE:
+            return energy, status
+        lay, core = self.layout, self.core
+        A, b_mf = energy.metric, energy._b
+        x = lay.pack(energy.position)
+        r = lay.pack(energy.gradient)
+        b = lay.pack(b_mf) if b_mf is not None else None
+        d = r.clone()
+        q = lay.empty()
+        ax = None
+        n = lay.size
+        sc = torch.zeros(_native.CG_NSCALARS, dtype=torch.float64, device=x.device)
+        host = torch.zeros(_native.CG_NSCALARS, dtype=torch.float64).pin_memory()
+        lib = _native.load()
+        ws = _native.workspace(lib.nft_reduce_workspace(n), x.device, "cg")
+        dt = _native.dtype_code(x.dtype)
+        sp = _native.stream_ptr()
+        P = _native.ptr
+
+        def chk(st):
+            _native._check(st)
+
+        chk(lib.nft_dot(P(r), P(r), n, dt, P(sc[_native.CG_GAMMA:]), P(ws), sp))
+        gamma = sc[_native.CG_GAMMA].item()
+        if np.isnan(gamma):
+            logger.error("Error: ConjugateGradient: previous_gamma==NaN")
+            return energy, ctl.ERROR
+        if gamma == 0:
+            return energy, ctl.CONVERGED
+
+        ii = 0
+        while True:
+            core.metric_flat(d, q, self.W, self.shift)
+            chk(lib.nft_dot(P(d), P(q), n, dt, P(sc[_native.CG_CURV:]), P(ws), sp))
+            self.niter += 1
+            ii += 1
+            if ii < self.nreset:
+                chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, P(sc), P(ws), sp))
+            else:
+                gp = sc[_native.CG_GAMMA].clone()
+                chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, P(sc), P(ws), sp))
+                if ax is None:
+                    ax = lay.empty()
+                core.metric_flat(x, ax, self.W, self.shift)
+                flag = sc[_native.CG_FLAG].clone()
+                chk(lib.nft_cg_residual(P(r), P(ax), P(x), P(b), n, dt, P(sc), P(ws), sp))
+                sc[_native.CG_GPREV] = gp
+                sc[_native.CG_FLAG] = flag
+                ii = 0
+            host.copy_(sc, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            h = host.numpy()
+            if h[_native.CG_FLAG] != 0.0:
+                curv = h[_native.CG_CURV]
+                if np.isnan(curv):
+                    logger.error("Error: ConjugateGradient: curv==NaN")
+                elif curv == 0.:
+                    logger.error("Error: ConjugateGradient: curv==0.")
+                else:
+                    logger.error("Error: ConjugateGradient: alpha<0.")
+                return self._energy(A, b_mf, x, r), ctl.ERROR
+            gamma = float(h[_native.CG_GAMMA])
+            if np.isnan(gamma):
+                logger.error("Error: ConjugateGradient: gamma==NaN")
+                return self._energy(A, b_mf, x, r), ctl.ERROR
+            if gamma < 0:
+                logger.error("Positive definiteness of preconditioner violated!")
+                return self._energy(A, b_mf, x, r), ctl.ERROR
+            if gamma == 0:
+                return self._energy(A, b_mf, x, r), ctl.CONVERGED
+            cache = {}
+
+            def lazy():
+                if "v" not in cache:
+                    cache["v"] = (lay.unpack(x), lay.unpack(r))
+                return cache["v"]
+            value = 0.5 * (float(h[_native.CG_XR]) - float(h[_native.CG_XB]))
+            state = _State(value, math.sqrt(gamma), lazy)
+            status = ctl.check(state)
+            if status != ctl.CONTINUE:
+                return self._energy(A, b_mf, x, r), status
+            chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), sp))

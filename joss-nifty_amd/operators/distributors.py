@@ -1,0 +1,111 @@
+"""DOFDistributor / PowerDistributor (src/operators/distributors.py:28-157).
+
+Forward (gather) and adjoint (deterministic segmented scatter, bit-identical
+to np.bincount) run as native kernels (csrc/nft_cf.hip)."""
+import numpy as np
+import torch
+
+from .. import _native
+from ..domain_tuple import DomainTuple
+from ..domains import DOFSpace, PowerSpace
+from ..field import Field
+from ..utilities import infer_space
+from .linear_operator import LinearOperator
+
+
+class BinIndex:
+    """Device-resident bin index: pindex (int32) plus the stable bin->pixel
+    permutation and CSR offsets for the adjoint.  Built once on the host."""
+    _cache = {}
+
+    def __init__(self, dofdex, nbin, device):
+        dofdex = np.asarray(dofdex).ravel()
+        self.npix = dofdex.size
+        self.nbin = int(nbin)
+        perm = np.argsort(dofdex, kind="stable")
+        cnt = np.bincount(dofdex, minlength=self.nbin)
+        offs = np.zeros(self.nbin + 1, dtype=np.int64)
+        np.cumsum(cnt, out=offs[1:])
+        if self.npix >= 2 ** 31:
+            raise ValueError("grids with >= 2^31 pixels are not supported")
+        self.pindex = torch.from_numpy(dofdex.astype(np.int32)).to(device)
+        self.perm = torch.from_numpy(perm.astype(np.int32)).to(device)
+        self.offsets = torch.from_numpy(offs.astype(np.int32)).to(device)
+        self.counts = cnt
+
+    @classmethod
+    def get(cls, dofdex, nbin, device):
+        key = (id(dofdex), int(nbin), str(device))
+        obj = cls._cache.get(key)
+        if obj is None or obj._ref is not dofdex:
+            obj = cls(dofdex, nbin, device)
+            obj._ref = dofdex
+            cls._cache[key] = obj
+        return obj
+
+
+class DOFDistributor(LinearOperator):
+    def __init__(self, dofdex, target=None, space=None):
+        if target is None:
+            target = dofdex.domain
+        self._target = DomainTuple.make(target)
+        space = infer_space(self._target, space)
+        partner = self._target[space]
+        if not isinstance(dofdex, Field):
+            raise TypeError("dofdex must be a Field")
+        ldat = dofdex.val_np()
+        nbin = 0 if ldat.size == 0 else ldat.max()
+        nbin = int(nbin) + 1
+        if partner.scalar_dvol is not None:
+            wgt = np.bincount(ldat.ravel(), minlength=nbin) * partner.scalar_dvol
+        else:
+            wgt = np.bincount(ldat.ravel(), minlength=nbin, weights=np.broadcast_to(partner.dvol, ldat.shape).ravel())
+        wgt = wgt.astype(np.float64, copy=False)
+        if (wgt == 0).any():
+            raise ValueError("empty bins detected")
+        self._init2(ldat, space, DOFSpace(wgt))
+
+    def _init2(self, dofdex, space, other_space):
+        from .. import config
+        self._space = space
+        dom = list(self._target)
+        dom[self._space] = other_space
+        self._domain = DomainTuple.make(dom)
+        self._capability = self.TIMES | self.ADJOINT_TIMES
+        firstaxis = self._target.axes[self._space][0]
+        lastaxis = self._target.axes[self._space][-1]
+        arrshape = self._target.shape
+        self._pre = int(np.prod(arrshape[0:firstaxis], dtype=np.int64))
+        self._post = int(np.prod(arrshape[lastaxis + 1:], dtype=np.int64))
+        self._nbin = self._domain[self._space].shape[0]
+        self._dofdex_np = dofdex
+        self._bins = BinIndex.get(dofdex, self._nbin, config.device())
+
+    def apply(self, x, mode):
+        self._check_input(x, mode)
+        v = x.val.contiguous()
+        b = self._bins
+        if mode == self.TIMES:
+            out = torch.empty(self._target.shape, dtype=v.dtype, device=v.device)
+            _native.bin_gather(v, b.pindex, out, self._pre, b.npix, self._nbin, self._post)
+            return Field(self._target, out)
+        out = torch.empty(self._domain.shape, dtype=v.dtype, device=v.device)
+        _native.bin_scatter(v, b.perm, b.offsets, out, self._pre, b.npix, self._nbin, self._post)
+        return Field(self._domain, out)
+
+
+class PowerDistributor(DOFDistributor):
+    def __init__(self, target, power_space=None, space=None):
+        self._target = DomainTuple.make(target)
+        self._space = infer_space(self._target, space)
+        hspace = self._target[self._space]
+        if not hspace.harmonic:
+            raise ValueError("Operator requires harmonic target space")
+        if power_space is None:
+            power_space = PowerSpace(hspace)
+        else:
+            if not isinstance(power_space, PowerSpace):
+                raise TypeError("power_space argument must be a PowerSpace")
+            if power_space.harmonic_partner != hspace:
+                raise ValueError("power_space does not match its partner")
+        self._init2(power_space.pindex, self._space, power_space)

@@ -1,0 +1,212 @@
+"""Utilities (subset of src/utilities.py on the sampling path) and the
+process-group adapter used for sample sharding.
+
+Distribution model: one process per GPU, samples sharded by
+``shareRange`` (src/utilities.py:268-292), a single collective for the KL
+value/gradient mean.  ``TorchComm`` exposes the slice of the mpi4py
+communicator API the reference calls (Get_rank/Get_size/allgather/bcast/
+Barrier) on top of ``torch.distributed`` (backend "nccl" = RCCL over xGMI on
+the GPU box, "gloo" on CPU).
+"""
+import numpy as np
+import torch
+
+
+def myassert(val):
+    if not val:
+        raise AssertionError
+
+
+def shareRange(nwork, nshares, myshare):
+    """Fair contiguous split of `nwork` items (src/utilities.py:268-292)."""
+    nbase = nwork // nshares
+    additional = nwork % nshares
+    lo = myshare * nbase + min(myshare, additional)
+    hi = lo + nbase + int(myshare < additional)
+    return lo, hi
+
+
+def get_MPI_params_from_comm(comm):
+    if comm is None:
+        return 1, 0, True
+    size = comm.Get_size()
+    rank = comm.Get_rank()
+    return size, rank, rank == 0
+
+
+class TorchComm:
+    """mpi4py-like communicator over an initialised torch.distributed group."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self._dist = dist
+        self._group = group
+
+    def Get_rank(self):
+        return self._dist.get_rank(self._group)
+
+    def Get_size(self):
+        return self._dist.get_world_size(self._group)
+
+    def allgather(self, obj):
+        out = [None] * self.Get_size()
+        self._dist.all_gather_object(out, obj, group=self._group)
+        return out
+
+    def bcast(self, obj, root=0):
+        lst = [obj]
+        self._dist.broadcast_object_list(lst, src=root, group=self._group)
+        return lst[0]
+
+    def Barrier(self):
+        self._dist.barrier(group=self._group)
+
+    @property
+    def backend(self):
+        return self._dist.get_backend(self._group)
+
+    def allreduce_tensor_(self, t):
+        """In-place SUM all-reduce of a tensor (one RCCL call on GPU)."""
+        self._dist.all_reduce(t, group=self._group)
+        return t
+
+
+def pairwise_sum(vals):
+    """The fixed pairwise summation order of allreduce_sum
+    (src/utilities.py:374-387) for a local list."""
+    vals = list(vals)
+    n = len(vals)
+    step = 1
+    while step < n:
+        for j in range(0, n, 2 * step):
+            if j + step < n:
+                vals[j] = vals[j] + vals[j + step]
+                vals[j + step] = None
+        step *= 2
+    return vals[0]
+
+
+def allreduce_sum(obj, comm):
+    """Deterministic task-count-independent sum of a list of objects held by
+    the ranks (src/utilities.py:331-390).  Serial: the pairwise tree.
+    Distributed: every rank gathers all per-sample objects and evaluates the
+    same tree, so the result is bit-identical for any number of ranks."""
+    vals = list(obj)
+    if comm is None:
+        return pairwise_sum(vals)
+    allvals = comm.allgather(vals)
+    flat = [v for lst in allvals for v in lst]
+    return pairwise_sum(flat)
+
+
+def check_MPI_equality(obj, comm, hash_=False):
+    if comm is None:
+        return
+    import pickle
+    h = hash(pickle.dumps(obj)) if hash_ else obj
+    lst = comm.allgather(h)
+    if not all(x == lst[0] for x in lst):
+        raise RuntimeError("MPI tasks are not in sync")
+
+
+def check_MPI_synced_random_state(comm):
+    from .random import getState
+    if comm is None:
+        return
+    check_MPI_equality(getState(), comm)
+
+
+def lognormal_moments(mean, sigma, N=0):
+    """(src/utilities.py:405-418)"""
+    mean, sigma = (value_reshaper(p, N) for p in (mean, sigma))
+    if not np.all(mean > 0):
+        raise ValueError(f"mean must be greater 0; got {mean!r}")
+    if not np.all(sigma > 0):
+        raise ValueError(f"sig must be greater 0; got {sigma!r}")
+    logsigma = np.sqrt(np.log1p((sigma / mean) ** 2))
+    logmean = np.log(mean) - logsigma ** 2 / 2
+    return logmean, logsigma
+
+
+def value_reshaper(x, N):
+    x = np.asarray(x, dtype=np.float64)
+    if x.shape in [(), (1,)]:
+        return np.full(N, x) if N != 0 else x.reshape(())
+    if x.shape == (N,):
+        return x
+    raise TypeError("x and N are incompatible")
+
+
+def infer_space(domain, space):
+    if space is None:
+        if len(domain) != 1:
+            raise ValueError("'space' index must be given for objects based on DomainTuples "
+                             "containing more than one domain")
+        space = 0
+    space = int(space)
+    if space < 0 or space >= len(domain):
+        raise ValueError("space index out of range")
+    return space
+
+
+def parse_spaces(spaces, nspc):
+    nspc = int(nspc)
+    if spaces is None:
+        return tuple(range(nspc))
+    if np.isscalar(spaces):
+        spaces = (spaces,)
+    spaces = tuple(int(i) for i in spaces)
+    res = tuple(i if i >= 0 else i + nspc for i in spaces)
+    if any(i < 0 or i >= nspc for i in res):
+        raise ValueError("space index out of range")
+    return res
+
+
+def check_object_identity(obj1, obj2):
+    if obj1 is not obj2:
+        raise ValueError(f"Mismatch:\n{obj1}\n{obj2}")
+
+
+def check_dtype_or_none(obj, domain=None):
+    pass
+
+
+def iscomplextype(dtype):
+    if isinstance(dtype, torch.dtype):
+        return dtype.is_complex
+    return np.issubdtype(np.dtype(dtype), np.complexfloating)
+
+
+def torch_dtype(dtype):
+    """numpy-ish dtype -> torch dtype."""
+    if isinstance(dtype, torch.dtype):
+        return dtype
+    if dtype is float or dtype is None:
+        return torch.float64
+    if dtype is complex:
+        return torch.complex128
+    dt = np.dtype(dtype)
+    return {np.dtype(np.float64): torch.float64, np.dtype(np.float32): torch.float32,
+            np.dtype(np.complex128): torch.complex128, np.dtype(np.complex64): torch.complex64,
+            np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32,
+            np.dtype(np.bool_): torch.bool}[dt]
+
+
+def numpy_dtype(tdtype):
+    return {torch.float64: np.float64, torch.float32: np.float32, torch.complex128: np.complex128,
+            torch.complex64: np.complex64, torch.int64: np.int64, torch.int32: np.int32,
+            torch.bool: np.bool_}[tdtype]
+
+
+def indent(inp):
+    return "\n".join((("  " + s).rstrip() for s in inp.splitlines()))
+
+
+class frozendict(dict):
+    def __setitem__(self, *a):
+        raise TypeError("frozendict is immutable")
+
+    def __hash__(self):
+        return hash(tuple(sorted(self.items())))

@@ -201,7 +201,8 @@ def gen_draw_samples():
     and a small geoVI draw (kl_energies.py:90-158)."""
     cf, lh, data, mock, pos = _gaussian_problem(128)
     d = {}
-    for name, ic in (("fixed", ift.GradientNormController(iteration_limit=20)),
+    for name, ic in (("short", ift.GradientNormController(iteration_limit=8)),
+                     ("fixed", ift.GradientNormController(iteration_limit=20)),
                      ("absdelta", ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=100))):
         ic.enable_logging()
         H = ift.StandardHamiltonian(lh, ic)
@@ -231,6 +232,28 @@ def gen_draw_samples():
         for k, v in _flat(r).items():
             dd[f"r{i}_" + k] = v
     _save("geovi32.npz", dd)
+
+    # short, rounding-stable variant: 6 linear CG steps, one Newton step with
+    # its first-step inner CG (GradientNormController(iteration_limit=5))
+    dd = {"data": data.val}
+    for k, v in _flat(pos).items():
+        dd["pos_" + k] = v
+    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=6))
+    mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=1))
+    ift.random.push_sseq_from_seed(31)
+    sl = ift.minimization.kl_energies.draw_samples(pos, H, mini, 1, True)
+    ift.random.pop_sseq()
+    for i, r in enumerate(sl._r):
+        for k, v in _flat(r).items():
+            dd[f"r{i}_" + k] = v
+    # the MGVI (linear) residuals of the same draw, for the linear stage alone
+    ift.random.push_sseq_from_seed(31)
+    sl = ift.minimization.kl_energies.draw_samples(pos, H, None, 1, True)
+    ift.random.pop_sseq()
+    for i, r in enumerate(sl._r):
+        for k, v in _flat(r).items():
+            dd[f"lin{i}_" + k] = v
+    _save("geovi32_short.npz", dd)
 
 
 def gen_poisson():
@@ -262,7 +285,7 @@ def gen_poisson():
     for k, val in _flat(met(v)).items():
         d["mv_" + k] = val
     d["energy"] = np.array(lh(pos).val)
-    ic = ift.GradientNormController(iteration_limit=10)
+    ic = ift.GradientNormController(iteration_limit=6)
     H = ift.StandardHamiltonian(lh, ic)
     ift.random.push_sseq_from_seed(3)
     sl = ift.minimization.kl_energies.draw_samples(pos, H, None, 1, True)
