@@ -261,7 +261,7 @@ class CFJacobian(LinearOperator):
     def sandwich_apply(self, x, W):
         """J^T W J x for a latent MultiField x, W a grid tensor."""
         s = self._times_t({k: x[k].val for k in x.keys()})
-        res = self._adjoint_t(s * W)
+        res = self._adjoint_t(W(s) if callable(W) else s * W)
         return MultiField(self._domain, tuple(Field(self._domain[k], res[k].reshape(self._domain[k].shape))
                                               for k in self._domain.keys()))
 
@@ -270,7 +270,7 @@ class CFJacobian(LinearOperator):
         lay = self.layout
         dv = lay.views(d)
         s = self._times_t(dv)
-        res = self._adjoint_t(s * W)
+        res = self._adjoint_t(W(s) if callable(W) else s * W)
         qv = lay.views(q)
         for k in lay.keys:
             r = res[k].reshape(qv[k].shape)

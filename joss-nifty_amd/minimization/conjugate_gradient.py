@@ -14,6 +14,8 @@ from .minimizer import Minimizer
 
 
 class ConjugateGradient(Minimizer):
+    iterations_total = 0  # CG iterations run by all instances (benchmark bookkeeping)
+
     def __init__(self, controller, nreset=20, allow_fused=True):
         self._controller = controller
         self._nreset = nreset
@@ -59,6 +61,7 @@ class ConjugateGradient(Minimizer):
                 return energy, controller.ERROR
 
             ii += 1
+            ConjugateGradient.iterations_total += 1
             if ii < self._nreset:
                 r = r - q * alpha
                 energy = energy.at_with_grad(energy.position - alpha * d, r)

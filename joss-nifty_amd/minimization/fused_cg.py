@@ -21,6 +21,7 @@ import torch
 from .. import _native
 from ..logger import logger
 from ..packing import PackedLayout
+from .conjugate_gradient import ConjugateGradient
 
 
 def fusable_metric(A):
@@ -128,6 +129,7 @@ class FusedCG:
             core.metric_flat(d, q, self.W, self.shift)
             chk(lib.nft_dot(P(d), P(q), n, dt, P(sc[_native.CG_CURV:]), P(ws), sp))
             self.niter += 1
+            ConjugateGradient.iterations_total += 1
             ii += 1
             if ii < self.nreset:
                 chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, P(sc), P(ws), sp))

@@ -77,6 +77,28 @@ class SandwichOperator(EndomorphicOperator):
             return
         w = _pointwise_weight(ops[:cores[0]] + right, self._cheese)
         if w is None:
+            # non-pointwise middle (e.g. a line-of-sight response): the model
+            # Jacobian halves stay fused, the middle M^T C M runs through the
+            # generic operator tree on J's target
+            if not all(isinstance(op, ScalingOperator) and complex(op._factor).imag == 0 for op in right):
+                return
+            fct = 1.
+            for op in right:
+                fct *= complex(op._factor).real ** 2
+            left = ops[:cores[0]]
+            mid = ChainOperator.make(left) if len(left) > 0 else None
+            cheese = self._cheese
+            tgt = core.target
+
+            def middle(s):
+                from ..field import Field
+                f = Field(tgt, s)
+                if mid is None:
+                    r = cheese(f)
+                else:
+                    r = mid.adjoint_times(cheese(mid(f)))
+                return r.val * fct if fct != 1. else r.val
+            self._fused = (core, middle)
             return
         if not torch.is_tensor(w):
             w = torch.full(core.target.shape, float(w), dtype=torch.float64, device=core.device)

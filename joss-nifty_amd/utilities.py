@@ -88,17 +88,60 @@ def pairwise_sum(vals):
     return vals[0]
 
 
-def allreduce_sum(obj, comm):
-    """Deterministic task-count-independent sum of a list of objects held by
-    the ranks (src/utilities.py:331-390).  Serial: the pairwise tree.
-    Distributed: every rank gathers all per-sample objects and evaluates the
-    same tree, so the result is bit-identical for any number of ranks."""
+DETERMINISTIC_ALLREDUCE = False
+
+
+def _flatten(obj):
+    """object -> (list of tensors, rebuild function) for Field/MultiField/scalars"""
+    from .field import Field
+    from .multi_field import MultiField
+    if isinstance(obj, MultiField):
+        return [f.val for f in obj.values()], lambda ts: MultiField(
+            obj.domain, tuple(Field(d, t) for d, t in zip(obj.domain.values(), ts)))
+    if isinstance(obj, Field):
+        return [obj.val], lambda ts: Field(obj.domain, ts[0])
+    if isinstance(obj, (float, int, np.floating)):
+        return [torch.tensor(float(obj), dtype=torch.float64)], lambda ts: float(ts[0].item())
+    if isinstance(obj, torch.Tensor):
+        return [obj], lambda ts: ts[0]
+    raise TypeError(f"cannot all-reduce {type(obj)}")
+
+
+def allreduce_sum(obj, comm, deterministic=None):
+    """Sum of a list of per-sample objects held by the ranks
+    (src/utilities.py:331-390).
+
+    Serial: the reference's pairwise tree.  Distributed, default: each rank
+    sums its samples in pairwise order, then ONE all-reduce over a packed
+    fp64 buffer (RCCL over xGMI on the GPU box).  ``deterministic=True``
+    (or DETERMINISTIC_ALLREDUCE): every rank gathers all per-sample objects
+    and evaluates the reference's global tree, bit-identical for any number
+    of ranks (test_mpi/test_kl.py semantics)."""
     vals = list(obj)
     if comm is None:
         return pairwise_sum(vals)
-    allvals = comm.allgather(vals)
-    flat = [v for lst in allvals for v in lst]
-    return pairwise_sum(flat)
+    if deterministic is None:
+        deterministic = DETERMINISTIC_ALLREDUCE
+    if deterministic:
+        allvals = comm.allgather(vals)
+        flat = [v for lst in allvals for v in lst]
+        return pairwise_sum(flat)
+    if len(vals) == 0:
+        raise RuntimeError("every rank needs at least one sample for the fast all-reduce")
+    local = pairwise_sum(vals)
+    ts, rebuild = _flatten(local)
+    dev = ts[0].device
+    if getattr(comm, "backend", "gloo") == "nccl" and dev.type != "cuda":
+        from . import config
+        dev = config.device()
+    buf = torch.cat([t.reshape(-1).to(dev, torch.float64) for t in ts])
+    comm.allreduce_tensor_(buf)
+    out, off = [], 0
+    for t in ts:
+        n = t.numel()
+        out.append(buf[off:off + n].reshape(t.shape).to(t.device, t.dtype))
+        off += n
+    return rebuild(out)
 
 
 def check_MPI_equality(obj, comm, hash_=False):

@@ -46,12 +46,41 @@ class PointwiseLikelihood:
         raise ValueError(self.kind)
 
 
+class LOSLikelihood:
+    """Tomography likelihood of config C3: d = R sigmoid(s) + n, n ~ N(0, var)
+    (getting_started_3.py): the sampling metric's middle is
+    diag(sig') R^T N^-1 R diag(sig'), sig = 0.5 + 0.5 tanh (pointwise.py:148).
+    R is given as COO arrays (rows, cols, float32 weights), applied with
+    scipy.sparse as src/library/los_response.py:226-233 does."""
+
+    def __init__(self, cf, rows, cols, wgt, nlos, noise_var):
+        import scipy.sparse
+        self.cf = cf
+        self.R = scipy.sparse.coo_matrix((wgt, (rows, cols)), shape=(nlos, int(np.prod(cf.shape)))).tocsr()
+        self.noise_var = noise_var
+
+    def middle(self, lat0):
+        s0 = self.cf.value(lat0)
+        t = np.tanh(s0)
+        dsig = 0.5 * (1. - t * t)
+        R, iv = self.R, 1. / self.noise_var
+
+        def apply(v):
+            y = R @ (dsig * v).ravel()
+            return dsig * (R.T @ (iv * y)).reshape(v.shape)
+        return apply
+
+
 class SamplingMetric:
+    """x -> x + J^T W J x; W is a pointwise weight array or a callable middle."""
+
     def __init__(self, cf, lat0, W):
         self.cf, self.lat0, self.W = cf, lat0, W
 
     def __call__(self, x):
-        g = self.cf.vjp(self.lat0, self.W * self.cf.jvp(self.lat0, x))
+        s = self.cf.jvp(self.lat0, x)
+        s = self.W(s) if callable(self.W) else self.W * s
+        g = self.cf.vjp(self.lat0, s)
         return {k: x[k] + np.reshape(g[k], np.shape(x[k])) for k in _keys(x)}
 
 
