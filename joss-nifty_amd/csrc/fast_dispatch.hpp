@@ -1,0 +1,104 @@
+// Host-side dispatch of the engine-v2 kernels: thread-count choice per
+// length and tiling, launch, and the four-step split of long strided axes.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "fast_passes.hpp"
+#include "nft_api_internal.hpp"
+
+namespace nft {
+namespace fast {
+
+// threads per workgroup for a pass of length N
+constexpr int nt_rows(int N) { return N <= 2048 ? 256 : (N == 4096 ? 512 : 1024); }
+// strided: aim for >= 16 adjacent columns per tile
+constexpr int nt_strided(int N) { return N <= 128 ? 256 : (N == 256 ? 512 : 1024); }
+
+inline bool is_pow2(long long n) { return n > 0 && (n & (n - 1)) == 0; }
+
+inline bool rows_supported(int N) { return is_pow2(N) && N >= 8 && N <= 8192; }
+inline bool strided_supported(int N) { return is_pow2(N) && N >= 8 && N <= 512; }
+// lengths handled as a four-step pair of strided passes
+inline bool fourstep_supported(int N) { return is_pow2(N) && N >= 1024 && N <= 16384; }
+inline void fourstep_split(int N, int& N1, int& N2) {
+  int p = 0;
+  while ((1 << p) < N) ++p;
+  N1 = 1 << (p / 2);
+  N2 = N / N1;
+}
+
+template <typename T, int N, int NT, int KIND, bool ROWS>
+static int launch_one(const FastArgs<T>& a, hipStream_t s) {
+  constexpr int L = NT * VPT / N;
+  constexpr int PITCH = ROWS ? N : N + 1;
+  size_t lds = (size_t)L * PITCH * sizeof(cplx_t<T>) + (KIND == K_UNPACK ? (size_t)L * sizeof(UnpackLine) : 0);
+  long long ntiles;
+  if (ROWS) {
+    long long nl = (KIND == K_R2C || KIND == K_H1D) ? (a.Ireal + 1) / 2 : a.g.O;
+    ntiles = (nl + L - 1) / L;
+  } else {
+    ntiles = a.g.O * a.g.M * ((a.g.I + L - 1) / L);
+  }
+  if (ntiles <= 0) return NFT_OK;
+  if (ntiles > 0x7fffffffLL) {
+    set_last_error("too many tiles");
+    return NFT_ERR_UNSUPPORTED;
+  }
+  if (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS>), dim3((unsigned)ntiles), dim3(NT), lds, s, a);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+template <typename T, int KIND, bool ROWS>
+static int launch_n(int N, const FastArgs<T>& a, hipStream_t s) {
+#define NFT_CASE(n)                                                                   \
+  case n:                                                                             \
+    return launch_one<T, n, (ROWS ? nt_rows(n) : nt_strided(n)), KIND, ROWS>(a, s);
+  if (ROWS) {
+    switch (N) {
+      NFT_CASE(8) NFT_CASE(16) NFT_CASE(32) NFT_CASE(64) NFT_CASE(128) NFT_CASE(256) NFT_CASE(512)
+      NFT_CASE(1024) NFT_CASE(2048) NFT_CASE(4096) NFT_CASE(8192)
+    }
+  } else {
+    switch (N) {
+      NFT_CASE(8) NFT_CASE(16) NFT_CASE(32) NFT_CASE(64) NFT_CASE(128) NFT_CASE(256) NFT_CASE(512)
+    }
+  }
+#undef NFT_CASE
+  set_last_error("engine v2: unsupported length %d", N);
+  return NFT_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+static int launch(int kind, bool rows, int N, FastArgs<T>& a, hipStream_t s) {
+  const void* tw = nullptr;
+  int st = get_twiddles(N, sizeof(T) == 8 ? 0 : 1, &tw);
+  if (st != NFT_OK) return st;
+  a.tw = tw;
+  if (rows) {
+    switch (kind) {
+      case K_C2C: return launch_n<T, K_C2C, true>(N, a, s);
+      case K_R2C: return launch_n<T, K_R2C, true>(N, a, s);
+      case K_H1D: return launch_n<T, K_H1D, true>(N, a, s);
+      case K_UNPACK: return launch_n<T, K_UNPACK, true>(N, a, s);
+    }
+  } else {
+    switch (kind) {
+      case K_C2C: return launch_n<T, K_C2C, false>(N, a, s);
+      case K_UNPACK: return launch_n<T, K_UNPACK, false>(N, a, s);
+    }
+  }
+  set_last_error("engine v2: unsupported kind");
+  return NFT_ERR_UNSUPPORTED;
+}
+
+}  // namespace fast
+}  // namespace nft

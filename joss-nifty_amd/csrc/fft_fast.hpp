@@ -1,0 +1,117 @@
+// Compile-time power-of-two FFT passes for gfx950 (engine v2).
+//
+// For N = 2^p the radix plan is fixed at compile time (one radix-2 or -4
+// stage first if p % 3 != 0, then radix-8 stages), every thread owns exactly
+// VPT = 8 complex values per stage (L = NT*8/N lines per workgroup), and all
+// index arithmetic is shifts and masks.  This keeps the register budget low
+// (two or more waves per SIMD for fp64) and removes the runtime radix switch
+// of the generic engine (fft_core.hpp), which stays in use for other lengths.
+//
+// Lines are addressed (o, m, i) -> o*so + m*sm + i*si + x*sn, with separate
+// input and output strides.  The m dimension expresses the two sub-passes of
+// a four-step decomposition N = N1*N2 of a strided axis:
+//   A: lines (n2, c), elements rows n2 + N2*j (j < N1), FFT_N1, then the
+//      twiddle W_N^(n2*k1), written back in place;
+//   B: lines (k1, c), elements rows N2*k1 + n2 (n2 < N2), FFT_N2, output
+//      element k2 lands on row k1 + N1*k2.
+// Both sub-passes tile L adjacent columns (i) with L*16 B >= 512 B row
+// segments, so a 2048-point fp64 column transform streams at full width
+// instead of holding one 32 KB column per workgroup.
+#pragma once
+#include "fft_core.hpp"
+
+namespace nft {
+namespace fast {
+
+constexpr int VPT = 8;
+
+constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n / 2); }
+// radix of the stage that starts at span NS (product of previous radices)
+constexpr int radix_at(int N, int NS) {
+  return (NS == 1 && ilog2(N) % 3 == 1) ? 2 : ((NS == 1 && ilog2(N) % 3 == 2) ? 4 : 8);
+}
+
+struct Lines {
+  long long O, M, I;                   // line grid
+  long long in_so, in_sm, in_si, in_sn;
+  long long out_so, out_sm, out_si, out_sn;
+};
+
+// -------------------------------------------------------------- one stage
+template <typename T, int N, int NT, int L, int PITCH, int R, int NS>
+__device__ __forceinline__ void stage(cplx_t<T>* lds, const cplx_t<T>* __restrict__ tw, int tid) {
+  using C = cplx_t<T>;
+  constexpr int NBL = N / R;
+  constexpr int NBF = L * NBL;
+  constexpr int BPT = (NBF + NT - 1) / NT;
+  constexpr int SH_NBL = ilog2(NBL);
+  constexpr int TSTRIDE = N / (NS * R);
+  C v[BPT][R];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int b = tid + i * NT;
+    if (NBF % NT == 0 || b < NBF) {
+      const int line = b >> SH_NBL;
+      const int j = b & (NBL - 1);
+      const C* src = lds + line * PITCH + j;
+#pragma unroll
+      for (int t = 0; t < R; ++t) v[i][t] = src[t * NBL];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int b = tid + i * NT;
+    if (NBF % NT == 0 || b < NBF) {
+      const int line = b >> SH_NBL;
+      const int j = b & (NBL - 1);
+      const int k = j & (NS - 1);
+      if constexpr (NS > 1) {
+        const int step = k * TSTRIDE;
+#pragma unroll
+        for (int t = 1; t < R; ++t) v[i][t] = cmul(v[i][t], tw[t * step]);
+      }
+      dftR<T, R>(v[i]);
+      C* dst = lds + line * PITCH + (j - k) * R + k;
+#pragma unroll
+      for (int t = 0; t < R; ++t) dst[t * NS] = v[i][t];
+    }
+  }
+  __syncthreads();
+}
+
+template <typename T, int N, int NT, int L, int PITCH, int NS>
+__device__ __forceinline__ void stages(cplx_t<T>* lds, const cplx_t<T>* __restrict__ tw, int tid) {
+  if constexpr (NS < N) {
+    constexpr int R = radix_at(N, NS);
+    stage<T, N, NT, L, PITCH, R, NS>(lds, tw, tid);
+    stages<T, N, NT, L, PITCH, NS * R>(lds, tw, tid);
+  }
+}
+
+// forward FFT of the L lines in LDS (caller synced after filling)
+template <typename T, int N, int NT, int L, int PITCH>
+__device__ __forceinline__ void fft(cplx_t<T>* lds, const cplx_t<T>* __restrict__ tw, int tid) {
+  stages<T, N, NT, L, PITCH, 1>(lds, tw, tid);
+}
+
+// -------------------------------------------------------------- tiles
+// rows tiling: line l of tile -> flat line index tile*L + l over (o) (M == I == 1)
+// strided tiling: tile -> (o, m, i0); line l -> i = i0 + l
+struct Tile {
+  long long o, m, i0;
+};
+
+template <int L>
+__device__ __forceinline__ Tile strided_tile(const Lines& g, long long t) {
+  const long long tilesI = (g.I + L - 1) / L;
+  Tile r;
+  long long om = t / tilesI;
+  r.i0 = (t - om * tilesI) * L;
+  r.o = om / g.M;
+  r.m = om - r.o * g.M;
+  return r;
+}
+
+}  // namespace fast
+}  // namespace nft

@@ -22,6 +22,7 @@
 #include <mutex>
 #include <vector>
 
+#include "fast_dispatch.hpp"
 #include "fft_passes.hpp"
 #include "nft_api_internal.hpp"
 
@@ -426,6 +427,173 @@ static int hartley_impl(const void* in, void* out, const Geo& g, const std::vect
   }
 }
 
+// ------------------------------------------------------------ engine v2 path
+constexpr int NFT_FALLBACK = 1;  // geometry not covered by engine v2
+
+static LineDesc make_desc(const Geo& g, const long long* cs, const std::vector<int>& ax, int axis, int h) {
+  LineDesc d;
+  memset(&d, 0, sizeof(d));
+  d.nout = axis;
+  d.nin = g.nd - axis - 1;
+  d.half = -1;
+  long long rs[MAXD];
+  rs[g.nd - 1] = 1;
+  for (int k = g.nd - 2; k >= 0; --k) rs[k] = rs[k + 1] * g.shape[k + 1];
+  int j = 0;
+  for (int k = 0; k < g.nd; ++k) {
+    if (k == axis) continue;
+    d.ext[j] = (int)cs[k];
+    d.rstride[j] = rs[k];
+    d.nreal[j] = (int)g.shape[k];
+    d.neg[j] = std::find(ax.begin(), ax.end(), k) != ax.end();
+    if (k == h) d.half = j;
+    ++j;
+  }
+  return d;
+}
+
+template <typename T>
+static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector<int>& ax, int sigma,
+                      double scale, void* ws, size_t ws_bytes, hipStream_t s) {
+  using namespace fast;
+  const int m = (int)ax.size();
+  const int last = g.nd - 1;
+  if (m == 0) return NFT_FALLBACK;
+  if (m == 1) {
+    const int N = (int)g.shape[ax[0]];
+    if (ax[0] != last || !rows_supported(N)) return NFT_FALLBACK;
+    FastArgs<T> a;
+    memset(&a, 0, sizeof(a));
+    a.in = in;
+    a.out = out;
+    a.g.O = prod(g.shape, 0, last);
+    a.g.M = a.g.I = 1;
+    a.g.in_so = a.g.out_so = N;
+    a.g.in_sn = a.g.out_sn = 1;
+    a.Ireal = a.g.O;
+    a.sigma = sigma;
+    a.scale = (T)scale;
+    return launch<T>(K_H1D, true, N, a, s);
+  }
+  const int h = ax[m - 1];
+  if (h != last || !rows_supported((int)g.shape[h])) return NFT_FALLBACK;
+  for (int k = 1; k < m - 1; ++k)
+    if (!strided_supported((int)g.shape[ax[k]])) return NFT_FALLBACK;
+  const int N0 = (int)g.shape[ax[0]];
+  if (!strided_supported(N0) && !fourstep_supported(N0)) return NFT_FALLBACK;
+  long long cs[MAXD];
+  half_shape(g, h, cs);
+  size_t need = (size_t)prod(cs, 0, g.nd) * sizeof(cplx_t<T>);
+  if (ws == nullptr || ws_bytes < need) {
+    set_last_error("hartley workspace too small (%zu < %zu)", ws_bytes, need);
+    return NFT_ERR_ARG;
+  }
+  int st;
+  {  // R2C rows along the last axis
+    const int N = (int)g.shape[h];
+    FastArgs<T> a;
+    memset(&a, 0, sizeof(a));
+    a.in = in;
+    a.out = ws;
+    a.g.O = prod(g.shape, 0, last);
+    a.g.M = a.g.I = 1;
+    a.g.in_so = N;
+    a.g.in_sn = 1;
+    a.g.out_so = cs[last];
+    a.g.out_sn = 1;
+    a.Ireal = a.g.O;
+    a.scale = (T)1;
+    if ((st = launch<T>(K_R2C, true, N, a, s)) != NFT_OK) return st;
+  }
+  for (int k = m - 2; k >= 1; --k) {  // middle axes, strided C2C in place
+    const int axis = ax[k];
+    const int N = (int)g.shape[axis];
+    const long long I = prod(cs, axis + 1, g.nd);
+    FastArgs<T> a;
+    memset(&a, 0, sizeof(a));
+    a.in = ws;
+    a.out = ws;
+    a.g.O = prod(cs, 0, axis);
+    a.g.M = 1;
+    a.g.I = I;
+    a.g.in_so = a.g.out_so = I * N;
+    a.g.in_si = a.g.out_si = 1;
+    a.g.in_sn = a.g.out_sn = I;
+    a.scale = (T)1;
+    if ((st = launch<T>(K_C2C, false, N, a, s)) != NFT_OK) return st;
+  }
+  {  // last pass along ax[0]: C2C + unpack to real (four-step for long axes)
+    const int axis = ax[0];
+    const int N = N0;
+    const long long I = prod(cs, axis + 1, g.nd);
+    const long long O = prod(cs, 0, axis);
+    const long long rrs = prod(g.shape, axis + 1, g.nd);
+    LineDesc desc = make_desc(g, cs, ax, axis, h);
+    if (strided_supported(N)) {
+      FastArgs<T> a;
+      memset(&a, 0, sizeof(a));
+      a.in = ws;
+      a.out = out;
+      a.g.O = O;
+      a.g.M = 1;
+      a.g.I = I;
+      a.g.in_so = I * N;
+      a.g.in_si = 1;
+      a.g.in_sn = I;
+      a.km = 0;
+      a.kx = 1;
+      a.Nfull = N;
+      a.rs = rrs;
+      a.sigma = sigma;
+      a.scale = (T)scale;
+      a.desc = desc;
+      return launch<T>(K_UNPACK, false, N, a, s);
+    }
+    int N1, N2;
+    fourstep_split(N, N1, N2);
+    const void* twN = nullptr;
+    if ((st = get_twiddles(N, sizeof(T) == 8 ? 0 : 1, &twN)) != NFT_OK) return st;
+    {  // A: length-N1 FFTs over rows n2 + N2*j, post-twiddle W_N^(n2*k1), in place
+      FastArgs<T> a;
+      memset(&a, 0, sizeof(a));
+      a.in = ws;
+      a.out = ws;
+      a.g.O = O;
+      a.g.M = N2;
+      a.g.I = I;
+      a.g.in_so = a.g.out_so = I * N;
+      a.g.in_sm = a.g.out_sm = I;
+      a.g.in_si = a.g.out_si = 1;
+      a.g.in_sn = a.g.out_sn = I * N2;
+      a.tw2 = twN;
+      a.Nfull = N;
+      a.scale = (T)1;
+      if ((st = launch<T>(K_C2C, false, N1, a, s)) != NFT_OK) return st;
+    }
+    {  // B: length-N2 FFTs over rows N2*k1 + n2; element k2 -> k = k1 + N1*k2; unpack
+      FastArgs<T> a;
+      memset(&a, 0, sizeof(a));
+      a.in = ws;
+      a.out = out;
+      a.g.O = O;
+      a.g.M = N1;
+      a.g.I = I;
+      a.g.in_so = I * N;
+      a.g.in_sm = I * N2;
+      a.g.in_si = 1;
+      a.g.in_sn = I;
+      a.km = 1;
+      a.kx = N1;
+      a.Nfull = N;
+      a.rs = rrs;
+      a.sigma = sigma;
+      a.scale = (T)scale;
+      a.desc = desc;
+      return launch<T>(K_UNPACK, false, N2, a, s);
+    }
+  }
+}
+
 template <typename T>
 static int c2c_impl(const void* in, void* out, const Geo& g, const std::vector<int>& ax, int forward,
                     double scale, hipStream_t s) {
@@ -487,6 +655,12 @@ int nft_hartley(const void* in, void* out, int ndim, const int64_t* shape, int n
   int st = parse_axes(ndim, shape, naxes, axes, g, ax);
   if (st != NFT_OK) return st;
   int sigma = convention == 0 ? 1 : -1;
+  static const bool v1_only = getenv("NFT_ENGINE_V1") != nullptr;
+  if (!v1_only && (dtype == 0 || dtype == 1)) {
+    if (dtype == 0) st = hartley_v2<double>(in, out, g, ax, sigma, scale, workspace, ws_bytes, stream);
+    else if (dtype == 1) st = hartley_v2<float>(in, out, g, ax, sigma, scale, workspace, ws_bytes, stream);
+    if (st != NFT_FALLBACK) return st;
+  }
   if (dtype == 0) return hartley_impl<double>(in, out, g, ax, sigma, scale, workspace, ws_bytes, stream);
   if (dtype == 1) return hartley_impl<float>(in, out, g, ax, sigma, scale, workspace, ws_bytes, stream);
   set_last_error("bad dtype %d", dtype);
