@@ -30,6 +30,12 @@
  *                      from HarmonicTransformOperator o (PowerDistributor(A) * xi)
  *                      (src/library/correlated_fields_simple.py:155-160) sandwiched as
  *                      in src/minimization/kl_energies.py:115-123
+ *   nft_amp_*          Jacobian of the non-parametric amplitude subtree of the CF
+ *                      model: _TwoLogIntegrations, _SlopeRemover, _Normalization,
+ *                      fluctuation/zero-mode scaling (src/library/correlated_fields.py:
+ *                      91-201, correlated_fields_simple.py:86-127), linearised
+ *   nft_los_*          LOSResponse.apply on a box-blocked layout of the same COO
+ *                      matrix, src/library/los_response.py:180-233
  *   nft_spmv_*         LOSResponse.apply (scipy COO matvec / rmatvec),
  *                      src/library/los_response.py:226-233
  */
@@ -105,6 +111,117 @@ int nft_bin_scatter(const void* in, const int* perm, const int* offsets, void* o
 /* y[r] = scale * sum_j weights[j] * x[indices[j]], j in [indptr[r], indptr[r+1]) */
 int nft_spmv_csr(const int64_t* indptr, const int* indices, const float* weights, const void* x,
                  void* y, int64_t nrows, int dtype, double scale, int64_t nnz, hipStream_t stream);
+/* Host helper: partition CSR rows into CSR-stream blocks (<= 256 rows and
+ * <= 2048 nonzeros each; a longer single row gets its own block).  indptr is
+ * HOST memory; blocks[0..nblocks] receives the block row boundaries. */
+int nft_csr_rowblocks(const int64_t* indptr, int64_t nrows, int* blocks, int64_t cap,
+                      int64_t* nblocks);
+/* y[r] = scale * rowscale[r] * sum_j weights[j] * colscale[c_j] * x[c_j]
+ * (colscale / rowscale may be NULL = 1).  rowblocks (device, from
+ * nft_csr_rowblocks) selects the CSR-stream kernel for short rows; NULL
+ * selects one wave per row.  Fuses the diagonal factors around R in
+ * sampling metrics (e.g. sigmoid' and the noise weights). */
+int nft_spmv_scaled(const int64_t* indptr, const int* indices, const float* weights,
+                    const int* rowblocks, int64_t nblocks, const void* x, const void* colscale,
+                    const void* rowscale, void* y, int64_t nrows, int dtype, double scale,
+                    hipStream_t stream);
+
+/* ---- Hartley transform with fused elementwise prologue / epilogue ------ */
+/* Flat real indices i (input) and j (output) of the C-contiguous arrays:
+ *   u[i]    = (pro_a ? pro_a[i] : 1) * pro_x[i] + (pro_b ? pro_b[i] * pro_c[pro_index[i]] : 0)
+ *             (u = in when pro_x is NULL)
+ *   h       = scale * Hartley(u)
+ *   out[j]  = (epi_a ? epi_a[j] : 1) * h[j] + (epi_d ? epi_shift * epi_d[j] : 0)
+ *   epi_out2[j] = epi_b[j] * h[j]     (if epi_out2)
+ * On the compile-time-planned power-of-two paths the prologue runs inside the
+ * first axis pass and the epilogue inside the last one (no extra HBM pass);
+ * other shapes run them as separate elementwise kernels.  This is the
+ * correlated-field Jacobian's  HT[A*xi + xi0*dA[pindex]]  and its adjoint's
+ * (A*v + shift*d, xi0*v)  (src/library/correlated_fields_simple.py:155-160). */
+typedef struct nft_hartley_fuse {
+  const void *pro_a, *pro_x, *pro_b, *pro_c;
+  const int* pro_index;
+  const void *epi_a, *epi_d, *epi_b;
+  void* epi_out2;
+  double epi_shift;
+} nft_hartley_fuse;
+
+int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes,
+                                int dtype, size_t* bytes);
+int nft_hartley_fused(const nft_hartley_fuse* fuse, const void* in, void* out, int ndim,
+                      const int64_t* shape, int naxes, const int* axes, int dtype, int convention,
+                      double scale, void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* ---- box-blocked LOS response ----------------------------------------- */
+/* Device arrays of a line-of-sight response regrouped by 256-pixel boxes
+ * (16x16 over the last two grid axes, 1x256 for 1-D grids; the grid is
+ * viewed as [L, H, W]).  Built on the host from the COO triplets
+ * (LOSResponse._box_plan); all index arrays int32 unless noted.
+ *   forward:  nitems work items (box item_box[i], segments item_seg[i]..[i+1]);
+ *             a segment is the run of one line of sight inside one box:
+ *             entries seg_ent[s]..[s+1] with 8-bit local pixel ent_loc and fp32
+ *             weight ent_wf; its partial goes to slot seg_slot[s]; line l owns
+ *             slots los_ptr[l]..[l+1] (in box order).
+ *   adjoint:  box b owns entries box_ent[b]..[b+1], sorted by local pixel;
+ *             pixel t of the box owns pix_off[257*b+t]..[257*b+t+1] (uint16,
+ *             relative to box_ent[b]); the lines crossing box b are
+ *             box_lines[box_lptr[b]..box_lptr[b+1]) (ascending); each entry
+ *             holds its line as an index into that list (ent_lidx: uint8 if
+ *             lidx8 else uint16) and an fp32 weight ent_wa. */
+typedef struct nft_los_plan {
+  int64_t H, W;
+  int bh, bw, nby, nbx;
+  int64_t nbox, nlos, nitems, nseg;
+  const int *item_box, *item_seg, *seg_ent, *seg_slot;
+  const uint8_t* ent_loc;
+  const float* ent_wf;
+  const int* los_ptr;
+  const int* box_ent;
+  const uint16_t* pix_off;
+  const int *box_lptr, *box_lines;
+  const void* ent_lidx;
+  int lidx8;
+  const float* ent_wa;
+} nft_los_plan;
+
+size_t nft_los_workspace(const nft_los_plan* plan);
+/* y[l] = scale * rowscale[l] * sum_{(l,p)} w * colscale[p] * x[p]   (R x) */
+int nft_los_forward(const nft_los_plan* plan, const void* x, const void* colscale,
+                    const void* rowscale, void* y, void* ws, int dtype, double scale,
+                    hipStream_t stream);
+/* out[p] = scale * rowscale[p] * sum_{(l,p)} w * colscale[l] * y[l]   (R^T y) */
+int nft_los_adjoint(const nft_los_plan* plan, const void* y, const void* colscale,
+                    const void* rowscale, void* out, int dtype, double scale, hipStream_t stream);
+
+/* ---- correlated-field amplitude Jacobian ------------------------------ */
+/* Constants of the amplitude linearisation at one expansion point (all device
+ * pointers, fp64).  B = number of power bins, M = B - 2.
+ *   c0 = sf*sq0, sf, p0, p1, p2, lv          [M]   (spectrum/flex/asp coefficients)
+ *   vslope, sc, Qf, Qa, mspec = mult*spec, An [B]
+ * Qf/Qa: SlopeRemove(TwoLog(.)) of the flexibility/asperity coefficients. */
+typedef struct nft_amp_const {
+  const double *c0, *sf, *p0, *p1, *p2, *lv;
+  const double *vslope, *sc, *Qf, *Qa, *mspec, *An;
+  double fl, S, ls_f, sig_s, zm, ls_o, total_volume;
+  int64_t B;
+  int has_flex, has_asp, has_zm;
+} nft_amp_const;
+
+/* Cotangent outputs of the VJP (device pointers; NULL for absent keys):
+ * out = shift * d + J_amp^T g, d pointers may be NULL (then shift * d = 0). */
+typedef struct nft_amp_out {
+  double *fl, *sl, *flex, *asp, *zm, *spec;
+  const double *dfl, *dsl, *dflex, *dasp, *dzm, *dspec;
+  double shift;
+} nft_amp_out;
+
+size_t nft_amp_workspace(int64_t B);
+/* da[B] = J_amp [t_fl, t_sl, t_flex, t_asp, t_zm, t_spec(2,M)] */
+int nft_amp_jvp(const nft_amp_const* c, const double* t_fl, const double* t_sl,
+                const double* t_flex, const double* t_asp, const double* t_zm,
+                const double* t_spec, double* da, double* ws, hipStream_t stream);
+int nft_amp_vjp(const nft_amp_const* c, const double* g, const nft_amp_out* out, double* ws,
+                hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -33,7 +33,46 @@ SIGNATURES = {
     "nft_bin_gather": (_i, [_p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_bin_scatter": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
+    "nft_csr_rowblocks": (_i, [_p, _i64, _p, _i64, ctypes.POINTER(_i64)]),
+    "nft_spmv_scaled": (_i, [_p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i, _d, _p]),
+    "nft_hartley_fused_workspace": (_i, [_i, _p, _i, _p, _i, ctypes.POINTER(_sz)]),
+    "nft_hartley_fused": (_i, [_p, _p, _p, _i, _p, _i, _p, _i, _i, _d, _p, _sz, _p]),
+    "nft_los_workspace": (_sz, [_p]),
+    "nft_los_forward": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _p]),
+    "nft_los_adjoint": (_i, [_p, _p, _p, _p, _p, _i, _d, _p]),
+    "nft_amp_workspace": (_sz, [_i64]),
+    "nft_amp_jvp": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "nft_amp_vjp": (_i, [_p, _p, _p, _p, _p]),
 }
+
+
+class HartleyFuse(ctypes.Structure):
+    """nft_hartley_fuse (include/nifty_amd.h)."""
+    _fields_ = [(n, _p) for n in ("pro_a", "pro_x", "pro_b", "pro_c", "pro_index", "epi_a", "epi_d", "epi_b",
+                                  "epi_out2")] + [("epi_shift", _d)]
+
+
+class LosPlan(ctypes.Structure):
+    """nft_los_plan (include/nifty_amd.h)."""
+    _fields_ = [("H", _i64), ("W", _i64), ("bh", _i), ("bw", _i), ("nby", _i), ("nbx", _i),
+                ("nbox", _i64), ("nlos", _i64), ("nitems", _i64), ("nseg", _i64)] + \
+               [(n, _p) for n in ("item_box", "item_seg", "seg_ent", "seg_slot", "ent_loc", "ent_wf",
+                                  "los_ptr", "box_ent", "pix_off", "box_lptr", "box_lines", "ent_lidx")] + \
+               [("lidx8", _i), ("ent_wa", _p)]
+
+
+class AmpConst(ctypes.Structure):
+    """nft_amp_const (include/nifty_amd.h)."""
+    _fields_ = [(n, _p) for n in ("c0", "sf", "p0", "p1", "p2", "lv", "vslope", "sc", "Qf", "Qa",
+                                  "mspec", "An")] + \
+               [(n, _d) for n in ("fl", "S", "ls_f", "sig_s", "zm", "ls_o", "total_volume")] + \
+               [("B", _i64), ("has_flex", _i), ("has_asp", _i), ("has_zm", _i)]
+
+
+class AmpOut(ctypes.Structure):
+    """nft_amp_out (include/nifty_amd.h)."""
+    _fields_ = [(n, _p) for n in ("fl", "sl", "flex", "asp", "zm", "spec",
+                                  "dfl", "dsl", "dflex", "dasp", "dzm", "dspec")] + [("shift", _d)]
 
 CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD = range(8)
 CG_NSCALARS = 16
@@ -189,3 +228,96 @@ def spmv_csr(indptr, indices, weights, x, y, scale=1.0):
     _check(lib.nft_spmv_csr(ptr(indptr), ptr(indices), ptr(weights), ptr(x), ptr(y), nrows,
                             dtype_code(x.dtype), float(scale), indices.numel(), stream_ptr()))
     return y
+
+
+def csr_rowblocks(indptr):
+    """CSR-stream row blocks for a host int64 indptr array (numpy)."""
+    import numpy as np
+    lib = load()
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    nrows = indptr.size - 1
+    cap = nrows + 2
+    blocks = np.empty(cap, dtype=np.int32)
+    nb = ctypes.c_int64(0)
+    _check(lib.nft_csr_rowblocks(indptr.ctypes.data, nrows, blocks.ctypes.data, cap, ctypes.byref(nb)))
+    return blocks[:nb.value + 1].copy()
+
+
+def spmv_scaled(indptr, indices, weights, rowblocks, x, y, colscale=None, rowscale=None, scale=1.0):
+    lib = load()
+    require_device(indptr, indices, weights, rowblocks, x, y, colscale, rowscale)
+    nrows = indptr.numel() - 1
+    nb = rowblocks.numel() - 1 if rowblocks is not None else 0
+    _check(lib.nft_spmv_scaled(ptr(indptr), ptr(indices), ptr(weights), ptr(rowblocks), nb, ptr(x),
+                               ptr(colscale), ptr(rowscale), ptr(y), nrows, dtype_code(x.dtype),
+                               float(scale), stream_ptr()))
+    return y
+
+
+def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0):
+    """out = epilogue(scale * Hartley(prologue)) with
+    pro = dict(a=, x=, b=, c=, index=) and epi = dict(a=, d=, shift=, b=, out2=)
+    (nft_hartley_fused); `x` is the plain input when no prologue is given."""
+    lib = load()
+    f = HartleyFuse()
+    tens = [out, x]
+    if pro:
+        for k, fld in (("a", "pro_a"), ("x", "pro_x"), ("b", "pro_b"), ("c", "pro_c"), ("index", "pro_index")):
+            v = pro.get(k)
+            tens.append(v)
+            setattr(f, fld, v.data_ptr() if v is not None else None)
+    if epi:
+        for k, fld in (("a", "epi_a"), ("d", "epi_d"), ("b", "epi_b"), ("out2", "epi_out2")):
+            v = epi.get(k)
+            tens.append(v)
+            setattr(f, fld, v.data_ptr() if v is not None else None)
+        f.epi_shift = float(epi.get("shift", 0.0))
+    require_device(*tens)
+    for t in tens:
+        if t is not None and t.dtype != out.dtype and t.dtype != torch.int32:
+            raise TypeError("hartley_fused: operand dtype mismatch")
+    nd, sh, na, ax = _shape_args(tuple(out.shape), tuple(axes))
+    dt = dtype_code(out.dtype)
+    nbytes = ctypes.c_size_t(0)
+    _check(lib.nft_hartley_fused_workspace(nd, sh, na, ax, dt, ctypes.byref(nbytes)))
+    ws = workspace(nbytes.value, out.device, "hartley")
+    _check(lib.nft_hartley_fused(ctypes.byref(f), ptr(x), ptr(out), nd, sh, na, ax, dt, int(convention),
+                                 float(scale), ptr(ws), ctypes.c_size_t(ws.numel()), stream_ptr()))
+    return out
+
+
+def los_forward(plan, x, y, colscale=None, rowscale=None, scale=1.0):
+    """y = scale * rowscale * R (colscale * x) on a box plan (LosPlan)."""
+    lib = load()
+    require_device(x, y, colscale, rowscale)
+    ws = workspace(lib.nft_los_workspace(ctypes.byref(plan)), x.device, "los")
+    _check(lib.nft_los_forward(ctypes.byref(plan), ptr(x), ptr(colscale), ptr(rowscale), ptr(y), ptr(ws),
+                               dtype_code(x.dtype), float(scale), stream_ptr()))
+    return y
+
+
+def los_adjoint(plan, y, out, colscale=None, rowscale=None, scale=1.0):
+    """out = scale * rowscale * R^T (colscale * y)."""
+    lib = load()
+    require_device(y, out, colscale, rowscale)
+    _check(lib.nft_los_adjoint(ctypes.byref(plan), ptr(y), ptr(colscale), ptr(rowscale), ptr(out),
+                               dtype_code(y.dtype), float(scale), stream_ptr()))
+    return out
+
+
+def amp_jvp(const, t_fl, t_sl, t_flex, t_asp, t_zm, t_spec, da):
+    """da = J_amp t (constants `const`: AmpConst holding device pointers)."""
+    lib = load()
+    require_device(t_fl, t_sl, t_flex, t_asp, t_zm, t_spec, da)
+    ws = workspace(lib.nft_amp_workspace(const.B), da.device, "amp")
+    _check(lib.nft_amp_jvp(ctypes.byref(const), ptr(t_fl), ptr(t_sl), ptr(t_flex), ptr(t_asp),
+                           ptr(t_zm), ptr(t_spec), ptr(da), ptr(ws), stream_ptr()))
+    return da
+
+
+def amp_vjp(const, g, out):
+    """out (AmpOut of device pointers) = shift * d + J_amp^T g."""
+    lib = load()
+    require_device(g)
+    ws = workspace(lib.nft_amp_workspace(const.B), g.device, "amp")
+    _check(lib.nft_amp_vjp(ctypes.byref(const), ptr(g), ctypes.byref(out), ptr(ws), stream_ptr()))

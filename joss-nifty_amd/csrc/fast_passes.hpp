@@ -14,6 +14,40 @@ namespace fast {
 
 enum Kind { K_C2C = 0, K_R2C = 1, K_H1D = 2, K_UNPACK = 3 };
 
+// Optional elementwise work fused into the first / last pass of a transform
+// (flat real indices of the input / output array):
+//   prologue  u[i] = (pa ? pa[i] : 1) * px[i] + (pb ? pb[i] * pc[pidx[i]] : 0)
+//   epilogue  out[j] = (ea ? ea[j] : 1) * h + (ed ? eshift * ed[j] : 0);
+//             out2[j] = eb[j] * h   (if out2)
+struct FuseArgs {
+  const void *pa, *px, *pb, *pc;
+  const int* pidx;
+  const void *ea, *ed, *eb;
+  void* out2;
+  double eshift;
+  int pro, epi;
+};
+
+template <typename T>
+__device__ __forceinline__ T fuse_pro(const FuseArgs& f, long long i) {
+  T v = ((const T*)f.px)[i];
+  if (f.pa) v *= ((const T*)f.pa)[i];
+  if (f.pb) v += ((const T*)f.pb)[i] * ((const T*)f.pc)[f.pidx[i]];
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void fuse_store(const FuseArgs& f, T* out, long long j, T h) {
+  if (!f.epi) {
+    out[j] = h;
+    return;
+  }
+  T r = f.ea ? ((const T*)f.ea)[j] * h : h;
+  if (f.ed) r += (T)f.eshift * ((const T*)f.ed)[j];
+  out[j] = r;
+  if (f.out2) ((T*)f.out2)[j] = ((const T*)f.eb)[j] * h;
+}
+
 template <typename T> struct FastArgs {
   Lines g;
   const void* in;
@@ -26,6 +60,7 @@ template <typename T> struct FastArgs {
   long long rs;       // UNPACK: real-output stride along the axis
   T scale;
   LineDesc desc;      // UNPACK: (o, i) -> real output line / mirror line
+  FuseArgs f;         // R2C/H1D: prologue; UNPACK/H1D: epilogue
 };
 
 template <typename T, int N, int NT, int KIND, bool ROWS>
@@ -67,8 +102,14 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       const T* in = (const T*)a.in;
       const long long row0 = 2 * (o + l);
       if (row0 < a.Ireal) {
-        v.x = in[row0 * g.in_so + (long long)x * g.in_sn];
-        if (row0 + 1 < a.Ireal) v.y = in[(row0 + 1) * g.in_so + (long long)x * g.in_sn];
+        const long long i0 = row0 * g.in_so + (long long)x * g.in_sn;
+        if (a.f.pro) {
+          v.x = fuse_pro<T>(a.f, i0);
+          if (row0 + 1 < a.Ireal) v.y = fuse_pro<T>(a.f, i0 + g.in_so);
+        } else {
+          v.x = in[i0];
+          if (row0 + 1 < a.Ireal) v.y = in[i0 + g.in_so];
+        }
       }
     } else {
       const C* in = (const C*)a.in;
@@ -148,8 +189,9 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         const C zk = lds[l * PITCH + k];
         const C zm = lds[l * PITCH + ((N - k) & (N - 1))];
         const long long ko = (long long)k * g.out_sn;
-        out[row0 * g.out_so + ko] = hs * ((zk.x + zm.x) + sg * (zk.y - zm.y));
-        if (row0 + 1 < a.Ireal) out[(row0 + 1) * g.out_so + ko] = hs * ((zk.y + zm.y) - sg * (zk.x - zm.x));
+        fuse_store<T>(a.f, out, row0 * g.out_so + ko, hs * ((zk.x + zm.x) + sg * (zk.y - zm.y)));
+        if (row0 + 1 < a.Ireal)
+          fuse_store<T>(a.f, out, (row0 + 1) * g.out_so + ko, hs * ((zk.y + zm.y) - sg * (zk.x - zm.x)));
       }
     }
   } else {  // UNPACK
@@ -190,10 +232,10 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       if (!u.valid) continue;
       const C f = lds[l * PITCH + x];
       const int k = (int)m * a.km + x * a.kx;
-      out[u.base + (long long)k * a.rs] = sc * (f.x + sg * f.y);
+      fuse_store<T>(a.f, out, u.base + (long long)k * a.rs, sc * (f.x + sg * f.y));
       if (u.mirror) {
         const int km = (k == 0) ? 0 : Nf - k;
-        out[u.mbase + (long long)km * a.rs] = sc * (f.x - sg * f.y);
+        fuse_store<T>(a.f, out, u.mbase + (long long)km * a.rs, sc * (f.x - sg * f.y));
       }
     }
   }

@@ -1,0 +1,438 @@
+// Correlated-field amplitude Jacobian (JVP / VJP) on the power-spectrum bins.
+//
+// Replaces, for the sampling metric, the B-sized operator subtree of the
+// reference's CF model (src/library/correlated_fields.py:91-201,
+// correlated_fields_simple.py:86-127): NormalTransform/LognormalTransform
+// scalings, _TwoLogIntegrations (two cumulative sums), _SlopeRemover,
+// _Normalization (exp, sum over modes, sqrt), zero-mode insertion and volume
+// scaling.  The nonlinear parts are linearised at the expansion point; all
+// per-bin constants of that linearisation are precomputed there (see
+// AmpConst), so a JVP or VJP is four to six bandwidth-light kernels instead of
+// ~25 small tensor ops:
+//
+//   JVP:  scan(t1*sf) -> t = (c+c_prev)/2*lv + t0*c0 -> scan(t) -> dapre -> da
+//   VJP:  gapre -> reverse scan -> reverse scan -> spectrum / scalar cotangents
+//
+// Scans are block-local (1024 elements per workgroup) with the carry of each
+// block obtained by summing the totals of all preceding blocks in index order:
+// O(nblocks) per block, deterministic, no inter-workgroup hand-off.
+#include "nft_api_internal.hpp"
+
+namespace nft {
+
+using AmpConst = nft_amp_const;
+using AmpOut = nft_amp_out;
+
+constexpr int AT = 256;          // threads per block
+constexpr int AE = 4;            // elements per thread
+constexpr int ABLK = AT * AE;    // elements per block
+
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+// block-wide sum, result broadcast to all threads
+__device__ __forceinline__ double block_total(double v, double* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wsum(v);
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0;
+#pragma unroll
+  for (int i = 0; i < AT / 64; ++i) t += sh[i];
+  __syncthreads();
+  return t;
+}
+
+// inclusive block scan of AE values per thread (thread-contiguous chunks);
+// REV scans from the end.  Returns the block total.
+template <bool REV>
+__device__ __forceinline__ double block_scan(double (&v)[AE], double* sh) {
+  // thread-local inclusive scan
+  if (REV) {
+#pragma unroll
+    for (int k = AE - 2; k >= 0; --k) v[k] += v[k + 1];
+  } else {
+#pragma unroll
+    for (int k = 1; k < AE; ++k) v[k] += v[k - 1];
+  }
+  double mine = REV ? v[0] : v[AE - 1];
+  sh[threadIdx.x] = mine;
+  __syncthreads();
+  // Hillis-Steele over AT thread totals (in a second buffer half)
+  double* a = sh;
+  double* b = sh + AT;
+  for (int off = 1; off < AT; off <<= 1) {
+    double x = a[threadIdx.x];
+    if (!REV) {
+      if (threadIdx.x >= off) x += a[threadIdx.x - off];
+    } else {
+      if (threadIdx.x + off < AT) x += a[threadIdx.x + off];
+    }
+    b[threadIdx.x] = x;
+    __syncthreads();
+    double* t = a;
+    a = b;
+    b = t;
+  }
+  const double incl = a[threadIdx.x];
+  const double total = REV ? a[0] : a[AT - 1];
+  const double excl = incl - mine;
+#pragma unroll
+  for (int k = 0; k < AE; ++k) v[k] += excl;
+  __syncthreads();
+  return total;
+}
+
+// sum of block totals [0, blk) (or (blk, nb) for REV) in index order
+template <bool REV>
+__device__ __forceinline__ double carry_in(const double* tot, int blk, int nb, double* sh) {
+  double s = 0;
+  if (!REV) {
+    for (int i = threadIdx.x; i < blk; i += AT) s += tot[i];
+  } else {
+    for (int i = blk + 1 + threadIdx.x; i < nb; i += AT) s += tot[i];
+  }
+  return block_total(s, sh);
+}
+
+// ------------------------------------------------------------------ JVP
+// J1: cs1 = local scan of t1*sf over j < B-2
+__global__ __launch_bounds__(AT) void amp_jvp_1(AmpConst c, const double* __restrict__ tspec,
+                                                double* __restrict__ loc, double* __restrict__ tot1) {
+  __shared__ double sh[2 * AT];
+  const long long M = c.B - 2;
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  double v[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    long long j = j0 + k;
+    v[k] = j < M ? tspec[M + j] * c.sf[j] : 0.0;
+  }
+  double t = block_scan<false>(v, sh);
+#pragma unroll
+  for (int k = 0; k < AE; ++k)
+    if (j0 + k < M) loc[j0 + k] = v[k];
+  if (threadIdx.x == 0) tot1[blockIdx.x] = t;
+}
+
+// J3: c = loc + carry; t = (c + c_prev)/2*lv + t0*c0; local scan of t
+__global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c, const double* __restrict__ tspec,
+                                                const double* __restrict__ tot1, double* __restrict__ loc,
+                                                double* __restrict__ tot2) {
+  __shared__ double sh[2 * AT];
+  const long long M = c.B - 2;
+  const int nb = (int)((M + ABLK - 1) / ABLK);
+  const double carry = carry_in<false>(tot1, blockIdx.x, nb, sh);
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  double v[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    long long j = j0 + k;
+    if (j < M) {
+      const double cj = loc[j] + carry;
+      const double u1 = tspec[M + j] * c.sf[j];
+      const double cp = cj - u1;
+      v[k] = (cj + cp) / 2 * c.lv[j] + tspec[j] * c.c0[j];
+    } else {
+      v[k] = 0.0;
+    }
+  }
+  double t = block_scan<false>(v, sh);
+#pragma unroll
+  for (int k = 0; k < AE; ++k)
+    if (j0 + k < M) loc[j0 + k] = v[k];
+  if (threadIdx.x == 0) tot2[blockIdx.x] = t;
+}
+
+// J5: tl = [0,0, loc + carry]; dapre; partial sums of mspec*dapre
+__global__ __launch_bounds__(AT) void amp_jvp_5(AmpConst c, const double* tfl, const double* tsl,
+                                                const double* tflex, const double* tasp,
+                                                const double* __restrict__ loc, const double* __restrict__ tot2,
+                                                double* __restrict__ dapre, double* __restrict__ part) {
+  __shared__ double sh[2 * AT];
+  const long long B = c.B, M = B - 2;
+  const int nbM = c.has_flex ? (int)((M + ABLK - 1) / ABLK) : 0;
+  double T = 0;  // tl[B-1] = total of the second scan
+  if (c.has_flex) T = carry_in<false>(tot2, nbM, nbM, sh);
+  const double ssl = c.sig_s * tsl[0];
+  const double sf_ = c.has_flex ? tflex[0] : 0.0;
+  const double sa_ = c.has_asp ? tasp[0] : 0.0;
+  const long long b0 = (long long)blockIdx.x * ABLK;
+  // tl_b needs scan position j = b-2; this block's j-range spans at most the
+  // scan blocks blk0 and blk0+1
+  const int blk0 = b0 >= 2 ? (int)((b0 - 2) / ABLK) : 0;
+  double cr0 = 0, cr1 = 0;
+  if (c.has_flex) {
+    cr0 = carry_in<false>(tot2, blk0, nbM, sh);
+    cr1 = cr0 + (blk0 < nbM ? tot2[blk0] : 0.0);
+  }
+  double acc = 0;
+  for (int k = 0; k < AE; ++k) {
+    const long long b = b0 + threadIdx.x + (long long)k * AT;
+    if (b >= B) continue;
+    double tl = 0;
+    if (c.has_flex && b >= 2) {
+      const long long j = b - 2;
+      tl = loc[j] + ((int)(j / ABLK) == blk0 ? cr0 : cr1);
+    }
+    double d = c.vslope[b] * ssl + tl - T * c.sc[b];
+    if (c.has_flex) d += sf_ * c.Qf[b];
+    if (c.has_asp) d += sa_ * c.Qa[b];
+    dapre[b] = d;
+    acc += c.mspec[b] * d;
+  }
+  (void)tfl;
+  const double s = block_total(acc, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// J7: da from dapre and dS = sum(part)
+__global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c, const double* tfl, const double* tzm,
+                                                const double* __restrict__ dapre, const double* __restrict__ part,
+                                                int npart, double* __restrict__ da) {
+  __shared__ double sh[2 * AT];
+  double s = 0;
+  for (int i = threadIdx.x; i < npart; i += AT) s += part[i];
+  const double dS = block_total(s, sh);
+  const double dfl = c.fl * c.ls_f * tfl[0];
+  const long long B = c.B;
+  for (long long b = (long long)blockIdx.x * AT + threadIdx.x; b < B; b += (long long)gridDim.x * AT) {
+    double v;
+    if (b == 0) {
+      v = c.has_zm ? c.zm * c.ls_o * tzm[0] : 0.0;
+    } else {
+      const double An = c.An[b];
+      v = dfl * An + c.fl * An * (dapre[b] / 2. - dS / (2. * c.S));
+    }
+    da[b] = v * c.total_volume;
+  }
+}
+
+// ------------------------------------------------------------------ VJP
+// V1: partials of R1 = sum_{b>=1} TV*g_b*An_b
+__global__ __launch_bounds__(AT) void amp_vjp_1(AmpConst c, const double* __restrict__ g, double* __restrict__ part) {
+  __shared__ double sh[2 * AT];
+  double s = 0;
+  for (long long b = (long long)blockIdx.x * AT + threadIdx.x; b < c.B; b += (long long)gridDim.x * AT)
+    if (b > 0) s += c.total_volume * g[b] * c.An[b];
+  s = block_total(s, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// V2: gapre; partials R2 = sum vslope*gapre, R3 = sum gapre*sc
+__global__ __launch_bounds__(AT) void amp_vjp_2(AmpConst c, const double* __restrict__ g,
+                                                const double* __restrict__ part1, int np1,
+                                                double* __restrict__ gapre, double* __restrict__ part23) {
+  __shared__ double sh[2 * AT];
+  double s = 0;
+  for (int i = threadIdx.x; i < np1; i += AT) s += part1[i];
+  const double R1 = block_total(s, sh);
+  const double k = c.fl * R1 / (2. * c.S);
+  double r2 = 0, r3 = 0;
+  for (long long b = (long long)blockIdx.x * AT + threadIdx.x; b < c.B; b += (long long)gridDim.x * AT) {
+    const double gm = b > 0 ? c.total_volume * g[b] : 0.0;
+    const double gAn = c.fl * gm;
+    const double ga = c.An[b] * gAn / 2. - c.mspec[b] * k;
+    gapre[b] = ga;
+    r2 += c.vslope[b] * ga;
+    r3 += ga * c.sc[b];
+  }
+  r2 = block_total(r2, sh);
+  r3 = block_total(r3, sh);
+  if (threadIdx.x == 0) {
+    part23[2 * blockIdx.x] = r2;
+    part23[2 * blockIdx.x + 1] = r3;
+  }
+}
+
+// gtl[2+j] = gapre[2+j], minus R3 at the last bin
+__device__ __forceinline__ double gtl_at(const AmpConst& c, const double* gapre, long long j, double R3) {
+  const long long b = j + 2;
+  return gapre[b] - (b == c.B - 1 ? R3 : 0.0);
+}
+
+// V3: reverse local scan of gtl[2:] -> y (local) ; totals
+__global__ __launch_bounds__(AT) void amp_vjp_3(AmpConst c, const double* __restrict__ gapre,
+                                                const double* __restrict__ part23, int np,
+                                                double* __restrict__ loc, double* __restrict__ tot) {
+  __shared__ double sh[2 * AT];
+  double s = 0;
+  for (int i = threadIdx.x; i < np; i += AT) s += part23[2 * i + 1];
+  const double R3 = block_total(s, sh);
+  const long long M = c.B - 2;
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  double v[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    long long j = j0 + k;
+    v[k] = j < M ? gtl_at(c, gapre, j, R3) : 0.0;
+  }
+  double t = block_scan<true>(v, sh);
+#pragma unroll
+  for (int k = 0; k < AE; ++k)
+    if (j0 + k < M) loc[j0 + k] = v[k];
+  if (threadIdx.x == 0) tot[blockIdx.x] = t;
+}
+
+// V4: y = loc + suffix carry (g0); z = y*lv/2; w = z_j + z_{j+1}; reverse local scan of w
+__global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c, const double* __restrict__ gapre,
+                                                const double* __restrict__ part23, int np,
+                                                const double* __restrict__ tot3, double* __restrict__ y,
+                                                double* __restrict__ loc, double* __restrict__ tot4) {
+  __shared__ double sh[2 * AT];
+  double s = 0;
+  for (int i = threadIdx.x; i < np; i += AT) s += part23[2 * i + 1];
+  const double R3 = block_total(s, sh);
+  const long long M = c.B - 2;
+  const int nb = (int)((M + ABLK - 1) / ABLK);
+  const double carry = carry_in<true>(tot3, blockIdx.x, nb, sh);
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  double v[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    long long j = j0 + k;
+    if (j < M) {
+      const double yj = y[j] = loc[j] + carry;
+      const double zj = yj * c.lv[j] / 2.;
+      double zn = 0.0;
+      if (j + 1 < M) zn = (yj - gtl_at(c, gapre, j, R3)) * c.lv[j + 1] / 2.;
+      v[k] = zj + zn;
+    } else {
+      v[k] = 0.0;
+    }
+  }
+  double t = block_scan<true>(v, sh);
+#pragma unroll
+  for (int k = 0; k < AE; ++k)
+    if (j0 + k < M) loc[j0 + k] = v[k];
+  if (threadIdx.x == 0) tot4[blockIdx.x] = t;
+}
+
+
+
+// V5: g1 = loc + carry; spectrum cotangents; partials R4, R5
+__global__ __launch_bounds__(AT) void amp_vjp_5(AmpConst c, AmpOut o, const double* __restrict__ y,
+                                                const double* __restrict__ loc, const double* __restrict__ tot4,
+                                                double* __restrict__ part45) {
+  __shared__ double sh[2 * AT];
+  const long long M = c.B - 2;
+  const int nb = (int)((M + ABLK - 1) / ABLK);
+  const double carry = carry_in<true>(tot4, blockIdx.x, nb, sh);
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  double r4 = 0, r5 = 0;
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    long long j = j0 + k;
+    if (j < M) {
+      const double g0 = y[j];
+      const double g1 = loc[j] + carry;
+      double s0 = g0 * c.c0[j], s1 = g1 * c.sf[j];
+      if (o.dspec) {
+        s0 += o.shift * o.dspec[j];
+        s1 += o.shift * o.dspec[M + j];
+      }
+      o.spec[j] = s0;
+      o.spec[M + j] = s1;
+      r4 += g0 * c.p0[j] + g1 * c.p2[j];
+      if (c.has_asp) r5 += g0 * c.p1[j];
+    }
+  }
+  r4 = block_total(r4, sh);
+  r5 = block_total(r5, sh);
+  if (threadIdx.x == 0) {
+    part45[2 * blockIdx.x] = r4;
+    part45[2 * blockIdx.x + 1] = r5;
+  }
+}
+
+// V6: scalar cotangents (one block)
+__global__ __launch_bounds__(AT) void amp_vjp_6(AmpConst c, AmpOut o, const double* __restrict__ g,
+                                                const double* __restrict__ part1, int np1,
+                                                const double* __restrict__ part23, int np23,
+                                                const double* __restrict__ part45, int np45) {
+  __shared__ double sh[2 * AT];
+  double a = 0, b2 = 0, b4 = 0, b5 = 0;
+  for (int i = threadIdx.x; i < np1; i += AT) a += part1[i];
+  for (int i = threadIdx.x; i < np23; i += AT) b2 += part23[2 * i];
+  for (int i = threadIdx.x; i < np45; i += AT) {
+    b4 += part45[2 * i];
+    b5 += part45[2 * i + 1];
+  }
+  const double R1 = block_total(a, sh);
+  const double R2 = block_total(b2, sh);
+  const double R4 = block_total(b4, sh);
+  const double R5 = block_total(b5, sh);
+  if (threadIdx.x == 0) {
+    const double sh_ = o.shift;
+    o.fl[0] = c.fl * c.ls_f * R1 + (o.dfl ? sh_ * o.dfl[0] : 0.0);
+    o.sl[0] = c.sig_s * R2 + (o.dsl ? sh_ * o.dsl[0] : 0.0);
+    if (c.has_flex) o.flex[0] = R4 + (o.dflex ? sh_ * o.dflex[0] : 0.0);
+    if (c.has_asp) o.asp[0] = R5 + (o.dasp ? sh_ * o.dasp[0] : 0.0);
+    if (c.has_zm) o.zm[0] = c.zm * c.ls_o * c.total_volume * g[0] + (o.dzm ? sh_ * o.dzm[0] : 0.0);
+  }
+}
+
+static int nblk(long long n, int per) { return (int)std::max<long long>(1, (n + per - 1) / per); }
+
+}  // namespace nft
+
+using namespace nft;
+
+extern "C" {
+
+size_t nft_amp_workspace(int64_t B) { return (size_t)(3 * B + 16 * (B / 256 + 16)) * sizeof(double); }
+
+int nft_amp_jvp(const nft_amp_const* cst, const double* tfl, const double* tsl, const double* tflex, const double* tasp,
+                const double* tzm, const double* tspec, double* da, double* ws, hipStream_t s) {
+  const AmpConst& c = *cst;
+  const long long B = c.B, M = B - 2;
+  double* loc = ws;                 // M
+  double* dapre = ws + B;           // B
+  double* tot1 = ws + 2 * B;        // nbM
+  const int nbM = nblk(M, ABLK);
+  double* tot2 = tot1 + nbM + 1;
+  const int nbB = nblk(B, ABLK);
+  double* part = tot2 + nbM + 1;
+  if (c.has_flex) {
+    hipLaunchKernelGGL(amp_jvp_1, dim3(nbM), dim3(AT), 0, s, c, tspec, loc, tot1);
+    hipLaunchKernelGGL(amp_jvp_3, dim3(nbM), dim3(AT), 0, s, c, tspec, tot1, loc, tot2);
+  }
+  hipLaunchKernelGGL(amp_jvp_5, dim3(nbB), dim3(AT), 0, s, c, tfl, tsl, tflex, tasp, loc, tot2, dapre, part);
+  hipLaunchKernelGGL(amp_jvp_7, dim3(nblk(B, AT) < 1024 ? nblk(B, AT) : 1024), dim3(AT), 0, s, c, tfl, tzm,
+                     dapre, part, nbB, da);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_amp_vjp(const nft_amp_const* cst, const double* g, const nft_amp_out* out, double* ws, hipStream_t s) {
+  const AmpConst& c = *cst;
+  const AmpOut& o = *out;
+  const long long B = c.B, M = B - 2;
+  double* gapre = ws;               // B
+  double* loc = ws + B;             // M
+  double* y = ws + 2 * B;           // M
+  const int nbM = nblk(M, ABLK);
+  const int nr = std::min(nblk(B, AT), 1024);
+  double* part1 = ws + 3 * B;
+  double* part23 = part1 + nr + 1;
+  double* tot3 = part23 + 2 * nr + 2;
+  double* tot4 = tot3 + nbM + 1;
+  double* part45 = tot4 + nbM + 1;
+  hipLaunchKernelGGL(amp_vjp_1, dim3(nr), dim3(AT), 0, s, c, g, part1);
+  hipLaunchKernelGGL(amp_vjp_2, dim3(nr), dim3(AT), 0, s, c, g, part1, nr, gapre, part23);
+  if (c.has_flex) {
+    hipLaunchKernelGGL(amp_vjp_3, dim3(nbM), dim3(AT), 0, s, c, gapre, part23, nr, loc, tot3);
+    hipLaunchKernelGGL(amp_vjp_4, dim3(nbM), dim3(AT), 0, s, c, gapre, part23, nr, tot3, y, loc, tot4);
+    hipLaunchKernelGGL(amp_vjp_5, dim3(nbM), dim3(AT), 0, s, c, o, y, loc, tot4, part45);
+  }
+  hipLaunchKernelGGL(amp_vjp_6, dim3(1), dim3(AT), 0, s, c, o, g, part1, nr, part23, nr, part45,
+                     c.has_flex ? nbM : 0);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+}  // extern "C"

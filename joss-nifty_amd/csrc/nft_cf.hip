@@ -48,6 +48,55 @@ __global__ void bin_scatter_kernel(const T* __restrict__ in, const int* __restri
   }
 }
 
+// pre == post == 1: element-parallel gather + per-bin sums.  Block c owns the
+// sorted positions [c*BS_CH, (c+1)*BS_CH) and every bin that starts there; it
+// gathers in[perm[j]] for its range with all loads in flight (the per-bin
+// thread loop above is a chain of dependent random loads), stages them in LDS
+// and sums each bin sequentially in ascending j (np.bincount order, bit-exact);
+// a bin running past the chunk end reads its tail from global memory.
+constexpr int BS_CH = 2048;
+
+template <typename T>
+__global__ __launch_bounds__(256) void bin_scatter_chunk(const T* __restrict__ in, const int* __restrict__ perm,
+                                                         const int* __restrict__ offs, T* __restrict__ out,
+                                                         long long npix, long long nbins) {
+  constexpr int PER = BS_CH / 256;
+  __shared__ T vals[BS_CH];
+  __shared__ int bnd[2];
+  const long long j0 = (long long)blockIdx.x * BS_CH;
+  const int t = threadIdx.x;
+  const int n = (int)(npix - j0 < BS_CH ? npix - j0 : BS_CH);
+  int pv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) pv[i] = t + i * 256 < n ? perm[j0 + t + i * 256] : 0;
+  T v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[i] = t + i * 256 < n ? in[pv[i]] : (T)0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+    if (t + i * 256 < n) vals[t + i * 256] = v[i];
+  if (t < 2) {
+    // first bin whose start offset is >= j0 (+ BS_CH)
+    const long long target = j0 + (t ? BS_CH : 0);
+    long long lo = 0, hi = nbins;  // search in offs[0..nbins)
+    while (lo < hi) {
+      const long long mid = (lo + hi) >> 1;
+      if ((long long)offs[mid] < target) lo = mid + 1;
+      else hi = mid;
+    }
+    // the last chunk also owns trailing empty bins (start offset == npix)
+    bnd[t] = (t && j0 + BS_CH >= npix) ? (int)nbins : (int)lo;
+  }
+  __syncthreads();
+  const int b0 = bnd[0], b1 = bnd[1];
+  for (int b = b0 + t; b < b1; b += 256) {
+    const long long a = offs[b], e = offs[b + 1];
+    T acc = (T)0;
+    for (long long j = a; j < e; ++j) acc += (j - j0 < BS_CH) ? vals[j - j0] : in[perm[j]];
+    out[b] = acc;
+  }
+}
+
 static int nblocks(long long tot) {
   long long b = (tot + 255) / 256;
   if (b < 1) b = 1;
@@ -83,6 +132,21 @@ int nft_bin_scatter(const void* in, const int* perm, const int* offsets, void* o
                     int64_t npix, int64_t nbins, int64_t post, int dtype, hipStream_t stream) {
   long long tot = pre * nbins * post;
   if (tot <= 0) return NFT_OK;
+  if (pre == 1 && post == 1 && (dtype == 0 || dtype == 1)) {
+    const unsigned nb = (unsigned)((npix + BS_CH - 1) / BS_CH);
+    if (npix <= 0) {
+      NFT_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)nbins * (dtype == 0 ? 8 : 4), stream));
+      return NFT_OK;
+    }
+    if (dtype == 0)
+      hipLaunchKernelGGL(bin_scatter_chunk<double>, dim3(nb), dim3(256), 0, stream, (const double*)in, perm,
+                         offsets, (double*)out, (long long)npix, (long long)nbins);
+    else
+      hipLaunchKernelGGL(bin_scatter_chunk<float>, dim3(nb), dim3(256), 0, stream, (const float*)in, perm,
+                         offsets, (float*)out, (long long)npix, (long long)nbins);
+    NFT_HIP_CHECK(hipGetLastError());
+    return NFT_OK;
+  }
   if (dtype == 0)
     hipLaunchKernelGGL(bin_scatter_kernel<double>, dim3(nblocks(tot)), dim3(256), 0, stream,
                        (const double*)in, perm, offsets, (double*)out, (long long)pre, (long long)npix,

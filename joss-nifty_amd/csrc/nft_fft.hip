@@ -454,7 +454,8 @@ static LineDesc make_desc(const Geo& g, const long long* cs, const std::vector<i
 
 template <typename T>
 static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector<int>& ax, int sigma,
-                      double scale, void* ws, size_t ws_bytes, hipStream_t s) {
+                      double scale, void* ws, size_t ws_bytes, hipStream_t s,
+                      const fast::FuseArgs* fz = nullptr) {
   using namespace fast;
   const int m = (int)ax.size();
   const int last = g.nd - 1;
@@ -473,6 +474,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
     a.Ireal = a.g.O;
     a.sigma = sigma;
     a.scale = (T)scale;
+    if (fz) a.f = *fz;
     return launch<T>(K_H1D, true, N, a, s);
   }
   const int h = ax[m - 1];
@@ -503,6 +505,10 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
     a.g.out_sn = 1;
     a.Ireal = a.g.O;
     a.scale = (T)1;
+    if (fz) {
+      a.f = *fz;
+      a.f.epi = 0;
+    }
     if ((st = launch<T>(K_R2C, true, N, a, s)) != NFT_OK) return st;
   }
   for (int k = m - 2; k >= 1; --k) {  // middle axes, strided C2C in place
@@ -547,6 +553,10 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
       a.sigma = sigma;
       a.scale = (T)scale;
       a.desc = desc;
+      if (fz) {
+        a.f = *fz;
+        a.f.pro = 0;
+      }
       return launch<T>(K_UNPACK, false, N, a, s);
     }
     int N1, N2;
@@ -589,9 +599,59 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
       a.sigma = sigma;
       a.scale = (T)scale;
       a.desc = desc;
+      if (fz) {
+        a.f = *fz;
+        a.f.pro = 0;
+      }
       return launch<T>(K_UNPACK, false, N2, a, s);
     }
   }
+}
+
+// unfused fallback of nft_hartley_fused: prologue / epilogue as elementwise passes
+template <typename T>
+__global__ void fuse_pro_kernel(fast::FuseArgs f, T* __restrict__ dst, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = fast::fuse_pro<T>(f, i);
+}
+
+template <typename T>
+__global__ void fuse_epi_kernel(fast::FuseArgs f, T* __restrict__ out, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    fast::fuse_store<T>(f, out, i, out[i]);
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+template <typename T>
+static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out, const Geo& g,
+                              const std::vector<int>& ax, int sigma, double scale, void* ws, size_t ws_bytes,
+                              size_t hws, hipStream_t s) {
+  static const bool v1_only = getenv("NFT_ENGINE_V1") != nullptr;
+  if (!v1_only) {
+    int st = hartley_v2<T>(in, out, g, ax, sigma, scale, ws, ws_bytes, s, &f);
+    if (st != NFT_FALLBACK) return st;
+  }
+  const long long n = prod(g.shape, 0, g.nd);
+  const unsigned nb = (unsigned)std::min<long long>((n + 255) / 256, 65536);
+  const void* src = in;
+  if (f.pro) {
+    if (ws_bytes < align256(hws) + (size_t)n * sizeof(T)) {
+      set_last_error("hartley_fused workspace too small");
+      return NFT_ERR_ARG;
+    }
+    T* tmp = (T*)((char*)ws + align256(hws));
+    hipLaunchKernelGGL(fuse_pro_kernel<T>, dim3(nb), dim3(256), 0, s, f, tmp, n);
+    NFT_HIP_CHECK(hipGetLastError());
+    src = tmp;
+  }
+  int st = hartley_impl<T>(src, out, g, ax, sigma, scale, ws, hws, s);
+  if (st != NFT_OK) return st;
+  if (f.epi) {
+    hipLaunchKernelGGL(fuse_epi_kernel<T>, dim3(nb), dim3(256), 0, s, f, (T*)out, n);
+    NFT_HIP_CHECK(hipGetLastError());
+  }
+  return NFT_OK;
 }
 
 template <typename T>
@@ -663,6 +723,52 @@ int nft_hartley(const void* in, void* out, int ndim, const int64_t* shape, int n
   }
   if (dtype == 0) return hartley_impl<double>(in, out, g, ax, sigma, scale, workspace, ws_bytes, stream);
   if (dtype == 1) return hartley_impl<float>(in, out, g, ax, sigma, scale, workspace, ws_bytes, stream);
+  set_last_error("bad dtype %d", dtype);
+  return NFT_ERR_ARG;
+}
+
+int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes, int dtype,
+                                size_t* bytes) {
+  int st = nft_hartley_workspace(ndim, shape, naxes, axes, dtype, bytes);
+  if (st != NFT_OK) return st;
+  long long n = 1;
+  for (int d = 0; d < ndim; ++d) n *= shape[d];
+  *bytes = align256(*bytes) + (size_t)n * (dtype == 0 ? 8 : 4);
+  return NFT_OK;
+}
+
+int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int ndim, const int64_t* shape,
+                      int naxes, const int* axes, int dtype, int convention, double scale, void* workspace,
+                      size_t ws_bytes, hipStream_t stream) {
+  Geo g;
+  std::vector<int> ax;
+  int st = parse_axes(ndim, shape, naxes, axes, g, ax);
+  if (st != NFT_OK) return st;
+  size_t hws = 0;
+  if ((st = nft_hartley_workspace(ndim, shape, naxes, axes, dtype, &hws)) != NFT_OK) return st;
+  fast::FuseArgs f;
+  memset(&f, 0, sizeof(f));
+  if (fz) {
+    f.pa = fz->pro_a;
+    f.px = fz->pro_x;
+    f.pb = fz->pro_b;
+    f.pc = fz->pro_c;
+    f.pidx = fz->pro_index;
+    f.ea = fz->epi_a;
+    f.ed = fz->epi_d;
+    f.eb = fz->epi_b;
+    f.out2 = fz->epi_out2;
+    f.eshift = fz->epi_shift;
+    f.pro = f.px != nullptr;
+    f.epi = (f.ea || f.ed || f.out2) ? 1 : 0;
+    if ((f.pb && (!f.pc || !f.pidx)) || (f.out2 && !f.eb)) {
+      set_last_error("nft_hartley_fused: incomplete fusion spec");
+      return NFT_ERR_ARG;
+    }
+  }
+  const int sigma = convention == 0 ? 1 : -1;
+  if (dtype == 0) return hartley_fused_impl<double>(f, in, out, g, ax, sigma, scale, workspace, ws_bytes, hws, stream);
+  if (dtype == 1) return hartley_fused_impl<float>(f, in, out, g, ax, sigma, scale, workspace, ws_bytes, hws, stream);
   set_last_error("bad dtype %d", dtype);
   return NFT_ERR_ARG;
 }

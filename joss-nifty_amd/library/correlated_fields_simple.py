@@ -16,17 +16,19 @@ single fused Jacobian node, CFJacobian:
     J^T g           = ( A_full * v ,  dA^T( bins(xi0 * v) ) ),  v = c_h HT g
 
 whose grid work runs in the native kernels (Hartley passes, power-bin
-gather/scatter) and whose B-sized amplitude Jacobian is a short sequence of
-device tensor ops.  CFJacobian also implements ``sandwich_apply`` /
+gather/scatter) and whose B-sized amplitude Jacobian runs in the nft_amp_*
+scan kernels on constants precomputed at the expansion point.  CFJacobian also implements ``sandwich_apply`` /
 ``metric_flat`` so that SandwichOperator and the fused CG can evaluate
 J^T W J without materialising the operator tree."""
+import os
+
 import numpy as np
 import torch
 
 from .. import _native, config
 from ..domain_tuple import DomainTuple
 from ..domains import PowerSpace, UnstructuredDomain
-from ..ducc_dispatch import hartley
+from ..ducc_dispatch import hartley_convention_code
 from ..field import Field
 from ..linearization import Linearization
 from ..multi_domain import MultiDomain
@@ -38,6 +40,11 @@ from ..packing import PackedLayout
 from ..utilities import lognormal_moments
 from .correlated_fields import (_log_vol, _relative_log_k_lengths, mode_multiplicity, slope_remove,
                                 slope_remove_adjoint, twolog, twolog_adjoint)
+
+
+# torch formulation of the amplitude JVP/VJP instead of the nft_amp kernels
+# (A/B comparisons only; both run on the device)
+_AMP_TORCH = os.environ.get("NFT_AMP_TORCH") is not None
 
 
 def _t(a):
@@ -167,6 +174,59 @@ class _AmplitudeModel:
                 out[self.k_asp] = c["asp"] * self.ls_a * torch.sum(gsq0 / (2. * sq0))
         return out
 
+    # ------------------------------------------------- native linearisation
+    def native_const(self, c):
+        """Per-bin constants of the linearisation at the expansion point for
+        the native JVP/VJP kernels (nft_amp_*, include/nifty_amd.h).  Returns
+        (AmpConst, keep-alive dict of the device tensors it points to)."""
+        keep = {}
+        if self.has_flex:
+            xs, sf, sq0 = c["xs"], c["sf"], c["sq0"]
+            keep["c0"] = (sf * sq0).contiguous()
+            keep["sf"] = sf.contiguous()
+            keep["p0"] = (xs[0] * sf * (self.ls_x * sq0)).contiguous()
+            keep["p2"] = (xs[1] * sf * self.ls_x).contiguous()
+            keep["lv"] = self.lv
+            keep["Qf"] = slope_remove(twolog(keep["p0"], keep["p2"], self.lv), self.sc).contiguous()
+            if self.has_asp:
+                keep["p1"] = (xs[0] * sf * c["asp"] * self.ls_a / (2. * sq0)).contiguous()
+                keep["Qa"] = slope_remove(twolog(keep["p1"], torch.zeros_like(keep["p1"]), self.lv),
+                                          self.sc).contiguous()
+        keep["vslope"], keep["sc"] = self.vslope, self.sc
+        keep["mspec"] = (self.mult * c["spec"]).contiguous()
+        keep["An"] = c["An"].contiguous()
+        k = _native.AmpConst()
+        for name in ("c0", "sf", "p0", "p1", "p2", "lv", "vslope", "sc", "Qf", "Qa", "mspec", "An"):
+            setattr(k, name, keep[name].data_ptr() if name in keep else None)
+        k.fl, k.S = float(c["fl"]), float(c["S"])
+        k.ls_f, k.sig_s = self.ls_f, self.sig_s
+        k.zm = float(c["zm"]) if self.has_zm else 0.0
+        k.ls_o = self.ls_o if self.has_zm else 0.0
+        k.total_volume = self.total_vol
+        k.B = self.B
+        k.has_flex, k.has_asp, k.has_zm = int(self.has_flex), int(self.has_asp), int(self.has_zm)
+        return k, keep
+
+    def native_jvp(self, const, t, da):
+        g = t.get
+        _native.amp_jvp(const, g(self.k_fl), g(self.k_sl), g(self.k_flex), g(self.k_asp),
+                        g(self.k_zm), g(self.k_spec), da)
+        return da
+
+    def native_vjp(self, const, g, out, d=None, shift=0.0):
+        """out/d: dict key -> contiguous device tensors; out = shift*d + J^T g."""
+        o = _native.AmpOut()
+        names = (("fl", self.k_fl), ("sl", self.k_sl), ("flex", self.k_flex), ("asp", self.k_asp),
+                 ("zm", self.k_zm), ("spec", self.k_spec))
+        for short, key in names:
+            if key in out:
+                setattr(o, short, out[key].data_ptr())
+                if d is not None and shift != 0.0:
+                    setattr(o, "d" + short, d[key].data_ptr())
+        o.shift = float(shift)
+        _native.amp_vjp(const, g, o)
+        return out
+
 
 class _AmplitudeJacobian(LinearOperator):
     def __init__(self, amp, cache, domain, target):
@@ -222,33 +282,66 @@ class CFJacobian(LinearOperator):
         self._target = model.target
         self._capability = self.TIMES | self.ADJOINT_TIMES
         self.device = afull.device
+        self._k = None
 
     @property
     def layout(self):
         return self._m.layout
 
     # ---------------------------------------------------------- primitives
-    def _times_t(self, t):
-        """t: dict key->tensor tangent.  Returns position-space grid tensor."""
-        m = self._m
-        da = m.amp.jvp(self._c, t)
-        dafull = torch.empty_like(self._afull)
-        b = m.bins
-        _native.bin_gather(da, b.pindex, dafull, 1, b.npix, b.nbin, 1)
-        u = self._afull * t[m.k_xi] + self._xi0 * dafull
-        return hartley(u, scale=m.c_h)
+    def _const(self):
+        if self._k is None:
+            self._k = self._m.amp.native_const(self._c)
+        return self._k[0]
 
-    def _adjoint_t(self, g, out=None):
-        """g: grid tensor.  Returns dict key->tensor (or fills `out` views)."""
+    def _times_t(self, t):
+        """t: dict key->tensor tangent.  Returns position-space grid tensor:
+        c_h HT[A_full * t_xi + xi0 * dA[pindex]] in one fused native transform
+        (the gather and the two products run inside its first pass)."""
         m = self._m
-        v = hartley(g.contiguous(), scale=m.c_h)
-        gxi = self._afull * v
-        ga = torch.empty(m.amp.B, dtype=v.dtype, device=v.device)
+        if _AMP_TORCH:
+            da = m.amp.jvp(self._c, t)
+        else:
+            da = torch.empty(m.amp.B, dtype=torch.float64, device=self.device)
+            m.amp.native_jvp(self._const(), {k: v.contiguous() for k, v in t.items()}, da)
+        out = torch.empty(self._afull.shape, dtype=self._afull.dtype, device=self.device)
+        pro = dict(a=self._afull, x=t[m.k_xi].contiguous(), b=self._xi0, c=da.contiguous(), index=m.bins.pindex)
+        return _native.hartley_fused(out, range(out.ndim), m.c_h, pro=pro, convention=hartley_convention_code())
+
+    def _adjoint_t(self, g, out=None, d=None, shift=0.0):
+        """g: grid tensor.  Returns dict key->tensor, or fills the `out` views
+        with shift * d + J^T g.  One fused transform produces both
+        A_full * v (+ shift * d_xi) and xi0 * v, v = c_h HT g."""
+        m = self._m
         b = m.bins
-        _native.bin_scatter((self._xi0 * v).contiguous(), b.perm, b.offsets, ga, 1, b.npix, b.nbin, 1)
-        res = m.amp.vjp(self._c, ga)
-        res[m.k_xi] = gxi
-        return res
+        w = torch.empty(self._afull.shape, dtype=self._afull.dtype, device=self.device)
+        oxi = out[m.k_xi] if out is not None else torch.empty_like(w)
+        epi = dict(a=self._afull, b=self._xi0, out2=w)
+        if out is not None and shift != 0.0:
+            epi.update(d=d[m.k_xi], shift=shift)
+        _native.hartley_fused(oxi, range(w.ndim), m.c_h, x=g.contiguous(), epi=epi,
+                              convention=hartley_convention_code())
+        ga = torch.empty(m.amp.B, dtype=w.dtype, device=w.device)
+        _native.bin_scatter(w, b.perm, b.offsets, ga, 1, b.npix, b.nbin, 1)
+        if out is None:
+            if _AMP_TORCH:
+                res = m.amp.vjp(self._c, ga)
+            else:
+                res = {k: torch.empty(self._domain[k].shape, dtype=torch.float64, device=self.device)
+                       for k in m.amp.domain_dict}
+                m.amp.native_vjp(self._const(), ga, res)
+            res[m.k_xi] = oxi
+            return res
+        if _AMP_TORCH:
+            res = m.amp.vjp(self._c, ga)
+            for k, r in res.items():
+                if shift != 0.0:
+                    torch.add(r.reshape(out[k].shape), d[k], alpha=shift, out=out[k])
+                else:
+                    out[k].copy_(r.reshape(out[k].shape))
+        else:
+            m.amp.native_vjp(self._const(), ga, out, d, shift)
+        return out
 
     def apply(self, x, mode):
         self._check_input(x, mode)
@@ -270,14 +363,7 @@ class CFJacobian(LinearOperator):
         lay = self.layout
         dv = lay.views(d)
         s = self._times_t(dv)
-        res = self._adjoint_t(W(s) if callable(W) else s * W)
-        qv = lay.views(q)
-        for k in lay.keys:
-            r = res[k].reshape(qv[k].shape)
-            if shift != 0.0:
-                torch.add(r, dv[k], alpha=shift, out=qv[k])
-            else:
-                qv[k].copy_(r)
+        self._adjoint_t(W(s) if callable(W) else s * W, lay.views(q), dv, shift)
 
 
 class _CorrelatedFieldModel(Operator):
@@ -309,7 +395,9 @@ class _CorrelatedFieldModel(Operator):
         afull = torch.empty(self.harmonic_partner.shape, dtype=a.dtype, device=a.device)
         b = self.bins
         _native.bin_gather(a, b.pindex, afull, 1, b.npix, b.nbin, 1)
-        s = hartley(afull * lat[self.k_xi], scale=self.c_h)
+        s = _native.hartley_fused(torch.empty_like(afull), range(afull.ndim), self.c_h,
+                                  pro=dict(a=afull, x=lat[self.k_xi].contiguous()),
+                                  convention=hartley_convention_code())
         if self.offset_mean is not None:
             s = s + self.offset_mean
         return s, a, c, afull

@@ -4,9 +4,10 @@ Construction (host, setup only): every line of sight is traversed through the
 pixel grid (Amanatides-Woo style cell crossing distances), giving per-pixel
 path lengths (optionally tapered by the parallax error function); entries are
 ordered by 16x16 pixel boxes exactly as the reference orders its COO matrix.
-The matrix is then stored on the device twice: CSR over lines of sight (for
-R x) and CSR over pixels (= CSC, for R^T y), float32 weights as in the
-reference, applied by csrc/nft_spmv.hip with fp64 accumulation."""
+The triplets are then regrouped into the box-blocked layout of
+csrc/nft_los.hip (box_plan): per 256-pixel box, the runs of each line (for
+R x) and the runs of each pixel (for R^T y), float32 weights as in the
+reference, fp64 accumulation in fixed order."""
 import numpy as np
 import torch
 from scipy.special import erfc
@@ -131,13 +132,138 @@ def los_coo(shape, distances, starts, ends, sigmas=None, truncation=3.):
     return ilos[order], iarr[order], xwgt[order], nlos
 
 
-def _csr(rows, cols, w, nrows):
-    """stable CSR (entries of a row keep their COO storage order)"""
-    order = np.argsort(rows, kind="stable")
-    cnt = np.bincount(rows, minlength=nrows)
-    ptr = np.zeros(nrows + 1, dtype=np.int64)
-    np.cumsum(cnt, out=ptr[1:])
-    return ptr, cols[order].astype(np.int32), w[order].astype(np.float32)
+LOS_CAP_F = 2048   # entries per forward work item (csrc/nft_los.hip)
+BOX = 256
+
+
+def box_plan(rows, cols, w, shape, nlos):
+    """Regroup COO triplets (storage order) into the box-blocked layout of
+    nft_los_plan (include/nifty_amd.h).  Returns a dict of numpy arrays and
+    geometry ints.  Within every (box, line) segment and every (box, pixel)
+    run the entries keep their COO order."""
+    shape = tuple(int(v) for v in shape)
+    ndim = len(shape)
+    W = shape[-1]
+    H = shape[-2] if ndim >= 2 else 1
+    bh, bw = (16, 16) if ndim >= 2 else (1, BOX)
+    nby, nbx = -(-H // bh), -(-W // bw)
+    L = int(np.prod(shape[:-2])) if ndim > 2 else 1
+    nbox = L * nby * nbx
+    n = len(rows)
+    if n >= 2 ** 31 - 1:
+        raise ValueError("LOS response too large for int32 entry offsets")
+    rows = np.asarray(rows, dtype=np.int64)
+    c = np.asarray(cols, dtype=np.int64)
+    x = c % W
+    t = c // W
+    y = t % H
+    lyr = t // H
+    box = (lyr * nby + y // bh) * nbx + x // bw
+    loc = (y % bh) * bw + x % bw
+    # ---- forward: segments = runs of one line inside one box
+    key = box * nlos + rows
+    of = np.argsort(key, kind="stable")
+    kb = key[of]
+    segstart = np.flatnonzero(np.r_[True, kb[1:] != kb[:-1]]) if n else np.zeros(0, np.int64)
+    nseg = len(segstart)
+    seg_ent = np.r_[segstart, n].astype(np.int32)
+    seg_box = box[of][segstart]
+    seg_los = rows[of][segstart]
+    # work items: all segments of a box, split where a box exceeds 256
+    # segments or LOS_CAP_F entries
+    segcnt = np.bincount(seg_box, minlength=nbox)
+    entcnt = np.bincount(box, minlength=nbox)
+    first_seg = np.r_[0, np.cumsum(segcnt)][:-1]
+    big = (segcnt > BOX) | (entcnt > LOS_CAP_F)
+    item_box, item_seg = [], []
+    for b in np.flatnonzero(segcnt):
+        s0 = int(first_seg[b])
+        s1 = s0 + int(segcnt[b])
+        if not big[b]:
+            item_box.append(b)
+            item_seg.append(s0)
+            continue
+        s = s0
+        while s < s1:
+            e = s + 1
+            while e < s1 and e - s < BOX and seg_ent[e + 1] - seg_ent[s] <= LOS_CAP_F:
+                e += 1
+            if seg_ent[e] - seg_ent[s] > LOS_CAP_F:
+                raise ValueError("a single line crosses a box with more than LOS_CAP_F entries")
+            item_box.append(b)
+            item_seg.append(s)
+            s = e
+    item_seg.append(nseg)
+    # partial slots in line-major order (boxes ascending within a line)
+    olm = np.lexsort((seg_box, seg_los))
+    seg_slot = np.empty(nseg, dtype=np.int32)
+    seg_slot[olm] = np.arange(nseg, dtype=np.int32)
+    los_ptr = np.r_[0, np.cumsum(np.bincount(seg_los, minlength=nlos))].astype(np.int32)
+    # ---- adjoint: entries sorted by (box, local pixel)
+    key2 = box * BOX + loc
+    oa = np.argsort(key2, kind="stable")
+    if entcnt.max(initial=0) >= 65536:
+        raise ValueError("more than 65535 LOS entries in one 256-pixel box")
+    pc = np.bincount(key2, minlength=nbox * BOX).reshape(nbox, BOX)
+    pix_off = np.zeros((nbox, BOX + 1), dtype=np.uint16)
+    pix_off[:, 1:] = np.cumsum(pc, axis=1)
+    # lines crossing each box (= the forward segments, in (box, line) order)
+    # and each adjoint entry's index into its box's list
+    box_lptr = np.r_[0, np.cumsum(segcnt)].astype(np.int32)
+    seg_id = np.searchsorted(kb[segstart], key[oa])
+    lidx = seg_id - box_lptr[box[oa]]
+    if segcnt.max(initial=0) > 65535:
+        raise ValueError("more than 65535 lines of sight cross one 256-pixel box")
+    lidx8 = segcnt.max(initial=0) <= 256
+    wf = np.asarray(w, dtype=np.float32)
+    return dict(H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
+                nitems=len(item_box), nseg=nseg, L=L,
+                item_box=np.asarray(item_box, dtype=np.int32), item_seg=np.asarray(item_seg, dtype=np.int32),
+                seg_ent=seg_ent, seg_slot=seg_slot, ent_loc=loc[of].astype(np.uint8), ent_wf=wf[of],
+                los_ptr=los_ptr, box_ent=np.r_[0, np.cumsum(entcnt)].astype(np.int32), pix_off=pix_off,
+                box_lptr=box_lptr, box_lines=seg_los.astype(np.int32),
+                ent_lidx=lidx.astype(np.uint8 if lidx8 else np.uint16), lidx8=int(lidx8), ent_wa=wf[oa])
+
+
+def box_plan_apply(P, x, mode):
+    """numpy restatement of the nft_los kernels' arithmetic on a box plan
+    (host-side check of the layout; tests only)."""
+    nlos = P["nlos"]
+    H, W, bh, bw, nby, nbx = P["H"], P["W"], P["bh"], P["bw"], P["nby"], P["nbx"]
+    t = np.arange(BOX)
+    ly, lx = t // bw, t % bw
+
+    def pix(b):
+        lyr, r = divmod(b, nby * nbx)
+        by, bx = divmod(r, nbx)
+        yy, xx = by * bh + ly, bx * bw + lx
+        ok = (yy < H) & (xx < W)
+        return (lyr * H + yy) * W + xx, ok
+    if mode == "times":
+        x = x.reshape(-1)
+        part = np.zeros(P["nseg"])
+        for i in range(P["nitems"]):
+            p, ok = pix(int(P["item_box"][i]))
+            u = np.where(ok, x[np.where(ok, p, 0)], 0.)
+            for s in range(P["item_seg"][i], P["item_seg"][i + 1]):
+                acc = 0.
+                for k in range(P["seg_ent"][s], P["seg_ent"][s + 1]):
+                    acc += float(P["ent_wf"][k]) * u[P["ent_loc"][k]]
+                part[P["seg_slot"][s]] = acc
+        return np.array([part[P["los_ptr"][i]:P["los_ptr"][i + 1]].sum() for i in range(nlos)])
+    out = np.zeros(P["L"] * H * W)
+    for b in range(P["nbox"]):
+        p, ok = pix(b)
+        e0 = P["box_ent"][b]
+        for tt in range(BOX):
+            if not ok[tt]:
+                continue
+            acc = 0.
+            lines = P["box_lines"][P["box_lptr"][b]:P["box_lptr"][b + 1]]
+            for k in range(e0 + P["pix_off"][b, tt], e0 + P["pix_off"][b, tt + 1]):
+                acc += float(P["ent_wa"][k]) * x[lines[P["ent_lidx"][k]]]
+            out[p[tt]] = acc
+    return out
 
 
 class LOSResponse(LinearOperator):
@@ -149,24 +275,62 @@ class LOSResponse(LinearOperator):
         sp = self.domain[0]
         rows, cols, w, nlos = los_coo(sp.shape, sp.distances, starts, ends, sigmas, truncation)
         self._coo = (rows, cols, w)
-        npix = sp.size
-        dev = config.device()
-        p, c, ww = _csr(rows, cols, w, nlos)
-        self._fwd = tuple(torch.from_numpy(a).to(dev) for a in (p, c, ww))
-        p, c, ww = _csr(cols, rows, w, npix)
-        self._adj = tuple(torch.from_numpy(a).to(dev) for a in (p, c, ww))
         self._target = DomainTuple.make(UnstructuredDomain(nlos))
+        self._plan_np = box_plan(rows, cols, w, sp.shape, nlos)
+        self._plan = None
+
+    def _box_plan(self):
+        """Device copy of the box-blocked layout + its ctypes descriptor."""
+        if self._plan is None:
+            P = self._plan_np
+            dev = config.device()
+            keep = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+                    for k, v in P.items() if isinstance(v, np.ndarray)}
+            d = _native.LosPlan()
+            for k in ("H", "W", "bh", "bw", "nby", "nbx", "nbox", "nlos", "nitems", "nseg", "lidx8"):
+                setattr(d, k, int(P[k]))
+            for k, v in keep.items():
+                setattr(d, k, v.data_ptr() if v.numel() else None)
+            self._plan = (d, keep)
+        return self._plan[0]
 
     def apply(self, x, mode):
         self._check_input(x, mode)
         v = x.val.reshape(-1).contiguous()
+        plan = self._box_plan()
         if mode == self.TIMES:
             y = torch.empty(self._target.shape, dtype=v.dtype, device=v.device)
-            _native.spmv_csr(*self._fwd, v, y)
+            _native.los_forward(plan, v, y)
             return Field(self._target, y)
         y = torch.empty(self._domain.shape, dtype=v.dtype, device=v.device)
-        _native.spmv_csr(*self._adj, v, y.view(-1))
+        _native.los_adjoint(plan, v, y.view(-1))
         return Field(self._domain, y)
+
+    def fused_middle(self, dr, c, fct=1.0):
+        """Callable s -> fct * dr * R^T (c * R (dr * s)) on grid tensors: the
+        middle of a sampling metric J^T D R^T C R D J with pixel-space diagonal
+        dr (tensor or None) and data-space weight c (tensor or float) fused
+        into the two SpMV kernels (column / row scales)."""
+        nlos = self._target.shape[0]
+        shape = self._domain.shape
+        drf = None if dr is None else dr.reshape(-1).contiguous()
+        scale = float(fct)
+        cv = None
+        if torch.is_tensor(c):
+            cv = c.reshape(-1).expand(nlos).contiguous()
+        else:
+            scale *= float(c)
+
+        plan = self._box_plan()
+
+        def middle(s):
+            v = s.reshape(-1).contiguous()
+            y = torch.empty(nlos, dtype=v.dtype, device=v.device)
+            _native.los_forward(plan, v, y, colscale=drf, rowscale=cv, scale=scale)
+            out = torch.empty(shape, dtype=v.dtype, device=v.device)
+            _native.los_adjoint(plan, y, out.view(-1), rowscale=drf)
+            return out
+        return middle
 
     @property
     def coo(self):

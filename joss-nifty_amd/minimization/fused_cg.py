@@ -14,6 +14,7 @@ All scalars stay on the device; one 16-double D2H read per iteration feeds the
 host-side controller, exactly as the reference decides on host floats.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -22,6 +23,9 @@ from .. import _native
 from ..logger import logger
 from ..packing import PackedLayout
 from .conjugate_gradient import ConjugateGradient
+
+
+USE_GRAPHS = os.environ.get("NFT_NO_GRAPH") is None
 
 
 def fusable_metric(A):
@@ -124,16 +128,40 @@ class FusedCG:
         if gamma == 0:
             return energy, ctl.CONVERGED
 
-        ii = 0
-        while True:
+        def body(with_dir):
+            s_ = _native.stream_ptr()
+            if with_dir:
+                chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), s_))
             core.metric_flat(d, q, self.W, self.shift)
-            chk(lib.nft_dot(P(d), P(q), n, dt, P(sc[_native.CG_CURV:]), P(ws), sp))
+            chk(lib.nft_dot(P(d), P(q), n, dt, P(sc[_native.CG_CURV:]), P(ws), s_))
+            chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, P(sc), P(ws), s_))
+
+        graph = None
+        ii = 0
+        first = True
+        while True:
             self.niter += 1
             ConjugateGradient.iterations_total += 1
             ii += 1
             if ii < self.nreset:
-                chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, P(sc), P(ws), sp))
+                if first or not USE_GRAPHS:
+                    body(not first)
+                elif graph is None:
+                    # capture dir + matvec + dot + update once (HIP graph); the
+                    # eager first iteration has warmed every workspace/twiddle cache
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph):
+                        body(True)
+                    graph.replay()
+                else:
+                    graph.replay()
+                first = False
             else:
+                if not first:
+                    chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), sp))
+                first = False
+                core.metric_flat(d, q, self.W, self.shift)
+                chk(lib.nft_dot(P(d), P(q), n, dt, P(sc[_native.CG_CURV:]), P(ws), sp))
                 gp = sc[_native.CG_GAMMA].clone()
                 chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, P(sc), P(ws), sp))
                 if ax is None:
@@ -176,4 +204,3 @@ class FusedCG:
             status = ctl.check(state)
             if status != ctl.CONTINUE:
                 return self._energy(A, b_mf, x, r), status
-            chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), sp))

@@ -51,6 +51,51 @@ def _pointwise_weight(ops, cheese):
     return w
 
 
+def _pointwise_diag(ops):
+    """Product of the (real) diagonals of `ops` (tensor, float or None = 1),
+    or False if any factor is not pointwise."""
+    from .simple_linear_operators import GeometryRemover
+    d = None
+    for op in ops:
+        if isinstance(op, ScalingOperator):
+            f = complex(op._factor)
+            if f.imag != 0:
+                return False
+            d = f.real if d is None else d * f.real
+        elif isinstance(op, DiagonalOperator):
+            if op._complex:
+                return False
+            t = op.diagonal_tensor
+            d = t if d is None else d * t
+        elif isinstance(op, GeometryRemover):
+            continue
+        else:
+            return False
+    return d
+
+
+def _fused_response_middle(left, cheese, fct):
+    """Middle M^T C M for left = [data-side pointwise..., R, grid-side
+    pointwise...] with R providing `fused_middle` (LOSResponse), else None."""
+    ir = [i for i, op in enumerate(left) if hasattr(op, "fused_middle")]
+    if len(ir) != 1:
+        return None
+    i = ir[0]
+    c = _pointwise_weight(left[:i], cheese)
+    dr = _pointwise_diag(left[i + 1:])
+    if c is None or dr is False:
+        return None
+    if dr is not None and not torch.is_tensor(dr):
+        fct *= float(dr) ** 2
+        dr = None
+    R = left[i]
+    if dr is not None and dr.numel() != R.domain.size:
+        return None
+    if torch.is_tensor(c) and c.numel() not in (1, R.target.size):
+        return None
+    return R.fused_middle(dr, c, fct)
+
+
 class SandwichOperator(EndomorphicOperator):
     def __init__(self, bun, cheese, op, _callingfrommake=False):
         if not _callingfrommake:
@@ -86,6 +131,10 @@ class SandwichOperator(EndomorphicOperator):
             for op in right:
                 fct *= complex(op._factor).real ** 2
             left = ops[:cores[0]]
+            fm = _fused_response_middle(left, self._cheese, fct)
+            if fm is not None:
+                self._fused = (core, fm)
+                return
             mid = ChainOperator.make(left) if len(left) > 0 else None
             cheese = self._cheese
             tgt = core.target

@@ -296,6 +296,55 @@ def gen_poisson():
     _save("poisson64.npz", d)
 
 
+def gen_los_metric():
+    """Config C3 flavour (sigmoid(cf) observed through LOSResponse, Gaussian
+    noise) at 64^2 with 300 lines of sight: sampling-metric matvec and short
+    MGVI / geoVI draws (kl_energies.py:64-133)."""
+    pos_space = ift.RGSpace((64, 64))
+    cf = ift.SimpleCorrelatedField(pos_space, **CF_ARGS)
+    signal = ift.sigmoid(cf)
+    ift.random.push_sseq_from_seed(27)
+    rng = ift.random.current_rng()
+    starts = rng.random((300, 2)).T
+    ends = rng.random((300, 2)).T
+    R = ift.LOSResponse(pos_space, starts=list(starts), ends=list(ends))
+    sr = R(signal)
+    N = ift.ScalingOperator(R.target, 1e-3, np.float64)
+    mock = ift.from_random(sr.domain, "normal")
+    data = sr(mock) + N.draw_sample()
+    pos = 0.1 * ift.from_random(sr.domain, "normal")
+    ift.random.pop_sseq()
+    lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ sr
+    d = {"starts": starts, "ends": ends, "data": data.val}
+    for k, v in _flat(pos).items():
+        d["pos_" + k] = v
+    dtype, f_lh = lh.get_transformation()
+    fl = f_lh(ift.Linearization.make_var(pos))
+    met = ift.SandwichOperator.make(fl.jac, ift.ScalingOperator(f_lh.target, 1., dtype)) \
+        + ift.ScalingOperator(fl.domain, 1., float)
+    with ift.random.Context(5):
+        v = ift.from_random(fl.domain, "normal")
+    for k, val in _flat(v).items():
+        d["v_" + k] = val
+    for k, val in _flat(met(v)).items():
+        d["mv_" + k] = val
+    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=6))
+    ift.random.push_sseq_from_seed(31)
+    sl = ift.minimization.kl_energies.draw_samples(pos, H, None, 1, True)
+    ift.random.pop_sseq()
+    for i, r in enumerate(sl._r):
+        for k, val in _flat(r).items():
+            d[f"lin{i}_" + k] = val
+    mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=1))
+    ift.random.push_sseq_from_seed(31)
+    sl = ift.minimization.kl_energies.draw_samples(pos, H, mini, 1, True)
+    ift.random.pop_sseq()
+    for i, r in enumerate(sl._r):
+        for k, val in _flat(r).items():
+            d[f"r{i}_" + k] = val
+    _save("losmetric64.npz", d)
+
+
 def gen_los():
     """LOSResponse construction + matvec/rmatvec (los_response.py:34-233)."""
     d = {}
@@ -348,4 +397,5 @@ if __name__ == "__main__":
     gen_draw_samples()
     gen_poisson()
     gen_los()
+    gen_los_metric()
     gen_random()

@@ -107,6 +107,36 @@ def test_los_construction_bit_exact():
         np.testing.assert_array_equal(w, G[f"l{i}_wgt"])
 
 
+@pytest.mark.parametrize("i", range(3))
+def test_los_box_plan_layout(i):
+    """The box-blocked layout the nft_los kernels consume reproduces the
+    reference's COO matvec / rmatvec (golden COO + vectors, los.npz), via a
+    numpy restatement of the kernels' arithmetic; plus a forced split of
+    over-full boxes into several work items."""
+    import scipy.sparse
+    from nifty_amd.library import los_response as lr
+    G = golden("los.npz")
+    shape = tuple(int(s) for s in G[f"l{i}_shape"])
+    rows, cols, w = G[f"l{i}_row"], G[f"l{i}_col"], G[f"l{i}_wgt"]
+    nlos = len(G[f"l{i}_y"])
+    P = lr.box_plan(rows, cols, w, shape, nlos)
+    assert P["item_seg"][-1] == P["nseg"] and P["box_ent"][-1] == len(rows)
+    assert np.all(np.diff(P["item_seg"]) <= lr.BOX)
+    assert np.all(P["seg_ent"][P["item_seg"][1:]] - P["seg_ent"][P["item_seg"][:-1]] <= lr.LOS_CAP_F)
+    x, y = G[f"l{i}_x"], G[f"l{i}_y"]
+    assert np.allclose(lr.box_plan_apply(P, x, "times"), G[f"l{i}_Rx"], rtol=1e-13, atol=0)
+    assert np.allclose(lr.box_plan_apply(P, y, "adjoint"), G[f"l{i}_Rty"].ravel(), rtol=1e-13, atol=1e-300)
+    old = lr.LOS_CAP_F
+    try:
+        lr.LOS_CAP_F = 40
+        P2 = lr.box_plan(rows, cols, w, shape, nlos)
+        assert P2["nitems"] > P["nitems"]
+        assert np.allclose(lr.box_plan_apply(P2, x, "times"), G[f"l{i}_Rx"], rtol=1e-13, atol=0)
+    finally:
+        lr.LOS_CAP_F = old
+    del scipy
+
+
 def test_controllers_semantics():
     import nifty_amd as ift
 
