@@ -152,9 +152,13 @@ def main():
                         max_cg_iterations=args.newton_cg_max)
     nsamp = args.samples_per_gpu * ws
 
+    # one seeded stream for the whole run, each step spawning its sample seeds
+    # from it -- the way optimize_kl drives SampledKLEnergy (optimize_kl.py,
+    # kl_energies.py:131)
+    ift.random.push_sseq_from_seed(1000)
+
     def step(i):
-        with ift.random.Context(1000 + i):
-            sl = ift.draw_samples(pos, H, mini, nsamp, True, comm=comm)
+        sl = ift.draw_samples(pos, H, mini, nsamp, True, comm=comm)
         kl = ift.SampledKLEnergyClass(sl, H, [], None, True)
         return kl
 

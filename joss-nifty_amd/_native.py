@@ -132,8 +132,17 @@ def require_device(*tensors):
             raise NativeError("nifty_amd hot-path ops need contiguous tensors")
 
 
+_stream_ok = False
+
+
 def stream_ptr():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """hipStream_t of torch's current stream on the current device (raw query:
+    torch.cuda.current_stream() re-runs lazy-init checks on every call)."""
+    global _stream_ok
+    if not _stream_ok:
+        torch.cuda.init()
+        _stream_ok = True
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice()))
 
 
 def ptr(t):

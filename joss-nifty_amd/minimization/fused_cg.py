@@ -75,9 +75,13 @@ def fused_cg_or_none(energy, controller, nreset):
         return None
     spec = fusable_metric(energy.metric)
     if spec is None:
-        return None
+        from ..lowering import lowered_metric
+        lm = lowered_metric(energy.metric)
+        if lm is None:
+            return None
+        spec = (lm, None, 0.0)
     core, W, shift = spec
-    if energy.position.domain is not core.domain or not core.device.type == "cuda":
+    if energy.position.domain != core.domain or not core.device.type == "cuda":
         return None
     return FusedCG(core, W, shift, controller, nreset).run(energy)
 

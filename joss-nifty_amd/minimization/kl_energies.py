@@ -50,6 +50,7 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
     else:
         met = H(Linearization.make_var(sam_position, want_metric=True)).metric
 
+    parent = random._sseq[-1]
     sseq = random.spawn_sseq(n_samples)
     if mirror_samples:
         sseq = reduce(lambda a, b: a + b, [[ss] * 2 for ss in sseq]) if n_samples > 0 else []
@@ -57,11 +58,23 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
     utilities.check_MPI_synced_random_state(comm)
     y = None
     ntask, rank, _ = get_MPI_params_from_comm(comm)
-    for i in range(*shareRange(len(sseq), ntask, rank)):
-        with random.Context(sseq[i]):
+    lo, hi = shareRange(len(sseq), ntask, rank)
+    prefetched = False
+    for i in range(lo, hi):
+        ctx = random.Context(sseq[i])
+        with ctx:
             neg = mirror_samples and (i % 2 != 0)
             if not neg or y is None:
                 y, yi = met.special_draw_sample(True)
+                if not prefetched:
+                    # host RNG off the critical path: replay this sample's draws
+                    # for the remaining local seeds and the next call's seeds
+                    prefetched = True
+                    nxt = random.predict_spawn(n_samples, parent)
+                    if mirror_samples:
+                        nxt = [ss for ss in nxt for _ in range(2)]
+                    todo = _distinct([ss for ss in sseq[i + 1:hi] if ss is not sseq[i]]) + _distinct(nxt[lo:hi])
+                    random.prefetch(todo, ctx.script)
             if geometric:
                 m = transformation_mean - y if neg else transformation_mean + y
                 pos = sam_position - yi if neg else sam_position + yi
@@ -74,6 +87,15 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
                 local_samples.append(yi)
                 local_neg.append(neg)
     return ResidualSampleList(position, local_samples, local_neg, comm)
+
+
+def _distinct(seqs):
+    out, seen = [], set()
+    for ss in seqs:
+        if id(ss) not in seen:
+            seen.add(id(ss))
+            out.append(ss)
+    return out
 
 
 def SampledKLEnergy(position, hamiltonian, n_samples, minimizer_sampling, mirror_samples=True,

@@ -3,9 +3,22 @@
 Same semantics as src/random.py:84-291 (push/pop, spawn_sseq, Context), so a
 given seed produces the identical stream of normals as the reference.  Draws
 are made on the host with numpy (bit-compatibility, SURVEY.md §7 "hard parts")
-and uploaded to the device by Field.from_random; the sampler overlaps this
-host work with GPU solves (minimization/kl_energies.py).
+and uploaded to the device by Field.from_random.
+
+Host draws are the one part of sampling that does not run on the GPU (4M
+normals take ~45 ms on one core), so they are taken off the critical path:
+every Context records the draws made in it (a "script"); draw_samples asks
+``prefetch`` to replay that script on a background thread for the seed
+sequences it will use next (the remaining local samples, and the children the
+next spawn_sseq call will produce).  A Context entered with a prefetched seed
+serves the pre-drawn arrays while the requests match the script, and
+otherwise rebuilds the exact generator state (re-drawing what it served) and
+continues from the generator: results are bit-identical either way; a wrong
+prediction only costs background CPU time.
 """
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 
 _sseq = [np.random.SeedSequence(42)]
@@ -92,6 +105,131 @@ class Random:
         return x.astype(dtype, copy=False)
 
 
+# ------------------------------------------------------------- prefetching
+_RECORDED = ("normal", "uniform", "integers")
+
+
+def _req(method, args, kwargs):
+    def norm(v):
+        if isinstance(v, (list, tuple)):
+            return tuple(int(a) for a in v)
+        if isinstance(v, (np.integer, int)):
+            return int(v)
+        if isinstance(v, (np.floating, float)):
+            return float(v)
+        if isinstance(v, type):
+            return v.__name__
+        return v
+    return (method, tuple(norm(a) for a in args), tuple(sorted((k, norm(v)) for k, v in kwargs.items())))
+
+
+def _sseq_key(ss):
+    return (repr(ss.entropy), tuple(ss.spawn_key), ss.pool_size)
+
+
+class _Recorder:
+    """Generator proxy that logs the recorded draw requests of a Context."""
+
+    def __init__(self, gen):
+        self._gen = gen
+        self.script = []
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        attr = getattr(self._gen, name)
+        if name in _RECORDED:
+            def rec(*args, **kwargs):
+                if self.script is not None:
+                    self.script.append(_req(name, args, kwargs))
+                return attr(*args, **kwargs)
+            return rec
+        self.script = None  # an unrecorded draw: the script cannot be replayed
+        return attr
+
+
+class _Serving:
+    """Generator proxy that serves prefetched draws while requests match."""
+
+    def __init__(self, sseq, script, arrays):
+        self._sseq = sseq
+        self._script, self._arrays = script, arrays
+        self._pos = 0
+        self._gen = None
+        self.script = []
+
+    def _materialize(self):
+        if self._gen is None:
+            g = np.random.default_rng(self._sseq)
+            for (name, args, kw) in self._script[:self._pos]:
+                getattr(g, name)(*args, **dict(kw))
+            self._gen = g
+        return self._gen
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        if self._gen is None and name in _RECORDED:
+            def serve(*args, **kwargs):
+                r = _req(name, args, kwargs)
+                if self.script is not None:
+                    self.script.append(r)
+                if self._gen is None and self._pos < len(self._script) and self._script[self._pos] == r:
+                    self._pos += 1
+                    return self._arrays[self._pos - 1]
+                return getattr(self._materialize(), name)(*args, **kwargs)
+            return serve
+        if name not in _RECORDED:
+            self.script = None
+        return getattr(self._materialize(), name)
+
+
+_pool = None
+_cache = {}
+_lock = threading.Lock()
+last_script = None
+
+
+def _run_script(sseq, script):
+    g = np.random.default_rng(sseq)
+    return [getattr(g, name)(*args, **dict(kw)) for (name, args, kw) in script]
+
+
+def predict_spawn(n, parent=None):
+    """The SeedSequences the next spawn_sseq(n, parent) call will return,
+    without spawning."""
+    if parent is None:
+        parent = _sseq[-1]
+    k0 = parent.n_children_spawned
+    return [np.random.SeedSequence(parent.entropy, spawn_key=tuple(parent.spawn_key) + (k0 + i,),
+                                   pool_size=parent.pool_size) for i in range(n)]
+
+
+def prefetch(sseqs, script):
+    """Replay `script` for each SeedSequence in the background."""
+    global _pool
+    if not script:
+        return
+    if _pool is None:
+        _pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="nft-rng")
+    with _lock:
+        for ss in sseqs:
+            key = _sseq_key(ss)
+            if key not in _cache:
+                _cache[key] = (list(script), _pool.submit(_run_script, ss, list(script)))
+        while len(_cache) > 16:
+            _cache.pop(next(iter(_cache)))
+
+
+def _take(sseq):
+    with _lock:
+        ent = _cache.pop(_sseq_key(sseq), None)
+    if ent is None:
+        return None
+    script, fut = ent
+    return script, fut.result()
+
+
 class Context:
     """``with Context(seed_or_sseq): ...`` scoped RNG state (random.py:261-291)."""
 
@@ -102,10 +240,24 @@ class Context:
 
     def __enter__(self):
         self._depth = len(_sseq)
-        push_sseq(self._sseq)
+        pre = _take(self._sseq)
+        _sseq.append(self._sseq)
+        if pre is None:
+            self._proxy = _Recorder(np.random.default_rng(self._sseq))
+        else:
+            self._proxy = _Serving(self._sseq, *pre)
+        _rng.append(self._proxy)
 
     def __exit__(self, exc_type, exc_value, tb):
+        global last_script
         pop_sseq()
         if self._depth != len(_sseq):
             raise RuntimeError("inconsistent RNG usage detected")
+        if self._proxy.script:
+            last_script = self._proxy.script
         return exc_type is None
+
+    @property
+    def script(self):
+        """draw requests made so far in this context (None if not replayable)"""
+        return self._proxy.script

@@ -205,3 +205,48 @@ def test_cf_amplitude_cpu_matches_golden():
     lat = {k: torch.from_numpy(np.array(G["x_" + k])) for k in cf.amplitude.domain.keys()}
     a, c = cf.amp.forward(lat)
     assert np.max(np.abs(a.numpy() - G["amp"])) <= 1e-14 * np.max(np.abs(G["amp"]))
+
+
+def test_rng_prefetch_bit_identical():
+    """Prefetched draws (random.prefetch) equal direct draws; a request that
+    leaves the recorded script rebuilds the exact generator state."""
+    from nifty_amd import random as R
+    R.push_sseq_from_seed(123)
+    try:
+        kids = R.predict_spawn(3)
+        ref = []
+        spawned = R.spawn_sseq(3)
+        assert [k.spawn_key for k in kids] == [k.spawn_key for k in spawned]
+        for ss in spawned:
+            with R.Context(ss):
+                a = R.Random.normal(np.float64, (50, 7))
+                b = R.Random.uniform(np.float64, (5,))
+                c = R.Random.normal(np.float64, (3,))
+            ref.append((a, b, c))
+        script = [("normal", (0.0, 1.0, (50, 7)), ()), ("uniform", (0.0, 1.0, (5,)), ())]
+        # same seeds again: spawn from a fresh parent with the same entropy
+        R.pop_sseq()
+        R.push_sseq_from_seed(123)
+        nxt = R.predict_spawn(3)
+        R.prefetch(nxt, script)
+        out = []
+        for ss in R.spawn_sseq(3):
+            ctx = R.Context(ss)
+            with ctx:
+                a = R.Random.normal(np.float64, (50, 7))
+                b = R.Random.uniform(np.float64, (5,))
+                c = R.Random.normal(np.float64, (3,))   # beyond the script: generator rebuilt
+            out.append((a, b, c))
+            assert ctx.script[0][0] == "normal"
+        for (a, b, c), (x, y, z) in zip(ref, out):
+            np.testing.assert_array_equal(a, x)
+            np.testing.assert_array_equal(b, y)
+            np.testing.assert_array_equal(c, z)
+        # mismatching first request: falls back to the generator
+        R.prefetch(R.predict_spawn(1), script)
+        ss = R.spawn_sseq(1)[0]
+        with R.Context(ss):
+            u = R.Random.uniform(np.float64, (4,))
+        np.testing.assert_array_equal(u, np.random.default_rng(ss).uniform(0., 1., (4,)))
+    finally:
+        R.pop_sseq()
