@@ -89,31 +89,83 @@ def build_problem(ift, n, nlos):
     return cf, R, lh, pos, (starts, ends)
 
 
-def roofline_probe(ift, cf, n, reps=20):
-    """Average duration of the dominant kernel family (the Hartley passes of
-    the sampling-metric matvec: R2C rows + C2C/unpack columns at n x n fp64),
-    timed with HIP events on the stream the kernels are launched on."""
+def kernel_probe(ift, cf, R, lh, pos, reps=10):
+    """Per-kernel durations of one sampling-metric matvec M d = d + J^T W J d at
+    the bench expansion point -- the matvec the timed CG loop runs -- measured
+    with HIP events recorded on the launch stream before every hot-path launch
+    (nft_prof_*; the same kernels with the same arguments as inside the timed
+    region, run eagerly because events cannot be timed inside a HIP graph).
+
+    Returns {label: {"launches": per matvec, "avg_us", "bytes": algorithmic
+    bytes per launch, "gbs"}} with the algorithmic-byte model of DESIGN.md
+    §Measurement (every operand array counted once per launch, fp64)."""
     from nifty_amd import _native
-    x = torch.randn((n, n), dtype=torch.float64, device="cuda")
-    out = torch.empty_like(x)
+    from nifty_amd.minimization.fused_cg import fusable_metric
+    # the linear geoVI sampling metric exactly as draw_samples builds it
+    # (kl_energies.py:147-153): 1 + J^T J of the likelihood's transformation
+    dtype, f_lh = lh.get_transformation()
+    fl = f_lh(ift.Linearization.make_var(pos))
+    met = (ift.SandwichOperator.make(fl.jac, ift.ScalingOperator(f_lh.target, 1., dtype))
+           + ift.ScalingOperator(fl.domain, 1., float))
+    spec = fusable_metric(met)
+    assert spec is not None, "bench metric did not fuse"
+    core, W, shift = spec
+    lay = core.layout
+    d = lay.pack(ift.from_random(cf.domain, "normal"))
+    q = lay.empty()
+    # FusedCG forms q' = M' d without the identity shift (its CG kernels add
+    # shift*d element-wise), so the probe does the same
     for _ in range(3):
-        _native.hartley(x, (0, 1), out=out)
-    s = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
-        _native.hartley(x, (0, 1), out=out)
-    e1.record(s)
+        core.metric_flat(d, q, W, 0.0)
     torch.cuda.synchronize()
-    t_pair = e0.elapsed_time(e1) / reps * 1e-3          # one 2-D transform = 2 pass kernels
+    # keep the GPU busy while the probe launches are queued, so that the
+    # events bracket kernels and not host enqueue gaps
+    torch.cuda._sleep(200_000_000)
+    with _native.LaunchProfile() as prof:
+        for _ in range(reps):
+            core.metric_flat(d, q, W, 0.0)
+    acc = {}
+    for lab, ms in prof.records:
+        a = acc.setdefault(lab, [0, 0.0])
+        a[0] += 1
+        a[1] += ms
+    n = cf.target.shape[0]
     N = n * n
-    bytes_per_pass = N * 8 * 2                              # read N reals + write N/2 complex (= N reals)
-    t_pass = t_pair / 2
-    ach = bytes_per_pass / t_pass / 1e9
-    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "pass_kernel<double,*,R2C|UNPACK> (Hartley axis pass, 2048^2 fp64)",
-            "avg_launch_us": round(t_pass * 1e6, 2), "algorithmic_bytes_per_launch": bytes_per_pass}
+    Hh = n * (n // 2 + 1)
+    B = cf.amp.B
+    P = R._plan_np
+    nnz = int(P["box_ent"][-1])
+    nseg = int(P["nseg"])
+    model = {
+        "fft_r2c+pro": 3 * 8 * N + 4 * N + 8 * B + 16 * Hh,
+        "fft_r2c": 8 * N + 16 * Hh,
+        "fft_c2c": 2 * 16 * Hh,
+        "fft_unpack": 16 * Hh + 8 * N,
+        "fft_unpack+epi": 16 * Hh + 8 * N + 2 * 8 * N + 8 * N,
+        "los_fwd_items": 5 * nnz + 12 * nseg + 2 * 8 * N + 8 * nseg,
+        "los_fwd_reduce": 8 * nseg + 8 * R.target.shape[0],
+        "los_adj_boxes": 5 * nnz + 4 * nseg + 2 * 257 * int(P["nbox"]) + 2 * 8 * N,
+        "bin_scatter": 4 * N + 8 * N + 4 * B + 8 * B,
+    }
+    out = {}
+    for lab, (cnt, tot) in acc.items():
+        avg = tot / cnt * 1e3
+        by = model.get(lab)
+        out[lab] = {"launches": cnt // reps, "avg_us": round(avg, 2), "bytes": by,
+                    "gbs": round(by / (avg * 1e-6) / 1e9, 1) if by else None}
+    return out
+
+
+def roofline_of(kp):
+    """roofline object for the kernel with the largest time per matvec"""
+    lab = max(kp, key=lambda k: kp[k]["avg_us"] * kp[k]["launches"])
+    k = kp[lab]
+    if k["bytes"] is None:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernel": lab, "avg_launch_us": k["avg_us"]}
+    return {"bound": "hbm", "achieved": k["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(k["gbs"] / HBM_PEAK_GBS, 4), "traffic": None, "kernel": lab,
+            "avg_launch_us": k["avg_us"], "algorithmic_bytes_per_launch": k["bytes"]}
 
 
 def cpu_baseline(cf_np_args, lat0, R, n, iters):
@@ -181,7 +233,8 @@ def main():
     samples = 2 * nsamp * args.steps
     sps = samples / el
     cgps = iters / el
-    roof = roofline_probe(ift, cf, n) if torch.cuda.is_available() else None
+    kp = kernel_probe(ift, cf, R, lh, pos) if torch.cuda.is_available() else None
+    roof = roofline_of(kp) if kp else None
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         lat0 = {k: np.asarray(pos[k]) for k in cf.domain.keys()}
@@ -203,7 +256,7 @@ def main():
                                        f"(inner CG <= {args.newton_cg_max})",
                            "global_batch": samples // args.steps, "parallelism": f"sample-dp{ws}"},
                 "cg_iter_per_s": round(cgps, 3), "cg_iters": int(iters),
-                "roofline": roof, "cpu_baseline": cpu}
+                "roofline": roof, "cpu_baseline": cpu, "kernels": kp}
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist

@@ -88,15 +88,20 @@ size_t nft_reduce_workspace(int64_t n);
 int nft_dot(const void* a, const void* b, int64_t n, int dtype, double* out, void* ws,
             hipStream_t stream);
 int nft_scale(void* x, int64_t n, int dtype, double scale, hipStream_t stream);
-/* alpha = sc[GAMMA]/sc[CURV]; x -= alpha d; r -= alpha q; sc[GAMMA,XR,XB] <- r.r, x.r, x.b */
+/* For the metric shift*1 + M' with q = M' d formed without the shift:
+ * sc[CURV] = sum d*(q + shift*d) */
+int nft_cg_curv(const void* d, const void* q, int64_t n, int dtype, double shift, double* sc,
+                void* ws, hipStream_t stream);
+/* alpha = sc[GAMMA]/sc[CURV]; x -= alpha d; r -= alpha (q + shift d);
+ * sc[GAMMA,XR,XB] <- r.r, x.r, x.b */
 int nft_cg_update(void* x, void* r, const void* d, const void* q, const void* b, int64_t n,
-                  int dtype, double* sc, void* ws, hipStream_t stream);
+                  int dtype, double shift, double* sc, void* ws, hipStream_t stream);
 /* d = max(0, sc[GAMMA]/sc[GPREV]) d + r */
 int nft_cg_direction(void* d, const void* r, int64_t n, int dtype, const double* sc,
                      hipStream_t stream);
-/* r = ax - b; sc[GPREV] <- sc[GAMMA]; sc[GAMMA,XR,XB] <- r.r, x.r, x.b */
+/* r = (ax + shift x) - b; sc[GPREV] <- sc[GAMMA]; sc[GAMMA,XR,XB] <- r.r, x.r, x.b */
 int nft_cg_residual(void* r, const void* ax, const void* x, const void* b, int64_t n, int dtype,
-                    double* sc, void* ws, hipStream_t stream);
+                    double shift, double* sc, void* ws, hipStream_t stream);
 
 /* ---- power-bin distributor -------------------------------------------- */
 /* out[p,i,q] = in[p, pindex[i], q]; in: [pre, nbins, post], out: [pre, npix, post] */
@@ -157,7 +162,8 @@ int nft_hartley_fused(const nft_hartley_fuse* fuse, const void* in, void* out, i
  * (16x16 over the last two grid axes, 1x256 for 1-D grids; the grid is
  * viewed as [L, H, W]).  Built on the host from the COO triplets
  * (LOSResponse._box_plan); all index arrays int32 unless noted.
- *   forward:  nitems work items (box item_box[i], segments item_seg[i]..[i+1]);
+ *   forward:  nitems work items (box item_box[i], segments item_seg[i]..[i+1],
+ *             entries item_ent[i]..[i+1]);
  *             a segment is the run of one line of sight inside one box:
  *             entries seg_ent[s]..[s+1] with 8-bit local pixel ent_loc and fp32
  *             weight ent_wf; its partial goes to slot seg_slot[s]; line l owns
@@ -172,7 +178,7 @@ typedef struct nft_los_plan {
   int64_t H, W;
   int bh, bw, nby, nbx;
   int64_t nbox, nlos, nitems, nseg;
-  const int *item_box, *item_seg, *seg_ent, *seg_slot;
+  const int *item_box, *item_seg, *item_ent, *seg_ent, *seg_slot;
   const uint8_t* ent_loc;
   const float* ent_wf;
   const int* los_ptr;
@@ -222,6 +228,15 @@ int nft_amp_jvp(const nft_amp_const* c, const double* t_fl, const double* t_sl,
                 const double* t_spec, double* da, double* ws, hipStream_t stream);
 int nft_amp_vjp(const nft_amp_const* c, const double* g, const nft_amp_out* out, double* ws,
                 hipStream_t stream);
+
+/* ---- launch profiler (HIP events) -------------------------------------- */
+/* Between nft_prof_begin and nft_prof_end every hot-path kernel launch
+ * records a HIP event on its stream just before the launch; nft_prof_end
+ * returns the per-launch durations (ms) in launch order, nft_prof_label(i) the
+ * kernel family of launch i.  Not for use during HIP graph capture. */
+int nft_prof_begin(int capacity);
+int nft_prof_end(hipStream_t stream, float* ms, int cap, int* n);
+const char* nft_prof_label(int i);
 
 #ifdef __cplusplus
 }

@@ -27,9 +27,10 @@ SIGNATURES = {
     "nft_reduce_workspace": (_sz, [_i64]),
     "nft_dot": (_i, [_p, _p, _i64, _i, _p, _p, _p]),
     "nft_scale": (_i, [_p, _i64, _i, _d, _p]),
-    "nft_cg_update": (_i, [_p, _p, _p, _p, _p, _i64, _i, _p, _p, _p]),
+    "nft_cg_curv": (_i, [_p, _p, _i64, _i, _d, _p, _p, _p]),
+    "nft_cg_update": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _p, _p, _p]),
     "nft_cg_direction": (_i, [_p, _p, _i64, _i, _p, _p]),
-    "nft_cg_residual": (_i, [_p, _p, _p, _p, _i64, _i, _p, _p, _p]),
+    "nft_cg_residual": (_i, [_p, _p, _p, _p, _i64, _i, _d, _p, _p, _p]),
     "nft_bin_gather": (_i, [_p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_bin_scatter": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
@@ -40,6 +41,9 @@ SIGNATURES = {
     "nft_los_workspace": (_sz, [_p]),
     "nft_los_forward": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _p]),
     "nft_los_adjoint": (_i, [_p, _p, _p, _p, _p, _i, _d, _p]),
+    "nft_prof_begin": (_i, [_i]),
+    "nft_prof_end": (_i, [_p, _p, _i, ctypes.POINTER(_i)]),
+    "nft_prof_label": (ctypes.c_char_p, [_i]),
     "nft_amp_workspace": (_sz, [_i64]),
     "nft_amp_jvp": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "nft_amp_vjp": (_i, [_p, _p, _p, _p, _p]),
@@ -56,7 +60,7 @@ class LosPlan(ctypes.Structure):
     """nft_los_plan (include/nifty_amd.h)."""
     _fields_ = [("H", _i64), ("W", _i64), ("bh", _i), ("bw", _i), ("nby", _i), ("nbx", _i),
                 ("nbox", _i64), ("nlos", _i64), ("nitems", _i64), ("nseg", _i64)] + \
-               [(n, _p) for n in ("item_box", "item_seg", "seg_ent", "seg_slot", "ent_loc", "ent_wf",
+               [(n, _p) for n in ("item_box", "item_seg", "item_ent", "seg_ent", "seg_slot", "ent_loc", "ent_wf",
                                   "los_ptr", "box_ent", "pix_off", "box_lptr", "box_lines", "ent_lidx")] + \
                [("lidx8", _i), ("ent_wa", _p)]
 
@@ -330,3 +334,24 @@ def amp_vjp(const, g, out):
     require_device(g)
     ws = workspace(lib.nft_amp_workspace(const.B), g.device, "amp")
     _check(lib.nft_amp_vjp(ctypes.byref(const), ptr(g), ctypes.byref(out), ptr(ws), stream_ptr()))
+
+
+class LaunchProfile:
+    """``with LaunchProfile() as p: ...`` -> p.records = [(label, ms), ...] for
+    every hot-path kernel launched inside (HIP events on the launch stream)."""
+
+    def __init__(self, capacity=4096):
+        self.capacity = capacity
+        self.records = []
+
+    def __enter__(self):
+        _check(load().nft_prof_begin(self.capacity))
+        return self
+
+    def __exit__(self, *exc):
+        lib = load()
+        ms = (ctypes.c_float * self.capacity)()
+        n = ctypes.c_int(0)
+        _check(lib.nft_prof_end(stream_ptr(), ms, self.capacity, ctypes.byref(n)))
+        self.records = [(lib.nft_prof_label(i).decode(), float(ms[i])) for i in range(n.value)]
+        return False

@@ -52,6 +52,9 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
       attr_set = true;
     }
   }
+  static const char* const kind_name[4] = {"fft_c2c", "fft_r2c", "fft_h1d", "fft_unpack"};
+  static const char* const kind_fused[4] = {"fft_c2c", "fft_r2c+pro", "fft_h1d+fused", "fft_unpack+epi"};
+  prof_mark(s, (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
   hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS>), dim3((unsigned)ntiles), dim3(NT), lds, s, a);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;

@@ -398,10 +398,14 @@ int nft_amp_jvp(const nft_amp_const* cst, const double* tfl, const double* tsl, 
   const int nbB = nblk(B, ABLK);
   double* part = tot2 + nbM + 1;
   if (c.has_flex) {
+    prof_mark(s, "amp_jvp_1");
     hipLaunchKernelGGL(amp_jvp_1, dim3(nbM), dim3(AT), 0, s, c, tspec, loc, tot1);
+    prof_mark(s, "amp_jvp_3");
     hipLaunchKernelGGL(amp_jvp_3, dim3(nbM), dim3(AT), 0, s, c, tspec, tot1, loc, tot2);
   }
+  prof_mark(s, "amp_jvp_5");
   hipLaunchKernelGGL(amp_jvp_5, dim3(nbB), dim3(AT), 0, s, c, tfl, tsl, tflex, tasp, loc, tot2, dapre, part);
+  prof_mark(s, "amp_jvp_7");
   hipLaunchKernelGGL(amp_jvp_7, dim3(nblk(B, AT) < 1024 ? nblk(B, AT) : 1024), dim3(AT), 0, s, c, tfl, tzm,
                      dapre, part, nbB, da);
   NFT_HIP_CHECK(hipGetLastError());
@@ -422,13 +426,19 @@ int nft_amp_vjp(const nft_amp_const* cst, const double* g, const nft_amp_out* ou
   double* tot3 = part23 + 2 * nr + 2;
   double* tot4 = tot3 + nbM + 1;
   double* part45 = tot4 + nbM + 1;
+  prof_mark(s, "amp_vjp_1");
   hipLaunchKernelGGL(amp_vjp_1, dim3(nr), dim3(AT), 0, s, c, g, part1);
+  prof_mark(s, "amp_vjp_2");
   hipLaunchKernelGGL(amp_vjp_2, dim3(nr), dim3(AT), 0, s, c, g, part1, nr, gapre, part23);
   if (c.has_flex) {
+    prof_mark(s, "amp_vjp_3");
     hipLaunchKernelGGL(amp_vjp_3, dim3(nbM), dim3(AT), 0, s, c, gapre, part23, nr, loc, tot3);
+    prof_mark(s, "amp_vjp_4");
     hipLaunchKernelGGL(amp_vjp_4, dim3(nbM), dim3(AT), 0, s, c, gapre, part23, nr, tot3, y, loc, tot4);
+    prof_mark(s, "amp_vjp_5");
     hipLaunchKernelGGL(amp_vjp_5, dim3(nbM), dim3(AT), 0, s, c, o, y, loc, tot4, part45);
   }
+  prof_mark(s, "amp_vjp_6");
   hipLaunchKernelGGL(amp_vjp_6, dim3(1), dim3(AT), 0, s, c, o, g, part1, nr, part23, nr, part45,
                      c.has_flex ? nbM : 0);
   NFT_HIP_CHECK(hipGetLastError());

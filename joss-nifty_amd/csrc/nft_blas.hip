@@ -68,6 +68,23 @@ __global__ __launch_bounds__(RED_NT) void dot_partial(const T* __restrict__ a, c
   if (threadIdx.x == 0) part[blockIdx.x] = v[0];
 }
 
+// partial sums of d.(q + shift*d): the curvature of a CG step for the metric
+// shift*1 + M' when only q = M' d was formed (the shift never touches HBM)
+template <typename T>
+__global__ __launch_bounds__(RED_NT) void curv_partial(const T* __restrict__ d, const T* __restrict__ q,
+                                                       long long n, T shift, double* __restrict__ part) {
+  __shared__ double sh[RED_NT / 64];
+  double v[1] = {0.0};
+  const long long stride = (long long)gridDim.x * RED_NT;
+  for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
+    const T di = d[i];
+    const T qi = q[i] + shift * di;
+    v[0] += (double)di * (double)qi;
+  }
+  block_sum<1>(v, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = v[0];
+}
+
 // fold `nb` partial vectors of width W (layout part[k*nb + b]) into out[k]
 template <int W>
 __global__ __launch_bounds__(RED_NT) void fold_partials(const double* __restrict__ part, int nb,
@@ -114,7 +131,7 @@ template <typename T>
 __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T* __restrict__ r,
                                                            const T* __restrict__ d,
                                                            const T* __restrict__ q,
-                                                           const T* __restrict__ b, long long n,
+                                                           const T* __restrict__ b, long long n, T shift,
                                                            const double* __restrict__ sc,
                                                            double* __restrict__ part) {
   __shared__ double sh[3 * (RED_NT / 64)];
@@ -127,8 +144,9 @@ __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T*
   for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
     T xi = x[i], ri = r[i];
     if (ok) {
-      xi = xi - al * d[i];
-      ri = ri - al * q[i];
+      const T di = d[i];
+      xi = xi - al * di;
+      ri = ri - al * (q[i] + shift * di);
       x[i] = xi;
       r[i] = ri;
     }
@@ -189,16 +207,17 @@ __global__ void cg_dir_kernel(T* __restrict__ d, const T* __restrict__ r, long l
 template <typename T>
 __global__ __launch_bounds__(RED_NT) void cg_residual_kernel(T* __restrict__ r, const T* __restrict__ ax,
                                                              const T* __restrict__ x,
-                                                             const T* __restrict__ b, long long n,
+                                                             const T* __restrict__ b, long long n, T shift,
                                                              double* __restrict__ part) {
   __shared__ double sh[3 * (RED_NT / 64)];
   double v[3] = {0.0, 0.0, 0.0};
   const long long stride = (long long)gridDim.x * RED_NT;
   for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
     const T bi = b ? b[i] : (T)0;
-    const T ri = ax[i] - bi;
+    const T xt = x[i];
+    const T ri = (ax[i] + shift * xt) - bi;
     r[i] = ri;
-    const double xi = (double)x[i];
+    const double xi = (double)xt;
     v[0] += (double)ri * (double)ri;
     v[1] += xi * (double)ri;
     v[2] += xi * (double)bi;
@@ -245,6 +264,7 @@ int nft_dot(const void* a, const void* b, int64_t n, int dtype, double* out, voi
   }
   int nb = red_blocks(n);
   double* part = (double*)ws;
+  prof_mark(stream, "dot_partial");
   if (dtype == 0)
     hipLaunchKernelGGL(dot_partial<double>, dim3(nb), dim3(RED_NT), 0, stream, (const double*)a,
                        (const double*)b, (long long)n, part);
@@ -255,6 +275,7 @@ int nft_dot(const void* a, const void* b, int64_t n, int dtype, double* out, voi
     set_last_error("nft_dot: bad dtype %d", dtype);
     return NFT_ERR_ARG;
   }
+  prof_mark(stream, "fold_partials");
   hipLaunchKernelGGL(fold_partials<1>, dim3(1), dim3(RED_NT), 0, stream, part, nb, out);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
@@ -264,18 +285,41 @@ int nft_scale(void* x, int64_t n, int dtype, double scale, hipStream_t stream) {
   return scale_real(x, n, dtype, scale, stream);
 }
 
-int nft_cg_update(void* x, void* r, const void* d, const void* q, const void* b, int64_t n, int dtype,
-                  double* sc, void* ws, hipStream_t stream) {
+int nft_cg_curv(const void* d, const void* q, int64_t n, int dtype, double shift, double* sc, void* ws,
+                hipStream_t stream) {
   int nb = red_blocks(n);
   double* part = (double*)ws;
+  prof_mark(stream, "curv_partial");
+  if (dtype == 0)
+    hipLaunchKernelGGL(curv_partial<double>, dim3(nb), dim3(RED_NT), 0, stream, (const double*)d,
+                       (const double*)q, (long long)n, shift, part);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(curv_partial<float>, dim3(nb), dim3(RED_NT), 0, stream, (const float*)d,
+                       (const float*)q, (long long)n, (float)shift, part);
+  else {
+    set_last_error("nft_cg_curv: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
+  prof_mark(stream, "fold_partials");
+  hipLaunchKernelGGL(fold_partials<1>, dim3(1), dim3(RED_NT), 0, stream, part, nb, sc + NFT_CG_CURV);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_update(void* x, void* r, const void* d, const void* q, const void* b, int64_t n, int dtype,
+                  double shift, double* sc, void* ws, hipStream_t stream) {
+  int nb = red_blocks(n);
+  double* part = (double*)ws;
+  prof_mark(stream, "cg_update_kernel");
   if (dtype == 0)
     hipLaunchKernelGGL(cg_update_kernel<double>, dim3(nb), dim3(RED_NT), 0, stream, (double*)x,
                        (double*)r, (const double*)d, (const double*)q, (const double*)b, (long long)n,
-                       sc, part);
+                       shift, sc, part);
   else
     hipLaunchKernelGGL(cg_update_kernel<float>, dim3(nb), dim3(RED_NT), 0, stream, (float*)x,
-                       (float*)r, (const float*)d, (const float*)q, (const float*)b, (long long)n, sc,
-                       part);
+                       (float*)r, (const float*)d, (const float*)q, (const float*)b, (long long)n,
+                       (float)shift, sc, part);
+  prof_mark(stream, "cg_finalize_kernel");
   hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(RED_NT), 0, stream, part, nb, sc);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
@@ -285,6 +329,7 @@ int nft_cg_direction(void* d, const void* r, int64_t n, int dtype, const double*
                      hipStream_t stream) {
   int nb = (int)std::min<long long>((n + 255) / 256, 8192);
   if (nb < 1) nb = 1;
+  prof_mark(stream, "cg_dir_kernel");
   if (dtype == 0)
     hipLaunchKernelGGL(cg_dir_kernel<double>, dim3(nb), dim3(256), 0, stream, (double*)d,
                        (const double*)r, (long long)n, sc);
@@ -296,15 +341,18 @@ int nft_cg_direction(void* d, const void* r, int64_t n, int dtype, const double*
 }
 
 int nft_cg_residual(void* r, const void* ax, const void* x, const void* b, int64_t n, int dtype,
-                    double* sc, void* ws, hipStream_t stream) {
+                    double shift, double* sc, void* ws, hipStream_t stream) {
   int nb = red_blocks(n);
   double* part = (double*)ws;
+  prof_mark(stream, "cg_residual_kernel");
   if (dtype == 0)
     hipLaunchKernelGGL(cg_residual_kernel<double>, dim3(nb), dim3(RED_NT), 0, stream, (double*)r,
-                       (const double*)ax, (const double*)x, (const double*)b, (long long)n, part);
+                       (const double*)ax, (const double*)x, (const double*)b, (long long)n, shift, part);
   else
     hipLaunchKernelGGL(cg_residual_kernel<float>, dim3(nb), dim3(RED_NT), 0, stream, (float*)r,
-                       (const float*)ax, (const float*)x, (const float*)b, (long long)n, part);
+                       (const float*)ax, (const float*)x, (const float*)b, (long long)n, (float)shift,
+                       part);
+  prof_mark(stream, "cg_residual_finalize");
   hipLaunchKernelGGL(cg_residual_finalize, dim3(1), dim3(RED_NT), 0, stream, part, nb, sc);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;

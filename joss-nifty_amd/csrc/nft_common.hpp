@@ -27,6 +27,15 @@ template <typename C, typename T> __device__ __forceinline__ C cscale(C a, T s) 
 
 void set_last_error(const char* fmt, ...);
 
+// Launch profiler (nft_prof_begin / nft_prof_end): while active, prof_mark
+// records a HIP event on the launch stream before every hot-path kernel, so
+// consecutive events bracket exactly one kernel.  Inactive: one branch.
+extern bool g_prof_on;
+void prof_mark_impl(hipStream_t s, const char* label);
+inline void prof_mark(hipStream_t s, const char* label) {
+  if (g_prof_on) prof_mark_impl(s, label);
+}
+
 }  // namespace nft
 
 // error codes of the C ABI (NFT_OK / NFT_ERR_*) live in the public header

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
   }
   u[t] = v;
   const int s0 = p.item_seg[it], s1 = p.item_seg[it + 1];
-  const int e0 = p.seg_ent[s0], e1 = p.seg_ent[s1];
+  const int e0 = p.item_ent[it], e1 = p.item_ent[it + 1];
   const int n = e1 - e0;
   const bool staged = n <= LOS_CAP_F;  // host plans always fit; others take the direct path
   float wv[PER];
@@ -76,6 +76,15 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       lv[i] = k < n ? p.ent_loc[e0 + k] : 0;
     }
   }
+  // four lanes per segment; the first segment's bounds are loaded early too
+  const int sub = t & 3;
+  int s = s0 + (t >> 2);
+  int sa = 0, sb = 0, slot = 0;
+  if (s < s1) {
+    sa = p.seg_ent[s] - e0;
+    sb = p.seg_ent[s + 1] - e0;
+    slot = p.seg_slot[s];
+  }
   __syncthreads();
   if (staged) {
 #pragma unroll
@@ -85,19 +94,23 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
     }
   }
   __syncthreads();
-  // four lanes per segment, strided partial sums + fixed xor-tree
-  const int sub = t & 3;
-  for (int s = s0 + (t >> 2); s < s1; s += 64) {
-    const int a = p.seg_ent[s] - e0, b = p.seg_ent[s + 1] - e0;
+  // strided partial sums + fixed xor-tree per segment
+  while (s < s1) {
     double acc = 0.0;
     if (staged) {
-      for (int k = a + sub; k < b; k += 4) acc += prod[k];
+      for (int k = sa + sub; k < sb; k += 4) acc += prod[k];
     } else {
-      for (int k = a + sub; k < b; k += 4) acc += (double)p.ent_wf[e0 + k] * u[p.ent_loc[e0 + k]];
+      for (int k = sa + sub; k < sb; k += 4) acc += (double)p.ent_wf[e0 + k] * u[p.ent_loc[e0 + k]];
     }
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
-    if (sub == 0) part[p.seg_slot[s]] = acc;
+    if (sub == 0) part[slot] = acc;
+    s += 64;
+    if (s < s1) {
+      sa = p.seg_ent[s] - e0;
+      sb = p.seg_ent[s + 1] - e0;
+      slot = p.seg_slot[s];
+    }
   }
 }
 
@@ -129,6 +142,19 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int box = blockIdx.x, t = threadIdx.x;
   const int l0 = p.box_lptr[box], nl = p.box_lptr[box + 1] - l0;
+  const int e0 = p.box_ent[box], n = p.box_ent[box + 1] - e0;
+  const unsigned short* off = p.pix_off + (size_t)box * 257;
+  const int a = off[t], b = off[t + 1];
+  // the first chunk's entry loads go out before the line-table staging so the
+  // two dependent load chains overlap
+  int lv[PER];
+  float wv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = t + i * 256;
+    lv[i] = k < n ? (int)lidx[e0 + k] : 0;
+    wv[i] = k < n ? p.ent_wa[e0 + k] : 0.f;
+  }
   const bool tab = nl <= LOS_LMAX;  // line values of this box cached in LDS
   if (tab) {
     for (int i = t; i < nl; i += 256) {
@@ -138,21 +164,18 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
       yl[i] = v;
     }
   }
-  const int e0 = p.box_ent[box], n = p.box_ent[box + 1] - e0;
-  const unsigned short* off = p.pix_off + (size_t)box * 257;
-  const int a = off[t], b = off[t + 1];
   double acc = 0.0;
   for (int c0 = 0; c0 < n; c0 += LOS_CH_A) {  // uniform over the block
     const int cn = min(LOS_CH_A, n - c0);
-    __syncthreads();
-    int lv[PER];
-    float wv[PER];
+    if (c0 > 0) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int k = t + i * 256;
-      lv[i] = k < cn ? (int)lidx[e0 + c0 + k] : 0;
-      wv[i] = k < cn ? p.ent_wa[e0 + c0 + k] : 0.f;
+      for (int i = 0; i < PER; ++i) {
+        const int k = t + i * 256;
+        lv[i] = k < cn ? (int)lidx[e0 + c0 + k] : 0;
+        wv[i] = k < cn ? p.ent_wa[e0 + c0 + k] : 0.f;
+      }
     }
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int k = t + i * 256;
@@ -184,9 +207,11 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
 template <typename T>
 static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, const void* rs, void* y, double* part,
                          double scale, hipStream_t s) {
+  prof_mark(s, "los_fwd_items");
   if (p->nitems > 0)
     hipLaunchKernelGGL(los_fwd_items<T>, dim3((unsigned)p->nitems), dim3(256), 0, s, *p, (const T*)x, (const T*)cs,
                        part);
+  prof_mark(s, "los_fwd_reduce");
   if (p->nlos > 0)
     hipLaunchKernelGGL(los_fwd_reduce<T>, dim3((unsigned)((p->nlos + 3) / 4)), dim3(256), 0, s, *p, part,
                        (const T*)rs, (T*)y, scale);
@@ -198,6 +223,7 @@ template <typename T>
 static int los_adjoint_t(const nft_los_plan* p, const void* y, const void* cs, const void* rs, void* out, double scale,
                          hipStream_t s) {
   if (p->nbox <= 0) return NFT_OK;
+  prof_mark(s, "los_adj_boxes");
   if (p->lidx8)
     hipLaunchKernelGGL((los_adj_boxes<T, unsigned char>), dim3((unsigned)p->nbox), dim3(256), 0, s, *p,
                        (const unsigned char*)p->ent_lidx, (const T*)y, (const T*)cs, (const T*)rs, (T*)out, scale);

@@ -219,6 +219,7 @@ def box_plan(rows, cols, w, shape, nlos):
     return dict(H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
                 nitems=len(item_box), nseg=nseg, L=L,
                 item_box=np.asarray(item_box, dtype=np.int32), item_seg=np.asarray(item_seg, dtype=np.int32),
+                item_ent=seg_ent[np.asarray(item_seg, dtype=np.int64)].astype(np.int32),
                 seg_ent=seg_ent, seg_slot=seg_slot, ent_loc=loc[of].astype(np.uint8), ent_wf=wf[of],
                 los_ptr=los_ptr, box_ent=np.r_[0, np.cumsum(entcnt)].astype(np.int32), pix_off=pix_off,
                 box_lptr=box_lptr, box_lines=seg_los.astype(np.int32),

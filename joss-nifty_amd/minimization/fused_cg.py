@@ -3,10 +3,12 @@
 Same algorithm as ConjugateGradient.__call__ (src/minimization/
 conjugate_gradient.py:48-126), on packed device vectors:
 
-  q = M d                       fused model pipeline (core.metric_flat)
-  curv = d.q                    nft_dot            -> sc[CURV]
-  x -= a d ; r -= a q           nft_cg_update      -> sc[GAMMA]=r.r, x.r, x.b
+  q' = M' d                     fused model pipeline (core.metric_flat, M = shift + M')
+  curv = d.(q' + shift d)       nft_cg_curv        -> sc[CURV]
+  x -= a d ; r -= a (q' + s d)  nft_cg_update      -> sc[GAMMA]=r.r, x.r, x.b
   (every nreset-th step: r = M x - b exactly, nft_cg_residual)
+The shift is applied element-wise inside the CG kernels (same arithmetic as
+forming q = q' + shift d first), so the matvec never reads d a second time.
   host: guards + controller on (curv, gamma, value = (x.r - x.b)/2)
   d = max(0, g/g_prev) d + r    nft_cg_direction
 
@@ -26,6 +28,9 @@ from .conjugate_gradient import ConjugateGradient
 
 
 USE_GRAPHS = os.environ.get("NFT_NO_GRAPH") is None
+# iterations run eagerly before the loop body is captured: capturing costs a
+# few ms, which short solves (NewtonCG directions, ~5 steps) never win back
+GRAPH_AFTER = 4
 
 
 def fusable_metric(A):
@@ -120,6 +125,7 @@ class FusedCG:
         dt = _native.dtype_code(x.dtype)
         sp = _native.stream_ptr()
         P = _native.ptr
+        sh = self.shift
 
         def chk(st):
             _native._check(st)
@@ -136,9 +142,9 @@ class FusedCG:
             s_ = _native.stream_ptr()
             if with_dir:
                 chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), s_))
-            core.metric_flat(d, q, self.W, self.shift)
-            chk(lib.nft_dot(P(d), P(q), n, dt, P(sc[_native.CG_CURV:]), P(ws), s_))
-            chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, P(sc), P(ws), s_))
+            core.metric_flat(d, q, self.W, 0.0)
+            chk(lib.nft_cg_curv(P(d), P(q), n, dt, sh, P(sc), P(ws), s_))
+            chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, sh, P(sc), P(ws), s_))
 
         graph = None
         ii = 0
@@ -148,7 +154,7 @@ class FusedCG:
             ConjugateGradient.iterations_total += 1
             ii += 1
             if ii < self.nreset:
-                if first or not USE_GRAPHS:
+                if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER:
                     body(not first)
                 elif graph is None:
                     # capture dir + matvec + dot + update once (HIP graph); the
@@ -164,15 +170,15 @@ class FusedCG:
                 if not first:
                     chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), sp))
                 first = False
-                core.metric_flat(d, q, self.W, self.shift)
-                chk(lib.nft_dot(P(d), P(q), n, dt, P(sc[_native.CG_CURV:]), P(ws), sp))
+                core.metric_flat(d, q, self.W, 0.0)
+                chk(lib.nft_cg_curv(P(d), P(q), n, dt, sh, P(sc), P(ws), sp))
                 gp = sc[_native.CG_GAMMA].clone()
-                chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, P(sc), P(ws), sp))
+                chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, sh, P(sc), P(ws), sp))
                 if ax is None:
                     ax = lay.empty()
-                core.metric_flat(x, ax, self.W, self.shift)
+                core.metric_flat(x, ax, self.W, 0.0)
                 flag = sc[_native.CG_FLAG].clone()
-                chk(lib.nft_cg_residual(P(r), P(ax), P(x), P(b), n, dt, P(sc), P(ws), sp))
+                chk(lib.nft_cg_residual(P(r), P(ax), P(x), P(b), n, dt, sh, P(sc), P(ws), sp))
                 sc[_native.CG_GPREV] = gp
                 sc[_native.CG_FLAG] = flag
                 ii = 0
