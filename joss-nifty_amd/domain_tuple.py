@@ -29,6 +29,11 @@ class DomainTuple:
             i += nax
         return tuple(res)
 
+    def __reduce__(self):
+        # unpickling goes through make(): identity-based domain checks keep
+        # working for objects exchanged between ranks (domain_tuple.py:199-213)
+        return (_unpickle_domain_tuple, (self._dom,))
+
     @staticmethod
     def make(domain):
         if isinstance(domain, DomainTuple):
@@ -119,3 +124,7 @@ class DomainTuple:
         if DomainTuple._scalarDomain is None:
             DomainTuple._scalarDomain = DomainTuple.make(())
         return DomainTuple._scalarDomain
+
+
+def _unpickle_domain_tuple(dom):
+    return DomainTuple.make(dom)

@@ -12,6 +12,10 @@ class MultiDomain:
         self._domains = tuple(dct[k] for k in self._keys)
         self._idx = {k: i for i, k in enumerate(self._keys)}
 
+    def __reduce__(self):
+        # see DomainTuple.__reduce__ (multi_domain.py:136-144)
+        return (_unpickle_multi_domain, (dict(zip(self._keys, self._domains)),))
+
     @staticmethod
     def make(inp):
         if isinstance(inp, MultiDomain):
@@ -85,3 +89,7 @@ class MultiDomain:
                 else:
                     res[key] = subdom
         return MultiDomain.make(res)
+
+
+def _unpickle_multi_domain(dct):
+    return MultiDomain.make(dct)

@@ -1,0 +1,136 @@
+"""CPU: the multi-process path (one process per GPU on the box) with the gloo
+backend, world_size 2 -- sample sharding (shareRange over mirrored samples),
+the KL-mean all-reduce (fast: local pairwise sum + ONE all_reduce of a packed
+fp64 buffer; deterministic: the reference's global pairwise tree,
+bit-identical to the serial result, src/utilities.py:331-390), sample-list
+averaging and the communicator wrapper.  No GPU compute."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _values(n_total):
+    """per-sample MultiFields with awkward magnitudes (order-sensitive sums)"""
+    import nifty_amd as ift
+    dom = ift.makeDomain({"a": ift.RGSpace(7), "b": ift.DomainTuple.scalar_domain(),
+                          "xi": ift.RGSpace((4, 6))})
+    rng = np.random.default_rng(11)
+    out = []
+    for i in range(n_total):
+        d = {k: rng.standard_normal(dom[k].shape) * 10.0 ** rng.integers(-8, 8, dom[k].shape)
+             for k in dom.keys()}
+        out.append(ift.MultiField.from_dict({k: ift.makeField(dom[k], v) for k, v in d.items()}, dom))
+    return dom, out
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import nifty_amd as ift
+        from nifty_amd import utilities
+        comm = ift.TorchComm()
+        assert comm.Get_rank() == rank and comm.Get_size() == world
+        res = {}
+        # mirrored sample list sharded as draw_samples does (kl_energies.py:140-141)
+        nsamp = 5
+        lo, hi = utilities.shareRange(2 * nsamp, world, rank)
+        res["range"] = (lo, hi)
+        n_total = 2 * nsamp
+        dom, vals = _values(n_total)
+        mine = vals[lo:hi]
+        fast = utilities.allreduce_sum(mine, comm, deterministic=False)
+        det = utilities.allreduce_sum(mine, comm, deterministic=True)
+        res["fast"] = {k: np.asarray(fast[k]) for k in dom.keys()}
+        res["det"] = {k: np.asarray(det[k]) for k in dom.keys()}
+        # sample list averaging (mean +/- residual, mirrored signs)
+        mean = vals[0]
+        neg = [(i % 2) == 1 for i in range(lo, hi)]
+        sl = ift.ResidualSampleList(mean, vals[lo:hi], neg, comm)
+        assert sl.n_samples == n_total and sl.n_local_samples == hi - lo
+        avg = sl.average()
+        res["avg"] = {k: np.asarray(avg[k]) for k in dom.keys()}
+        # scalar tuple averaging (value, gradient) as SampledKLEnergyClass uses it
+        val, grad = sl._average_tuple(lambda s: (float(np.asarray(s["b"])), s))
+        res["tuple"] = (val, {k: np.asarray(grad[k]) for k in dom.keys()})
+        res["bcast"] = comm.bcast(rank * 7 + 3, root=0)
+        comm.Barrier()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception as e:  # surface the failure in the parent
+        import traceback
+        q.put((rank, "ERROR " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.fixture(scope="module")
+def results():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, res = q.get(timeout=240)
+        out[r] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r, res in out.items():
+        assert not isinstance(res, str), res
+    return out
+
+
+def test_share_range_covers_mirrored_samples(results):
+    rngs = sorted(results[r]["range"] for r in results)
+    assert rngs[0][0] == 0 and rngs[-1][1] == 10
+    assert rngs[0][1] == rngs[1][0]
+
+
+def test_allreduce_fast_and_deterministic(results):
+    sys.path.insert(0, ROOT)
+    from nifty_amd import utilities
+    dom, vals = _values(10)
+    serial = utilities.pairwise_sum(vals)
+    for r in results:
+        for k in dom.keys():
+            ref = np.asarray(serial[k])
+            # deterministic mode: the reference's global tree, bit for bit
+            np.testing.assert_array_equal(results[r]["det"][k], ref)
+            # fast mode: same value up to summation order
+            np.testing.assert_allclose(results[r]["fast"][k], ref, rtol=1e-12, atol=1e-300)
+            # identical on every rank
+            np.testing.assert_array_equal(results[r]["fast"][k], results[0]["fast"][k])
+
+
+def test_sample_list_average_over_ranks(results):
+    sys.path.insert(0, ROOT)
+    dom, vals = _values(10)
+    mean = vals[0]
+    full = [mean - v if i % 2 else mean + v for i, v in enumerate(vals)]
+    for r in results:
+        for k in dom.keys():
+            ref = sum(np.asarray(f[k]) for f in full) / 10
+            np.testing.assert_allclose(results[r]["avg"][k], ref, rtol=1e-10, atol=1e-300)
+        val, grad = results[r]["tuple"]
+        assert val == pytest.approx(float(np.mean([np.asarray(f["b"]) for f in full])), rel=1e-10)
+        np.testing.assert_allclose(grad["xi"], results[r]["avg"]["xi"], rtol=1e-12, atol=1e-300)
+    assert results[0]["bcast"] == results[1]["bcast"] == 3
