@@ -38,7 +38,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--size", type=int, default=2048)
     p.add_argument("--nlos", type=int, default=16384)
-    p.add_argument("--samples-per-gpu", type=int, default=1, help="mirrored pairs per GPU")
+    # C3 (BASELINE.json configs[2]): geoVI n_samples=8 mirrored pairs across 2
+    # GPUs -> 4 pairs (8 samples) per GPU, held fixed per GPU (weak scaling)
+    p.add_argument("--samples-per-gpu", type=int, default=4, help="mirrored pairs per GPU")
     p.add_argument("--lin-iters", type=int, default=100)
     p.add_argument("--newton-iters", type=int, default=2)
     p.add_argument("--newton-cg-max", type=int, default=50)

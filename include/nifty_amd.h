@@ -65,6 +65,7 @@ extern "C" {
 #define NFT_CG_XB 5 /* x.b */
 #define NFT_CG_FLAG 6 /* 1.0: curvature/alpha guard tripped, x and r left unchanged */
 #define NFT_CG_DD 7   /* d.d (fused sampling metric) */
+#define NFT_CG_DONE 8 /* set by the host: this right-hand side has stopped (batched solves) */
 #define NFT_CG_NSCALARS 16
 
 const char* nft_last_error(void);
@@ -102,6 +103,22 @@ int nft_cg_direction(void* d, const void* r, int64_t n, int dtype, const double*
 /* r = (ax + shift x) - b; sc[GPREV] <- sc[GAMMA]; sc[GAMMA,XR,XB] <- r.r, x.r, x.b */
 int nft_cg_residual(void* r, const void* ax, const void* x, const void* b, int64_t n, int dtype,
                     double shift, double* sc, void* ws, hipStream_t stream);
+/* Batched forms: nrhs independent right-hand sides, vectors vstride elements
+ * apart, scalar blocks NFT_CG_NSCALARS apart in sc, workspace nrhs times
+ * nft_reduce_workspace(n).  Per RHS bitwise identical to the single forms;
+ * a RHS with sc[NFT_CG_DONE] != 0 is left unchanged. */
+int nft_dot_batched(const void* a, const void* b, int64_t n, int64_t vstride, int nrhs, int dtype,
+                    double* out, int64_t out_stride, void* ws, hipStream_t stream);
+int nft_cg_curv_batched(const void* d, const void* q, int64_t n, int64_t vstride, int nrhs,
+                        int dtype, double shift, double* sc, void* ws, hipStream_t stream);
+int nft_cg_update_batched(void* x, void* r, const void* d, const void* q, const void* b, int64_t n,
+                          int64_t vstride, int nrhs, int dtype, double shift, double* sc, void* ws,
+                          hipStream_t stream);
+int nft_cg_direction_batched(void* d, const void* r, int64_t n, int64_t vstride, int nrhs, int dtype,
+                             const double* sc, hipStream_t stream);
+int nft_cg_residual_batched(void* r, const void* ax, const void* x, const void* b, int64_t n,
+                            int64_t vstride, int nrhs, int dtype, double shift, double* sc, void* ws,
+                            hipStream_t stream);
 
 /* ---- power-bin distributor -------------------------------------------- */
 /* out[p,i,q] = in[p, pindex[i], q]; in: [pre, nbins, post], out: [pre, npix, post] */
@@ -142,13 +159,20 @@ int nft_spmv_scaled(const int64_t* indptr, const int* indices, const float* weig
  * first axis pass and the epilogue inside the last one (no extra HBM pass);
  * other shapes run them as separate elementwise kernels.  This is the
  * correlated-field Jacobian's  HT[A*xi + xi0*dA[pindex]]  and its adjoint's
- * (A*v + shift*d, xi0*v)  (src/library/correlated_fields_simple.py:155-160). */
+ * (A*v + shift*d, xi0*v)  (src/library/correlated_fields_simple.py:155-160),
+ * optionally for a batch of right-hand sides sharing A, xi0 and pindex. */
 typedef struct nft_hartley_fuse {
   const void *pro_a, *pro_x, *pro_b, *pro_c;
   const int* pro_index;
   const void *epi_a, *epi_d, *epi_b;
   void* epi_out2;
   double epi_shift;
+  /* batch of transforms along a leading axis (0: no batch): elements per item,
+   * and the per-item strides of pro_x, pro_c, out, epi_d, epi_out2 (0: the
+   * item size, resp. B = pro_c's length for pro_c).  pro_a, pro_b,
+   * pro_index, epi_a, epi_b are shared by all items. */
+  int64_t batch_period;
+  int64_t x_bstride, c_bstride, out_bstride, d_bstride, out2_bstride;
 } nft_hartley_fuse;
 
 int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes,
@@ -198,6 +222,16 @@ int nft_los_forward(const nft_los_plan* plan, const void* x, const void* colscal
 /* out[p] = scale * rowscale[p] * sum_{(l,p)} w * colscale[l] * y[l]   (R^T y) */
 int nft_los_adjoint(const nft_los_plan* plan, const void* y, const void* colscale,
                     const void* rowscale, void* out, int dtype, double scale, hipStream_t stream);
+/* Batched over 1 <= nvec <= 8 vectors (x / y / out advance by their strides;
+ * the forward workspace holds nvec partial vectors: nvec * nft_los_workspace).
+ * The matrix entries are read once per launch for all vectors; per vector
+ * the results are bitwise those of the single forms. */
+int nft_los_forward_batched(const nft_los_plan* plan, const void* x, const void* colscale,
+                            const void* rowscale, void* y, void* ws, int dtype, double scale,
+                            int nvec, int64_t x_stride, int64_t y_stride, hipStream_t stream);
+int nft_los_adjoint_batched(const nft_los_plan* plan, const void* y, const void* colscale,
+                            const void* rowscale, void* out, int dtype, double scale, int nvec,
+                            int64_t y_stride, int64_t out_stride, hipStream_t stream);
 
 /* ---- correlated-field amplitude Jacobian ------------------------------ */
 /* Constants of the amplitude linearisation at one expansion point (all device
@@ -228,6 +262,16 @@ int nft_amp_jvp(const nft_amp_const* c, const double* t_fl, const double* t_sl,
                 const double* t_spec, double* da, double* ws, hipStream_t stream);
 int nft_amp_vjp(const nft_amp_const* c, const double* g, const nft_amp_out* out, double* ws,
                 hipStream_t stream);
+/* Batched: nrhs right-hand sides; tangent / cotangent pointers (and d) advance
+ * by lat_stride elements per RHS, da / g by da_stride (g_stride); workspace
+ * nrhs * nft_amp_workspace(B).  Per RHS identical to the single forms. */
+int nft_amp_jvp_batched(const nft_amp_const* c, const double* t_fl, const double* t_sl,
+                        const double* t_flex, const double* t_asp, const double* t_zm,
+                        const double* t_spec, double* da, double* ws, int nrhs, int64_t lat_stride,
+                        int64_t da_stride, hipStream_t stream);
+int nft_amp_vjp_batched(const nft_amp_const* c, const double* g, const nft_amp_out* out,
+                        double* ws, int nrhs, int64_t lat_stride, int64_t g_stride,
+                        hipStream_t stream);
 
 /* ---- launch profiler (HIP events) -------------------------------------- */
 /* Between nft_prof_begin and nft_prof_end every hot-path kernel launch

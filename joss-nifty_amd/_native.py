@@ -28,6 +28,11 @@ SIGNATURES = {
     "nft_dot": (_i, [_p, _p, _i64, _i, _p, _p, _p]),
     "nft_scale": (_i, [_p, _i64, _i, _d, _p]),
     "nft_cg_curv": (_i, [_p, _p, _i64, _i, _d, _p, _p, _p]),
+    "nft_dot_batched": (_i, [_p, _p, _i64, _i64, _i, _i, _p, _i64, _p, _p]),
+    "nft_cg_curv_batched": (_i, [_p, _p, _i64, _i64, _i, _i, _d, _p, _p, _p]),
+    "nft_cg_update_batched": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i, _i, _d, _p, _p, _p]),
+    "nft_cg_direction_batched": (_i, [_p, _p, _i64, _i64, _i, _i, _p, _p]),
+    "nft_cg_residual_batched": (_i, [_p, _p, _p, _p, _i64, _i64, _i, _i, _d, _p, _p, _p]),
     "nft_cg_update": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _p, _p, _p]),
     "nft_cg_direction": (_i, [_p, _p, _i64, _i, _p, _p]),
     "nft_cg_residual": (_i, [_p, _p, _p, _p, _i64, _i, _d, _p, _p, _p]),
@@ -41,19 +46,25 @@ SIGNATURES = {
     "nft_los_workspace": (_sz, [_p]),
     "nft_los_forward": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _p]),
     "nft_los_adjoint": (_i, [_p, _p, _p, _p, _p, _i, _d, _p]),
+    "nft_los_forward_batched": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p]),
+    "nft_los_adjoint_batched": (_i, [_p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p]),
     "nft_prof_begin": (_i, [_i]),
     "nft_prof_end": (_i, [_p, _p, _i, ctypes.POINTER(_i)]),
     "nft_prof_label": (ctypes.c_char_p, [_i]),
     "nft_amp_workspace": (_sz, [_i64]),
     "nft_amp_jvp": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "nft_amp_vjp": (_i, [_p, _p, _p, _p, _p]),
+    "nft_amp_jvp_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _p]),
+    "nft_amp_vjp_batched": (_i, [_p, _p, _p, _p, _i, _i64, _i64, _p]),
 }
 
 
 class HartleyFuse(ctypes.Structure):
     """nft_hartley_fuse (include/nifty_amd.h)."""
     _fields_ = [(n, _p) for n in ("pro_a", "pro_x", "pro_b", "pro_c", "pro_index", "epi_a", "epi_d", "epi_b",
-                                  "epi_out2")] + [("epi_shift", _d)]
+                                  "epi_out2")] + [("epi_shift", _d)] + \
+               [(n, _i64) for n in ("batch_period", "x_bstride", "c_bstride", "out_bstride", "d_bstride",
+                                    "out2_bstride")]
 
 
 class LosPlan(ctypes.Structure):
@@ -78,7 +89,7 @@ class AmpOut(ctypes.Structure):
     _fields_ = [(n, _p) for n in ("fl", "sl", "flex", "asp", "zm", "spec",
                                   "dfl", "dsl", "dflex", "dasp", "dzm", "dspec")] + [("shift", _d)]
 
-CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD = range(8)
+CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD, CG_DONE = range(9)
 CG_NSCALARS = 16
 
 _lib = None
@@ -267,12 +278,20 @@ def spmv_scaled(indptr, indices, weights, rowblocks, x, y, colscale=None, rowsca
     return y
 
 
-def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0):
+def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None):
     """out = epilogue(scale * Hartley(prologue)) with
     pro = dict(a=, x=, b=, c=, index=) and epi = dict(a=, d=, shift=, b=, out2=)
-    (nft_hartley_fused); `x` is the plain input when no prologue is given."""
+    (nft_hartley_fused); `x` is the plain input when no prologue is given.
+    Batched transforms: `shape` = (k, *grid), axes over the grid, and
+    batch = dict(period=, x=, c=, out=, d=, out2=) with the per-item strides
+    of the operands (elements); `out` may then be a strided base pointer."""
     lib = load()
     f = HartleyFuse()
+    if batch:
+        f.batch_period = int(batch["period"])
+        for k, fld in (("x", "x_bstride"), ("c", "c_bstride"), ("out", "out_bstride"), ("d", "d_bstride"),
+                       ("out2", "out2_bstride")):
+            setattr(f, fld, int(batch.get(k, 0)))
     tens = [out, x]
     if pro:
         for k, fld in (("a", "pro_a"), ("x", "pro_x"), ("b", "pro_b"), ("c", "pro_c"), ("index", "pro_index")):
@@ -285,11 +304,16 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
             tens.append(v)
             setattr(f, fld, v.data_ptr() if v is not None else None)
         f.epi_shift = float(epi.get("shift", 0.0))
-    require_device(*tens)
+    if batch:
+        for t in tens:
+            if t is not None and not t.is_cuda:
+                raise NativeError("nifty_amd hot-path ops run on the GPU only; no CPU fallback exists")
+    else:
+        require_device(*tens)
     for t in tens:
         if t is not None and t.dtype != out.dtype and t.dtype != torch.int32:
             raise TypeError("hartley_fused: operand dtype mismatch")
-    nd, sh, na, ax = _shape_args(tuple(out.shape), tuple(axes))
+    nd, sh, na, ax = _shape_args(tuple(out.shape) if shape is None else tuple(shape), tuple(axes))
     dt = dtype_code(out.dtype)
     nbytes = ctypes.c_size_t(0)
     _check(lib.nft_hartley_fused_workspace(nd, sh, na, ax, dt, ctypes.byref(nbytes)))
@@ -315,6 +339,29 @@ def los_adjoint(plan, y, out, colscale=None, rowscale=None, scale=1.0):
     require_device(y, out, colscale, rowscale)
     _check(lib.nft_los_adjoint(ctypes.byref(plan), ptr(y), ptr(colscale), ptr(rowscale), ptr(out),
                                dtype_code(y.dtype), float(scale), stream_ptr()))
+    return out
+
+
+def los_forward_batched(plan, x, y, colscale=None, rowscale=None, scale=1.0):
+    """y[b] = scale * rowscale * R (colscale * x[b]) for b < k (x: (k, ...) contiguous)."""
+    lib = load()
+    require_device(x, y, colscale, rowscale)
+    k = x.shape[0]
+    ws = workspace(k * lib.nft_los_workspace(ctypes.byref(plan)), x.device, "los")
+    _check(lib.nft_los_forward_batched(ctypes.byref(plan), ptr(x), ptr(colscale), ptr(rowscale), ptr(y), ptr(ws),
+                                       dtype_code(x.dtype), float(scale), k, x[0].numel(), y[0].numel(),
+                                       stream_ptr()))
+    return y
+
+
+def los_adjoint_batched(plan, y, out, colscale=None, rowscale=None, scale=1.0):
+    """out[b] = scale * rowscale * R^T (colscale * y[b])."""
+    lib = load()
+    require_device(y, out, colscale, rowscale)
+    k = y.shape[0]
+    _check(lib.nft_los_adjoint_batched(ctypes.byref(plan), ptr(y), ptr(colscale), ptr(rowscale), ptr(out),
+                                       dtype_code(y.dtype), float(scale), k, y[0].numel(), out[0].numel(),
+                                       stream_ptr()))
     return out
 
 

@@ -3,6 +3,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "fast_passes.hpp"
 #include "nft_api_internal.hpp"
 
@@ -52,10 +55,26 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
       attr_set = true;
     }
   }
+  FastArgs<T> b = a;
+  b.ntiles = ntiles;
+  // persistent grid: enough workgroups to fill every CU twice over
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      ncu = v;
+    else
+      ncu = 256;
+  }
+  static const int per_cu = getenv("NFT_FFT_WG_PER_CU") ? atoi(getenv("NFT_FFT_WG_PER_CU")) : 8;
+  const long long grid = persist_ok<N, NT, KIND>()
+                             ? std::min<long long>(ntiles, (long long)ncu * std::max(1, per_cu))
+                             : ntiles;
   static const char* const kind_name[4] = {"fft_c2c", "fft_r2c", "fft_h1d", "fft_unpack"};
   static const char* const kind_fused[4] = {"fft_c2c", "fft_r2c+pro", "fft_h1d+fused", "fft_unpack+epi"};
   prof_mark(s, (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
-  hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS>), dim3((unsigned)ntiles), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS>), dim3((unsigned)grid), dim3(NT), lds, s, b);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

@@ -23,6 +23,23 @@ namespace nft {
 using AmpConst = nft_amp_const;
 using AmpOut = nft_amp_out;
 
+// right-hand side blockIdx.y of a batched launch: latent tangents / cotangents
+// advance by ls elements, B-sized vectors by vs, the workspace by wsd
+__device__ __forceinline__ void amp_out_offset(nft_amp_out& o, long long off) {
+  if (o.fl) o.fl += off;
+  if (o.sl) o.sl += off;
+  if (o.flex) o.flex += off;
+  if (o.asp) o.asp += off;
+  if (o.zm) o.zm += off;
+  if (o.spec) o.spec += off;
+  if (o.dfl) o.dfl += off;
+  if (o.dsl) o.dsl += off;
+  if (o.dflex) o.dflex += off;
+  if (o.dasp) o.dasp += off;
+  if (o.dzm) o.dzm += off;
+  if (o.dspec) o.dspec += off;
+}
+
 constexpr int AT = 256;          // threads per block
 constexpr int AE = 4;            // elements per thread
 constexpr int ABLK = AT * AE;    // elements per block
@@ -102,7 +119,10 @@ __device__ __forceinline__ double carry_in(const double* tot, int blk, int nb, d
 // ------------------------------------------------------------------ JVP
 // J1: cs1 = local scan of t1*sf over j < B-2
 __global__ __launch_bounds__(AT) void amp_jvp_1(AmpConst c, const double* __restrict__ tspec,
-                                                double* __restrict__ loc, double* __restrict__ tot1) {
+                                                double* __restrict__ loc, double* __restrict__ tot1, long long ls, long long vs, long long wsd) {
+  if (tspec) tspec += blockIdx.y * ls;
+  loc += blockIdx.y * wsd;
+  tot1 += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   const long long M = c.B - 2;
   const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
@@ -122,7 +142,11 @@ __global__ __launch_bounds__(AT) void amp_jvp_1(AmpConst c, const double* __rest
 // J3: c = loc + carry; t = (c + c_prev)/2*lv + t0*c0; local scan of t
 __global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c, const double* __restrict__ tspec,
                                                 const double* __restrict__ tot1, double* __restrict__ loc,
-                                                double* __restrict__ tot2) {
+                                                double* __restrict__ tot2, long long ls, long long vs, long long wsd) {
+  if (tspec) tspec += blockIdx.y * ls;
+  tot1 += blockIdx.y * wsd;
+  loc += blockIdx.y * wsd;
+  tot2 += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   const long long M = c.B - 2;
   const int nb = (int)((M + ABLK - 1) / ABLK);
@@ -152,7 +176,15 @@ __global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c, const double* __rest
 __global__ __launch_bounds__(AT) void amp_jvp_5(AmpConst c, const double* tfl, const double* tsl,
                                                 const double* tflex, const double* tasp,
                                                 const double* __restrict__ loc, const double* __restrict__ tot2,
-                                                double* __restrict__ dapre, double* __restrict__ part) {
+                                                double* __restrict__ dapre, double* __restrict__ part, long long ls, long long vs, long long wsd) {
+  if (tfl) tfl += blockIdx.y * ls;
+  if (tsl) tsl += blockIdx.y * ls;
+  if (tflex) tflex += blockIdx.y * ls;
+  if (tasp) tasp += blockIdx.y * ls;
+  loc += blockIdx.y * wsd;
+  tot2 += blockIdx.y * wsd;
+  dapre += blockIdx.y * wsd;
+  part += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   const long long B = c.B, M = B - 2;
   const int nbM = c.has_flex ? (int)((M + ABLK - 1) / ABLK) : 0;
@@ -193,7 +225,12 @@ __global__ __launch_bounds__(AT) void amp_jvp_5(AmpConst c, const double* tfl, c
 // J7: da from dapre and dS = sum(part)
 __global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c, const double* tfl, const double* tzm,
                                                 const double* __restrict__ dapre, const double* __restrict__ part,
-                                                int npart, double* __restrict__ da) {
+                                                int npart, double* __restrict__ da, long long ls, long long vs, long long wsd) {
+  if (tfl) tfl += blockIdx.y * ls;
+  if (tzm) tzm += blockIdx.y * ls;
+  dapre += blockIdx.y * wsd;
+  part += blockIdx.y * wsd;
+  da += blockIdx.y * vs;
   __shared__ double sh[2 * AT];
   double s = 0;
   for (int i = threadIdx.x; i < npart; i += AT) s += part[i];
@@ -214,7 +251,9 @@ __global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c, const double* tfl, c
 
 // ------------------------------------------------------------------ VJP
 // V1: partials of R1 = sum_{b>=1} TV*g_b*An_b
-__global__ __launch_bounds__(AT) void amp_vjp_1(AmpConst c, const double* __restrict__ g, double* __restrict__ part) {
+__global__ __launch_bounds__(AT) void amp_vjp_1(AmpConst c, const double* __restrict__ g, double* __restrict__ part, long long ls, long long vs, long long wsd) {
+  g += blockIdx.y * vs;
+  part += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   double s = 0;
   for (long long b = (long long)blockIdx.x * AT + threadIdx.x; b < c.B; b += (long long)gridDim.x * AT)
@@ -226,7 +265,11 @@ __global__ __launch_bounds__(AT) void amp_vjp_1(AmpConst c, const double* __rest
 // V2: gapre; partials R2 = sum vslope*gapre, R3 = sum gapre*sc
 __global__ __launch_bounds__(AT) void amp_vjp_2(AmpConst c, const double* __restrict__ g,
                                                 const double* __restrict__ part1, int np1,
-                                                double* __restrict__ gapre, double* __restrict__ part23) {
+                                                double* __restrict__ gapre, double* __restrict__ part23, long long ls, long long vs, long long wsd) {
+  g += blockIdx.y * vs;
+  part1 += blockIdx.y * wsd;
+  gapre += blockIdx.y * wsd;
+  part23 += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   double s = 0;
   for (int i = threadIdx.x; i < np1; i += AT) s += part1[i];
@@ -258,7 +301,11 @@ __device__ __forceinline__ double gtl_at(const AmpConst& c, const double* gapre,
 // V3: reverse local scan of gtl[2:] -> y (local) ; totals
 __global__ __launch_bounds__(AT) void amp_vjp_3(AmpConst c, const double* __restrict__ gapre,
                                                 const double* __restrict__ part23, int np,
-                                                double* __restrict__ loc, double* __restrict__ tot) {
+                                                double* __restrict__ loc, double* __restrict__ tot, long long ls, long long vs, long long wsd) {
+  gapre += blockIdx.y * wsd;
+  part23 += blockIdx.y * wsd;
+  loc += blockIdx.y * wsd;
+  tot += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   double s = 0;
   for (int i = threadIdx.x; i < np; i += AT) s += part23[2 * i + 1];
@@ -282,7 +329,13 @@ __global__ __launch_bounds__(AT) void amp_vjp_3(AmpConst c, const double* __rest
 __global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c, const double* __restrict__ gapre,
                                                 const double* __restrict__ part23, int np,
                                                 const double* __restrict__ tot3, double* __restrict__ y,
-                                                double* __restrict__ loc, double* __restrict__ tot4) {
+                                                double* __restrict__ loc, double* __restrict__ tot4, long long ls, long long vs, long long wsd) {
+  gapre += blockIdx.y * wsd;
+  part23 += blockIdx.y * wsd;
+  tot3 += blockIdx.y * wsd;
+  y += blockIdx.y * wsd;
+  loc += blockIdx.y * wsd;
+  tot4 += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   double s = 0;
   for (int i = threadIdx.x; i < np; i += AT) s += part23[2 * i + 1];
@@ -317,7 +370,12 @@ __global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c, const double* __rest
 // V5: g1 = loc + carry; spectrum cotangents; partials R4, R5
 __global__ __launch_bounds__(AT) void amp_vjp_5(AmpConst c, AmpOut o, const double* __restrict__ y,
                                                 const double* __restrict__ loc, const double* __restrict__ tot4,
-                                                double* __restrict__ part45) {
+                                                double* __restrict__ part45, long long ls, long long vs, long long wsd) {
+  amp_out_offset(o, blockIdx.y * ls);
+  y += blockIdx.y * wsd;
+  loc += blockIdx.y * wsd;
+  tot4 += blockIdx.y * wsd;
+  part45 += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   const long long M = c.B - 2;
   const int nb = (int)((M + ABLK - 1) / ABLK);
@@ -353,7 +411,12 @@ __global__ __launch_bounds__(AT) void amp_vjp_5(AmpConst c, AmpOut o, const doub
 __global__ __launch_bounds__(AT) void amp_vjp_6(AmpConst c, AmpOut o, const double* __restrict__ g,
                                                 const double* __restrict__ part1, int np1,
                                                 const double* __restrict__ part23, int np23,
-                                                const double* __restrict__ part45, int np45) {
+                                                const double* __restrict__ part45, int np45, long long ls, long long vs, long long wsd) {
+  amp_out_offset(o, blockIdx.y * ls);
+  g += blockIdx.y * vs;
+  part1 += blockIdx.y * wsd;
+  part23 += blockIdx.y * wsd;
+  part45 += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   double a = 0, b2 = 0, b4 = 0, b5 = 0;
   for (int i = threadIdx.x; i < np1; i += AT) a += part1[i];
@@ -386,10 +449,13 @@ extern "C" {
 
 size_t nft_amp_workspace(int64_t B) { return (size_t)(3 * B + 16 * (B / 256 + 16)) * sizeof(double); }
 
-int nft_amp_jvp(const nft_amp_const* cst, const double* tfl, const double* tsl, const double* tflex, const double* tasp,
-                const double* tzm, const double* tspec, double* da, double* ws, hipStream_t s) {
+int nft_amp_jvp_batched(const nft_amp_const* cst, const double* tfl, const double* tsl, const double* tflex,
+                        const double* tasp, const double* tzm, const double* tspec, double* da, double* ws, int nrhs,
+                        int64_t lat_stride, int64_t da_stride, hipStream_t s) {
   const AmpConst& c = *cst;
   const long long B = c.B, M = B - 2;
+  const long long wsd = (long long)(nft_amp_workspace(B) / sizeof(double));
+  const long long ls = lat_stride, vs = da_stride;
   double* loc = ws;                 // M
   double* dapre = ws + B;           // B
   double* tot1 = ws + 2 * B;        // nbM
@@ -397,25 +463,35 @@ int nft_amp_jvp(const nft_amp_const* cst, const double* tfl, const double* tsl, 
   double* tot2 = tot1 + nbM + 1;
   const int nbB = nblk(B, ABLK);
   double* part = tot2 + nbM + 1;
+  const unsigned ny = (unsigned)nrhs;
   if (c.has_flex) {
     prof_mark(s, "amp_jvp_1");
-    hipLaunchKernelGGL(amp_jvp_1, dim3(nbM), dim3(AT), 0, s, c, tspec, loc, tot1);
+    hipLaunchKernelGGL(amp_jvp_1, dim3(nbM, ny), dim3(AT), 0, s, c, tspec, loc, tot1, ls, vs, wsd);
     prof_mark(s, "amp_jvp_3");
-    hipLaunchKernelGGL(amp_jvp_3, dim3(nbM), dim3(AT), 0, s, c, tspec, tot1, loc, tot2);
+    hipLaunchKernelGGL(amp_jvp_3, dim3(nbM, ny), dim3(AT), 0, s, c, tspec, tot1, loc, tot2, ls, vs, wsd);
   }
   prof_mark(s, "amp_jvp_5");
-  hipLaunchKernelGGL(amp_jvp_5, dim3(nbB), dim3(AT), 0, s, c, tfl, tsl, tflex, tasp, loc, tot2, dapre, part);
+  hipLaunchKernelGGL(amp_jvp_5, dim3(nbB, ny), dim3(AT), 0, s, c, tfl, tsl, tflex, tasp, loc, tot2, dapre, part, ls,
+                     vs, wsd);
   prof_mark(s, "amp_jvp_7");
-  hipLaunchKernelGGL(amp_jvp_7, dim3(nblk(B, AT) < 1024 ? nblk(B, AT) : 1024), dim3(AT), 0, s, c, tfl, tzm,
-                     dapre, part, nbB, da);
+  hipLaunchKernelGGL(amp_jvp_7, dim3(nblk(B, AT) < 1024 ? nblk(B, AT) : 1024, ny), dim3(AT), 0, s, c, tfl, tzm,
+                     dapre, part, nbB, da, ls, vs, wsd);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
 
-int nft_amp_vjp(const nft_amp_const* cst, const double* g, const nft_amp_out* out, double* ws, hipStream_t s) {
+int nft_amp_jvp(const nft_amp_const* cst, const double* tfl, const double* tsl, const double* tflex,
+                const double* tasp, const double* tzm, const double* tspec, double* da, double* ws, hipStream_t s) {
+  return nft_amp_jvp_batched(cst, tfl, tsl, tflex, tasp, tzm, tspec, da, ws, 1, 0, 0, s);
+}
+
+int nft_amp_vjp_batched(const nft_amp_const* cst, const double* g, const nft_amp_out* out, double* ws, int nrhs,
+                        int64_t lat_stride, int64_t g_stride, hipStream_t s) {
   const AmpConst& c = *cst;
   const AmpOut& o = *out;
   const long long B = c.B, M = B - 2;
+  const long long wsd = (long long)(nft_amp_workspace(B) / sizeof(double));
+  const long long ls = lat_stride, vs = g_stride;
   double* gapre = ws;               // B
   double* loc = ws + B;             // M
   double* y = ws + 2 * B;           // M
@@ -426,23 +502,29 @@ int nft_amp_vjp(const nft_amp_const* cst, const double* g, const nft_amp_out* ou
   double* tot3 = part23 + 2 * nr + 2;
   double* tot4 = tot3 + nbM + 1;
   double* part45 = tot4 + nbM + 1;
+  const unsigned ny = (unsigned)nrhs;
   prof_mark(s, "amp_vjp_1");
-  hipLaunchKernelGGL(amp_vjp_1, dim3(nr), dim3(AT), 0, s, c, g, part1);
+  hipLaunchKernelGGL(amp_vjp_1, dim3(nr, ny), dim3(AT), 0, s, c, g, part1, ls, vs, wsd);
   prof_mark(s, "amp_vjp_2");
-  hipLaunchKernelGGL(amp_vjp_2, dim3(nr), dim3(AT), 0, s, c, g, part1, nr, gapre, part23);
+  hipLaunchKernelGGL(amp_vjp_2, dim3(nr, ny), dim3(AT), 0, s, c, g, part1, nr, gapre, part23, ls, vs, wsd);
   if (c.has_flex) {
     prof_mark(s, "amp_vjp_3");
-    hipLaunchKernelGGL(amp_vjp_3, dim3(nbM), dim3(AT), 0, s, c, gapre, part23, nr, loc, tot3);
+    hipLaunchKernelGGL(amp_vjp_3, dim3(nbM, ny), dim3(AT), 0, s, c, gapre, part23, nr, loc, tot3, ls, vs, wsd);
     prof_mark(s, "amp_vjp_4");
-    hipLaunchKernelGGL(amp_vjp_4, dim3(nbM), dim3(AT), 0, s, c, gapre, part23, nr, tot3, y, loc, tot4);
+    hipLaunchKernelGGL(amp_vjp_4, dim3(nbM, ny), dim3(AT), 0, s, c, gapre, part23, nr, tot3, y, loc, tot4, ls, vs,
+                       wsd);
     prof_mark(s, "amp_vjp_5");
-    hipLaunchKernelGGL(amp_vjp_5, dim3(nbM), dim3(AT), 0, s, c, o, y, loc, tot4, part45);
+    hipLaunchKernelGGL(amp_vjp_5, dim3(nbM, ny), dim3(AT), 0, s, c, o, y, loc, tot4, part45, ls, vs, wsd);
   }
   prof_mark(s, "amp_vjp_6");
-  hipLaunchKernelGGL(amp_vjp_6, dim3(1), dim3(AT), 0, s, c, o, g, part1, nr, part23, nr, part45,
-                     c.has_flex ? nbM : 0);
+  hipLaunchKernelGGL(amp_vjp_6, dim3(1, ny), dim3(AT), 0, s, c, o, g, part1, nr, part23, nr, part45,
+                     c.has_flex ? nbM : 0, ls, vs, wsd);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
+}
+
+int nft_amp_vjp(const nft_amp_const* cst, const double* g, const nft_amp_out* out, double* ws, hipStream_t s) {
+  return nft_amp_vjp_batched(cst, g, out, ws, 1, 0, 0, s);
 }
 
 }  // extern "C"

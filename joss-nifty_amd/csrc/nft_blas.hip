@@ -58,8 +58,11 @@ static int red_blocks(long long n) {
 // ------------------------------------------------------------------ dot
 template <typename T>
 __global__ __launch_bounds__(RED_NT) void dot_partial(const T* __restrict__ a, const T* __restrict__ b,
-                                                      long long n, double* __restrict__ part) {
+                                                      long long n, long long vs, double* __restrict__ part) {
   __shared__ double sh[RED_NT / 64];
+  a += (long long)blockIdx.y * vs;
+  b += (long long)blockIdx.y * vs;
+  part += (long long)blockIdx.y * gridDim.x;
   double v[1] = {0.0};
   const long long stride = (long long)gridDim.x * RED_NT;
   for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride)
@@ -72,8 +75,12 @@ __global__ __launch_bounds__(RED_NT) void dot_partial(const T* __restrict__ a, c
 // shift*1 + M' when only q = M' d was formed (the shift never touches HBM)
 template <typename T>
 __global__ __launch_bounds__(RED_NT) void curv_partial(const T* __restrict__ d, const T* __restrict__ q,
-                                                       long long n, T shift, double* __restrict__ part) {
+                                                       long long n, long long vs, T shift,
+                                                       double* __restrict__ part) {
   __shared__ double sh[RED_NT / 64];
+  d += (long long)blockIdx.y * vs;
+  q += (long long)blockIdx.y * vs;
+  part += (long long)blockIdx.y * gridDim.x;
   double v[1] = {0.0};
   const long long stride = (long long)gridDim.x * RED_NT;
   for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
@@ -86,10 +93,14 @@ __global__ __launch_bounds__(RED_NT) void curv_partial(const T* __restrict__ d, 
 }
 
 // fold `nb` partial vectors of width W (layout part[k*nb + b]) into out[k]
+// fold `nb` partial vectors of width W (layout part[k*nb + b]) into out[k];
+// one workgroup per RHS (partials advance by W*nb, out by ostride)
 template <int W>
 __global__ __launch_bounds__(RED_NT) void fold_partials(const double* __restrict__ part, int nb,
-                                                        double* __restrict__ out) {
+                                                        double* __restrict__ out, long long ostride) {
   __shared__ double sh[W * (RED_NT / 64)];
+  part += (long long)blockIdx.x * W * nb;
+  out += (long long)blockIdx.x * ostride;
   double v[W];
 #pragma unroll
   for (int k = 0; k < W; ++k) {
@@ -122,7 +133,14 @@ int scale_real(void* x, long long n, int dtype, double scale, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ CG
-// x -= alpha d ; r -= alpha q   with alpha = sc[GAMMA] / sc[CURV]
+// Every CG kernel handles a batch of independent right-hand sides: blockIdx.y
+// selects the RHS (vectors advance by `vs` elements, scalars by
+// NFT_CG_NSCALARS, partials by 3*nb).  Each RHS runs exactly the arithmetic
+// and reduction tree of a single solve, so a batched solve is bitwise equal
+// to solving the RHS one after another.  sc[NFT_CG_DONE] != 0 freezes a RHS
+// (the host sets it once that RHS's controller has stopped).
+//
+// x -= alpha d ; r -= alpha (q + shift d)  with alpha = sc[GAMMA] / sc[CURV]
 // partial dots: r.r, x.r, x.b
 // A non-finite or non-positive curvature, or alpha < 0, leaves x and r
 // untouched (the host maps the flag to IterationController.ERROR, exactly
@@ -131,13 +149,22 @@ template <typename T>
 __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T* __restrict__ r,
                                                            const T* __restrict__ d,
                                                            const T* __restrict__ q,
-                                                           const T* __restrict__ b, long long n, T shift,
-                                                           const double* __restrict__ sc,
+                                                           const T* __restrict__ b, long long n, long long vs,
+                                                           T shift, const double* __restrict__ sc,
                                                            double* __restrict__ part) {
   __shared__ double sh[3 * (RED_NT / 64)];
+  const long long o = (long long)blockIdx.y * vs;
+  sc += blockIdx.y * NFT_CG_NSCALARS;
+  part += (long long)blockIdx.y * 3 * gridDim.x;
+  x += o;
+  r += o;
+  d += o;
+  q += o;
+  if (b) b += o;
   const double curv = sc[NFT_CG_CURV], gprev = sc[NFT_CG_GAMMA];
   const double alpha = gprev / curv;
-  const bool ok = (curv == curv) && curv != 0.0 && (alpha >= 0.0) && (alpha == alpha);
+  const bool ok = (curv == curv) && curv != 0.0 && (alpha >= 0.0) && (alpha == alpha) &&
+                  sc[NFT_CG_DONE] == 0.0;
   const T al = (T)alpha;
   double v[3] = {0.0, 0.0, 0.0};
   const long long stride = (long long)gridDim.x * RED_NT;
@@ -164,10 +191,12 @@ __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T*
   }
 }
 
-// one workgroup: fold the 3 partial vectors, shift gamma, record alpha/flags
+// one workgroup per RHS: fold the 3 partial vectors, shift gamma, record alpha/flags
 __global__ __launch_bounds__(RED_NT) void cg_finalize_kernel(const double* __restrict__ part, int nb,
                                                              double* __restrict__ sc) {
   __shared__ double sh[3 * (RED_NT / 64)];
+  sc += blockIdx.x * NFT_CG_NSCALARS;
+  part += (long long)blockIdx.x * 3 * nb;
   double v[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -175,7 +204,7 @@ __global__ __launch_bounds__(RED_NT) void cg_finalize_kernel(const double* __res
     for (int b = threadIdx.x; b < nb; b += RED_NT) v[k] += part[k * nb + b];
   }
   block_sum<3>(v, sh);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && sc[NFT_CG_DONE] == 0.0) {
     const double curv = sc[NFT_CG_CURV], gprev = sc[NFT_CG_GAMMA];
     const double alpha = gprev / curv;
     const bool ok = (curv == curv) && curv != 0.0 && (alpha >= 0.0) && (alpha == alpha);
@@ -192,8 +221,12 @@ __global__ __launch_bounds__(RED_NT) void cg_finalize_kernel(const double* __res
 
 // d = max(0, gamma/gprev) d + r
 template <typename T>
-__global__ void cg_dir_kernel(T* __restrict__ d, const T* __restrict__ r, long long n,
+__global__ void cg_dir_kernel(T* __restrict__ d, const T* __restrict__ r, long long n, long long vs,
                               const double* __restrict__ sc) {
+  sc += blockIdx.y * NFT_CG_NSCALARS;
+  if (sc[NFT_CG_DONE] != 0.0) return;
+  d += (long long)blockIdx.y * vs;
+  r += (long long)blockIdx.y * vs;
   double beta = sc[NFT_CG_GAMMA] / sc[NFT_CG_GPREV];
   if (!(beta > 0.0)) beta = 0.0;
   const T bt = (T)beta;
@@ -202,21 +235,35 @@ __global__ void cg_dir_kernel(T* __restrict__ d, const T* __restrict__ r, long l
     d[i] = bt * d[i] + r[i];
 }
 
-// r = ax - b (exact residual refresh, conjugate_gradient.py:103-105 via
-// QuadraticEnergy.__init__) and partial dots r.r, x.r, x.b
+// r = (ax + shift x) - b (exact residual refresh, conjugate_gradient.py:103-105
+// via QuadraticEnergy.__init__) and partial dots r.r, x.r, x.b
 template <typename T>
 __global__ __launch_bounds__(RED_NT) void cg_residual_kernel(T* __restrict__ r, const T* __restrict__ ax,
                                                              const T* __restrict__ x,
-                                                             const T* __restrict__ b, long long n, T shift,
+                                                             const T* __restrict__ b, long long n, long long vs,
+                                                             T shift, const double* __restrict__ sc,
                                                              double* __restrict__ part) {
   __shared__ double sh[3 * (RED_NT / 64)];
+  const long long o = (long long)blockIdx.y * vs;
+  sc += blockIdx.y * NFT_CG_NSCALARS;
+  part += (long long)blockIdx.y * 3 * gridDim.x;
+  const bool live = sc[NFT_CG_DONE] == 0.0;
+  r += o;
+  ax += o;
+  x += o;
+  if (b) b += o;
   double v[3] = {0.0, 0.0, 0.0};
   const long long stride = (long long)gridDim.x * RED_NT;
   for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
     const T bi = b ? b[i] : (T)0;
     const T xt = x[i];
-    const T ri = (ax[i] + shift * xt) - bi;
-    r[i] = ri;
+    T ri;
+    if (live) {
+      ri = (ax[i] + shift * xt) - bi;
+      r[i] = ri;
+    } else {
+      ri = r[i];
+    }
     const double xi = (double)xt;
     v[0] += (double)ri * (double)ri;
     v[1] += xi * (double)ri;
@@ -233,6 +280,8 @@ __global__ __launch_bounds__(RED_NT) void cg_residual_kernel(T* __restrict__ r, 
 
 __global__ void cg_residual_finalize(const double* __restrict__ part, int nb, double* __restrict__ sc) {
   __shared__ double sh[3 * (RED_NT / 64)];
+  sc += blockIdx.x * NFT_CG_NSCALARS;
+  part += (long long)blockIdx.x * 3 * nb;
   double v[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -240,7 +289,7 @@ __global__ void cg_residual_finalize(const double* __restrict__ part, int nb, do
     for (int b = threadIdx.x; b < nb; b += RED_NT) v[k] += part[k * nb + b];
   }
   block_sum<3>(v, sh);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && sc[NFT_CG_DONE] == 0.0) {
     sc[NFT_CG_GPREV] = sc[NFT_CG_GAMMA];
     sc[NFT_CG_GAMMA] = v[0];
     sc[NFT_CG_XR] = v[1];
@@ -256,106 +305,147 @@ extern "C" {
 
 size_t nft_reduce_workspace(int64_t n) { return (size_t)3 * red_blocks(n) * sizeof(double); }
 
-int nft_dot(const void* a, const void* b, int64_t n, int dtype, double* out, void* ws,
-            hipStream_t stream) {
-  if (n < 0 || !out || !ws) {
+int nft_dot_batched(const void* a, const void* b, int64_t n, int64_t vstride, int nrhs, int dtype, double* out,
+                    int64_t out_stride, void* ws, hipStream_t stream) {
+  if (n < 0 || !out || !ws || nrhs < 1) {
     set_last_error("nft_dot: bad arguments");
     return NFT_ERR_ARG;
   }
   int nb = red_blocks(n);
   double* part = (double*)ws;
+  const dim3 grid(nb, nrhs);
   prof_mark(stream, "dot_partial");
   if (dtype == 0)
-    hipLaunchKernelGGL(dot_partial<double>, dim3(nb), dim3(RED_NT), 0, stream, (const double*)a,
-                       (const double*)b, (long long)n, part);
+    hipLaunchKernelGGL(dot_partial<double>, grid, dim3(RED_NT), 0, stream, (const double*)a, (const double*)b,
+                       (long long)n, (long long)vstride, part);
   else if (dtype == 1)
-    hipLaunchKernelGGL(dot_partial<float>, dim3(nb), dim3(RED_NT), 0, stream, (const float*)a,
-                       (const float*)b, (long long)n, part);
+    hipLaunchKernelGGL(dot_partial<float>, grid, dim3(RED_NT), 0, stream, (const float*)a, (const float*)b,
+                       (long long)n, (long long)vstride, part);
   else {
     set_last_error("nft_dot: bad dtype %d", dtype);
     return NFT_ERR_ARG;
   }
   prof_mark(stream, "fold_partials");
-  hipLaunchKernelGGL(fold_partials<1>, dim3(1), dim3(RED_NT), 0, stream, part, nb, out);
+  hipLaunchKernelGGL(fold_partials<1>, dim3(nrhs), dim3(RED_NT), 0, stream, part, nb, out, (long long)out_stride);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
+}
+
+int nft_dot(const void* a, const void* b, int64_t n, int dtype, double* out, void* ws, hipStream_t stream) {
+  return nft_dot_batched(a, b, n, 0, 1, dtype, out, 0, ws, stream);
 }
 
 int nft_scale(void* x, int64_t n, int dtype, double scale, hipStream_t stream) {
   return scale_real(x, n, dtype, scale, stream);
 }
 
-int nft_cg_curv(const void* d, const void* q, int64_t n, int dtype, double shift, double* sc, void* ws,
-                hipStream_t stream) {
+int nft_cg_curv_batched(const void* d, const void* q, int64_t n, int64_t vstride, int nrhs, int dtype, double shift,
+                        double* sc, void* ws, hipStream_t stream) {
   int nb = red_blocks(n);
   double* part = (double*)ws;
+  const dim3 grid(nb, nrhs);
   prof_mark(stream, "curv_partial");
   if (dtype == 0)
-    hipLaunchKernelGGL(curv_partial<double>, dim3(nb), dim3(RED_NT), 0, stream, (const double*)d,
-                       (const double*)q, (long long)n, shift, part);
+    hipLaunchKernelGGL(curv_partial<double>, grid, dim3(RED_NT), 0, stream, (const double*)d, (const double*)q,
+                       (long long)n, (long long)vstride, shift, part);
   else if (dtype == 1)
-    hipLaunchKernelGGL(curv_partial<float>, dim3(nb), dim3(RED_NT), 0, stream, (const float*)d,
-                       (const float*)q, (long long)n, (float)shift, part);
+    hipLaunchKernelGGL(curv_partial<float>, grid, dim3(RED_NT), 0, stream, (const float*)d, (const float*)q,
+                       (long long)n, (long long)vstride, (float)shift, part);
   else {
     set_last_error("nft_cg_curv: bad dtype %d", dtype);
     return NFT_ERR_ARG;
   }
   prof_mark(stream, "fold_partials");
-  hipLaunchKernelGGL(fold_partials<1>, dim3(1), dim3(RED_NT), 0, stream, part, nb, sc + NFT_CG_CURV);
+  hipLaunchKernelGGL(fold_partials<1>, dim3(nrhs), dim3(RED_NT), 0, stream, part, nb, sc + NFT_CG_CURV,
+                     (long long)NFT_CG_NSCALARS);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_curv(const void* d, const void* q, int64_t n, int dtype, double shift, double* sc, void* ws,
+                hipStream_t stream) {
+  return nft_cg_curv_batched(d, q, n, 0, 1, dtype, shift, sc, ws, stream);
+}
+
+int nft_cg_update_batched(void* x, void* r, const void* d, const void* q, const void* b, int64_t n, int64_t vstride,
+                          int nrhs, int dtype, double shift, double* sc, void* ws, hipStream_t stream) {
+  int nb = red_blocks(n);
+  double* part = (double*)ws;
+  const dim3 grid(nb, nrhs);
+  prof_mark(stream, "cg_update_kernel");
+  if (dtype == 0)
+    hipLaunchKernelGGL(cg_update_kernel<double>, grid, dim3(RED_NT), 0, stream, (double*)x, (double*)r,
+                       (const double*)d, (const double*)q, (const double*)b, (long long)n, (long long)vstride,
+                       shift, sc, part);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(cg_update_kernel<float>, grid, dim3(RED_NT), 0, stream, (float*)x, (float*)r,
+                       (const float*)d, (const float*)q, (const float*)b, (long long)n, (long long)vstride,
+                       (float)shift, sc, part);
+  else {
+    set_last_error("nft_cg_update: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
+  prof_mark(stream, "cg_finalize_kernel");
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(nrhs), dim3(RED_NT), 0, stream, part, nb, sc);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
 
 int nft_cg_update(void* x, void* r, const void* d, const void* q, const void* b, int64_t n, int dtype,
                   double shift, double* sc, void* ws, hipStream_t stream) {
-  int nb = red_blocks(n);
-  double* part = (double*)ws;
-  prof_mark(stream, "cg_update_kernel");
-  if (dtype == 0)
-    hipLaunchKernelGGL(cg_update_kernel<double>, dim3(nb), dim3(RED_NT), 0, stream, (double*)x,
-                       (double*)r, (const double*)d, (const double*)q, (const double*)b, (long long)n,
-                       shift, sc, part);
-  else
-    hipLaunchKernelGGL(cg_update_kernel<float>, dim3(nb), dim3(RED_NT), 0, stream, (float*)x,
-                       (float*)r, (const float*)d, (const float*)q, (const float*)b, (long long)n,
-                       (float)shift, sc, part);
-  prof_mark(stream, "cg_finalize_kernel");
-  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(RED_NT), 0, stream, part, nb, sc);
-  NFT_HIP_CHECK(hipGetLastError());
-  return NFT_OK;
+  return nft_cg_update_batched(x, r, d, q, b, n, 0, 1, dtype, shift, sc, ws, stream);
 }
 
-int nft_cg_direction(void* d, const void* r, int64_t n, int dtype, const double* sc,
-                     hipStream_t stream) {
+int nft_cg_direction_batched(void* d, const void* r, int64_t n, int64_t vstride, int nrhs, int dtype,
+                             const double* sc, hipStream_t stream) {
   int nb = (int)std::min<long long>((n + 255) / 256, 8192);
   if (nb < 1) nb = 1;
+  const dim3 grid(nb, nrhs);
   prof_mark(stream, "cg_dir_kernel");
   if (dtype == 0)
-    hipLaunchKernelGGL(cg_dir_kernel<double>, dim3(nb), dim3(256), 0, stream, (double*)d,
-                       (const double*)r, (long long)n, sc);
-  else
-    hipLaunchKernelGGL(cg_dir_kernel<float>, dim3(nb), dim3(256), 0, stream, (float*)d,
-                       (const float*)r, (long long)n, sc);
+    hipLaunchKernelGGL(cg_dir_kernel<double>, grid, dim3(256), 0, stream, (double*)d, (const double*)r,
+                       (long long)n, (long long)vstride, sc);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(cg_dir_kernel<float>, grid, dim3(256), 0, stream, (float*)d, (const float*)r, (long long)n,
+                       (long long)vstride, sc);
+  else {
+    set_last_error("nft_cg_direction: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
 
-int nft_cg_residual(void* r, const void* ax, const void* x, const void* b, int64_t n, int dtype,
-                    double shift, double* sc, void* ws, hipStream_t stream) {
+int nft_cg_direction(void* d, const void* r, int64_t n, int dtype, const double* sc, hipStream_t stream) {
+  return nft_cg_direction_batched(d, r, n, 0, 1, dtype, sc, stream);
+}
+
+int nft_cg_residual_batched(void* r, const void* ax, const void* x, const void* b, int64_t n, int64_t vstride,
+                            int nrhs, int dtype, double shift, double* sc, void* ws, hipStream_t stream) {
   int nb = red_blocks(n);
   double* part = (double*)ws;
+  const dim3 grid(nb, nrhs);
   prof_mark(stream, "cg_residual_kernel");
   if (dtype == 0)
-    hipLaunchKernelGGL(cg_residual_kernel<double>, dim3(nb), dim3(RED_NT), 0, stream, (double*)r,
-                       (const double*)ax, (const double*)x, (const double*)b, (long long)n, shift, part);
-  else
-    hipLaunchKernelGGL(cg_residual_kernel<float>, dim3(nb), dim3(RED_NT), 0, stream, (float*)r,
-                       (const float*)ax, (const float*)x, (const float*)b, (long long)n, (float)shift,
+    hipLaunchKernelGGL(cg_residual_kernel<double>, grid, dim3(RED_NT), 0, stream, (double*)r, (const double*)ax,
+                       (const double*)x, (const double*)b, (long long)n, (long long)vstride, shift, sc, part);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(cg_residual_kernel<float>, grid, dim3(RED_NT), 0, stream, (float*)r, (const float*)ax,
+                       (const float*)x, (const float*)b, (long long)n, (long long)vstride, (float)shift, sc,
                        part);
+  else {
+    set_last_error("nft_cg_residual: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
   prof_mark(stream, "cg_residual_finalize");
-  hipLaunchKernelGGL(cg_residual_finalize, dim3(1), dim3(RED_NT), 0, stream, part, nb, sc);
+  hipLaunchKernelGGL(cg_residual_finalize, dim3(nrhs), dim3(RED_NT), 0, stream, part, nb, sc);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
+}
+
+int nft_cg_residual(void* r, const void* ax, const void* x, const void* b, int64_t n, int dtype, double shift,
+                    double* sc, void* ws, hipStream_t stream) {
+  return nft_cg_residual_batched(r, ax, x, b, n, 0, 1, dtype, shift, sc, ws, stream);
 }
 
 }  // extern "C"

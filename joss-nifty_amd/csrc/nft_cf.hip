@@ -73,6 +73,8 @@ __global__ __launch_bounds__(256) void bin_scatter_chunk(const T* __restrict__ i
   const int per = (nchunks + NXCD - 1) / NXCD;
   const int c = (int)(blockIdx.x % NXCD) * per + (int)(blockIdx.x / NXCD);
   if (c >= nchunks) return;
+  in += (long long)blockIdx.y * npix;  // batch of inputs sharing the binning (pre axis)
+  out += (long long)blockIdx.y * nbins;
   const long long j0 = (long long)c * BS_CH;
   const int t = threadIdx.x;
   const int n = (int)(npix - j0 < BS_CH ? npix - j0 : BS_CH);
@@ -142,19 +144,19 @@ int nft_bin_scatter(const void* in, const int* perm, const int* offsets, void* o
                     int64_t npix, int64_t nbins, int64_t post, int dtype, hipStream_t stream) {
   long long tot = pre * nbins * post;
   if (tot <= 0) return NFT_OK;
-  if (pre == 1 && post == 1 && (dtype == 0 || dtype == 1)) {
+  if (post == 1 && pre <= 65535 && (dtype == 0 || dtype == 1)) {
     const int nchunks = (int)((npix + BS_CH - 1) / BS_CH);
     const unsigned nb = (unsigned)(((nchunks + NXCD - 1) / NXCD) * NXCD);
     if (npix <= 0) {
-      NFT_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)nbins * (dtype == 0 ? 8 : 4), stream));
+      NFT_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)pre * nbins * (dtype == 0 ? 8 : 4), stream));
       return NFT_OK;
     }
     prof_mark(stream, "bin_scatter");
     if (dtype == 0)
-      hipLaunchKernelGGL(bin_scatter_chunk<double>, dim3(nb), dim3(256), 0, stream, (const double*)in, perm,
+      hipLaunchKernelGGL(bin_scatter_chunk<double>, dim3(nb, (unsigned)pre), dim3(256), 0, stream, (const double*)in, perm,
                          offsets, (double*)out, (long long)npix, (long long)nbins, nchunks);
     else
-      hipLaunchKernelGGL(bin_scatter_chunk<float>, dim3(nb), dim3(256), 0, stream, (const float*)in, perm,
+      hipLaunchKernelGGL(bin_scatter_chunk<float>, dim3(nb, (unsigned)pre), dim3(256), 0, stream, (const float*)in, perm,
                          offsets, (float*)out, (long long)npix, (long long)nbins, nchunks);
     NFT_HIP_CHECK(hipGetLastError());
     return NFT_OK;

@@ -616,9 +616,9 @@ __global__ void fuse_pro_kernel(fast::FuseArgs f, T* __restrict__ dst, long long
 }
 
 template <typename T>
-__global__ void fuse_epi_kernel(fast::FuseArgs f, T* __restrict__ out, long long n) {
+__global__ void fuse_epi_kernel(fast::FuseArgs f, const T* __restrict__ h, T* __restrict__ out, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    fast::fuse_store<T>(f, out, i, out[i]);
+    fast::fuse_store<T>(f, out, i, h[i]);
 }
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -645,10 +645,20 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     NFT_HIP_CHECK(hipGetLastError());
     src = tmp;
   }
-  int st = hartley_impl<T>(src, out, g, ax, sigma, scale, ws, hws, s);
+  // with an epilogue the transform goes to a second temporary: the epilogue's
+  // output may use a different batch layout than the transform's
+  T* dst = (T*)out;
+  if (f.epi) {
+    if (ws_bytes < align256(hws) + 2 * (size_t)n * sizeof(T)) {
+      set_last_error("hartley_fused workspace too small");
+      return NFT_ERR_ARG;
+    }
+    dst = (T*)((char*)ws + align256(hws)) + n;
+  }
+  int st = hartley_impl<T>(src, dst, g, ax, sigma, scale, ws, hws, s);
   if (st != NFT_OK) return st;
   if (f.epi) {
-    hipLaunchKernelGGL(fuse_epi_kernel<T>, dim3(nb), dim3(256), 0, s, f, (T*)out, n);
+    hipLaunchKernelGGL(fuse_epi_kernel<T>, dim3(nb), dim3(256), 0, s, f, (const T*)dst, (T*)out, n);
     NFT_HIP_CHECK(hipGetLastError());
   }
   return NFT_OK;
@@ -733,7 +743,7 @@ int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const
   if (st != NFT_OK) return st;
   long long n = 1;
   for (int d = 0; d < ndim; ++d) n *= shape[d];
-  *bytes = align256(*bytes) + (size_t)n * (dtype == 0 ? 8 : 4);
+  *bytes = align256(*bytes) + 2 * (size_t)n * (dtype == 0 ? 8 : 4);
   return NFT_OK;
 }
 
@@ -761,6 +771,22 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     f.eshift = fz->epi_shift;
     f.pro = f.px != nullptr;
     f.epi = (f.ea || f.ed || f.out2) ? 1 : 0;
+    f.P = fz->batch_period;
+    f.pshift = -1;
+    if (f.P > 0 && (f.P & (f.P - 1)) == 0) {
+      int sh = 0;
+      while ((1LL << sh) < f.P) ++sh;
+      f.pshift = sh;
+    }
+    f.sx = fz->x_bstride ? fz->x_bstride : f.P;
+    f.sc = fz->c_bstride;
+    f.so = fz->out_bstride ? fz->out_bstride : f.P;
+    f.sd = fz->d_bstride ? fz->d_bstride : f.P;
+    f.s2 = fz->out2_bstride ? fz->out2_bstride : f.P;
+    if (f.P < 0 || (f.P > 0 && f.pb && f.sc == 0)) {
+      set_last_error("nft_hartley_fused: batch needs c_bstride");
+      return NFT_ERR_ARG;
+    }
     if ((f.pb && (!f.pc || !f.pidx)) || (f.out2 && !f.eb)) {
       set_last_error("nft_hartley_fused: incomplete fusion spec");
       return NFT_ERR_ARG;

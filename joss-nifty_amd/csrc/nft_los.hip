@@ -27,7 +27,8 @@ namespace nft {
 
 constexpr int LOS_CAP_F = 2048;  // entries per forward work item (host-guaranteed)
 constexpr int LOS_CH_A = 2048;   // adjoint: entries staged in LDS per chunk
-constexpr int LOS_LMAX = 1024;   // adjoint: lines per box cached in LDS
+constexpr int LOS_YL = 2048;     // adjoint: LDS slots for the line values of a box (all batch vectors)
+constexpr int LOS_KMAX = 8;      // vectors per batched launch
 
 struct BoxGeom {
   long long H, W;
@@ -44,37 +45,51 @@ struct BoxGeom {
   }
 };
 
-template <typename T>
+// Batched over K vectors (template, 1 <= K <= LOS_KMAX): the entries of a
+// work item (fp32 weight + 8-bit local pixel) are staged in LDS ONCE and
+// applied to every vector's tile; each segment's 4-lane group accumulates all
+// K vectors in registers.  Per vector the products and their summation order
+// are those of K = 1 (bitwise).
+template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __restrict__ x,
-                                                     const T* __restrict__ cs, double* __restrict__ part) {
+                                                     const T* __restrict__ cs, double* __restrict__ part,
+                                                     long long xs, long long ps) {
+  // every product is rounded before it is summed, in all K variants alike
+  // (no FMA contraction): batched results are bitwise the K = 1 results
+#pragma clang fp contract(off)
   constexpr int PER = LOS_CAP_F / 256;
-  __shared__ double u[256];
-  __shared__ double prod[LOS_CAP_F];
+  __shared__ double u[K][256];
+  __shared__ float ew[K == 1 ? 1 : LOS_CAP_F];
+  __shared__ unsigned char el[K == 1 ? 1 : LOS_CAP_F];
+  __shared__ double prodbuf[K == 1 ? LOS_CAP_F : 1];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int it = blockIdx.x, t = threadIdx.x;
   const int box = p.item_box[it];
   bool ok;
   const long long px = g.pixel(box, t, ok);
-  double v = 0.0;
-  if (ok) {
-    v = (double)x[px];
-    if (cs) v *= (double)cs[px];
-  }
-  u[t] = v;
   const int s0 = p.item_seg[it], s1 = p.item_seg[it + 1];
   const int e0 = p.item_ent[it], e1 = p.item_ent[it + 1];
   const int n = e1 - e0;
   const bool staged = n <= LOS_CAP_F;  // host plans always fit; others take the direct path
   float wv[PER];
-  int lv[PER];
+  unsigned char lv[PER];
   if (staged) {
-    // issue every entry load of this thread before the tile is needed
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int k = t + i * 256;
       wv[i] = k < n ? p.ent_wf[e0 + k] : 0.f;
       lv[i] = k < n ? p.ent_loc[e0 + k] : 0;
     }
+  }
+  const double c = (ok && cs) ? (double)cs[px] : 1.0;
+#pragma unroll
+  for (int b = 0; b < K; ++b) {
+    double v = 0.0;
+    if (ok) {
+      v = (double)x[b * xs + px];
+      if (cs) v *= c;
+    }
+    u[b][t] = v;
   }
   // four lanes per segment; the first segment's bounds are loaded early too
   const int sub = t & 3;
@@ -85,26 +100,65 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
     sb = p.seg_ent[s + 1] - e0;
     slot = p.seg_slot[s];
   }
-  __syncthreads();
-  if (staged) {
+  if (K > 1 && staged) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int k = t + i * 256;
-      if (k < n) prod[k] = (double)wv[i] * u[lv[i]];
+      if (k < n) {
+        ew[k] = wv[i];
+        el[k] = lv[i];
+      }
     }
   }
   __syncthreads();
-  // strided partial sums + fixed xor-tree per segment
-  while (s < s1) {
-    double acc = 0.0;
+  if constexpr (K == 1) {
+    // single vector: stage the products once (fewer LDS reads per entry)
+    double* prod = prodbuf;
     if (staged) {
-      for (int k = sa + sub; k < sb; k += 4) acc += prod[k];
-    } else {
-      for (int k = sa + sub; k < sb; k += 4) acc += (double)p.ent_wf[e0 + k] * u[p.ent_loc[e0 + k]];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int k = t + i * 256;
+        if (k < n) prod[k] = (double)wv[i] * u[0][lv[i]];
+      }
     }
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    if (sub == 0) part[slot] = acc;
+    __syncthreads();
+    while (s < s1) {
+      double a0 = 0.0;
+      if (staged) {
+        for (int k = sa + sub; k < sb; k += 4) a0 += prod[k];
+      } else {
+        for (int k = sa + sub; k < sb; k += 4)
+          a0 = a0 + (double)p.ent_wf[e0 + k] * u[0][p.ent_loc[e0 + k]];
+      }
+      a0 += __shfl_xor(a0, 1, 64);
+      a0 += __shfl_xor(a0, 2, 64);
+      if (sub == 0) part[slot] = a0;
+      s += 64;
+      if (s < s1) {
+        sa = p.seg_ent[s] - e0;
+        sb = p.seg_ent[s + 1] - e0;
+        slot = p.seg_slot[s];
+      }
+    }
+    return;
+  }
+  while (s < s1) {
+    double acc[K];
+#pragma unroll
+    for (int b = 0; b < K; ++b) acc[b] = 0.0;
+    for (int k = sa + sub; k < sb; k += 4) {
+      const double w = staged ? (double)ew[k] : (double)p.ent_wf[e0 + k];
+      const int l = staged ? el[k] : p.ent_loc[e0 + k];
+#pragma unroll
+      for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[b][l];
+    }
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      double a = acc[b];
+      a += __shfl_xor(a, 1, 64);
+      a += __shfl_xor(a, 2, 64);
+      if (sub == 0) part[b * ps + slot] = a;
+    }
     s += 64;
     if (s < s1) {
       sa = p.seg_ent[s] - e0;
@@ -116,10 +170,13 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 
 template <typename T>
 __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const double* __restrict__ part,
-                                                      const T* __restrict__ rs, T* __restrict__ y, double scale) {
+                                                      const T* __restrict__ rs, T* __restrict__ y, double scale,
+                                                      long long ps, long long ys) {
   const int lane = threadIdx.x & 63;
   const long long l = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= p.nlos) return;
+  part += blockIdx.y * ps;
+  y += blockIdx.y * ys;
   const int a = p.los_ptr[l], b = p.los_ptr[l + 1];
   double acc = 0.0;
   for (int k = a + lane; k < b; k += 64) acc += part[k];
@@ -132,13 +189,22 @@ __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const doub
   }
 }
 
-template <typename T, typename IDX>
+// Batched over K vectors (template): the chunk's entries (line index +
+// fp32 weight) are staged in LDS once; every pixel thread sums its run for
+// all K vectors in registers from the per-vector line tables.  Per vector the
+// products and their order are those of K = 1 (bitwise).
+template <typename T, typename IDX, int K>
 __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* __restrict__ lidx,
                                                      const T* __restrict__ yv, const T* __restrict__ cs,
-                                                     const T* __restrict__ rs, T* __restrict__ out, double scale) {
+                                                     const T* __restrict__ rs, T* __restrict__ out, double scale,
+                                                     long long ys, long long os) {
+#pragma clang fp contract(off)
   constexpr int PER = LOS_CH_A / 256;
-  __shared__ double yl[LOS_LMAX];
-  __shared__ double prod[LOS_CH_A];
+  constexpr int YL = LOS_YL;
+  __shared__ double yl[YL];
+  // K == 1 uses ew as a double product buffer (LOS_CH_A doubles)
+  __shared__ __align__(16) float ew[K == 1 ? 2 * LOS_CH_A : LOS_CH_A];
+  __shared__ unsigned short el[K == 1 ? 1 : LOS_CH_A];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int box = blockIdx.x, t = threadIdx.x;
   const int l0 = p.box_lptr[box], nl = p.box_lptr[box + 1] - l0;
@@ -155,16 +221,22 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
     lv[i] = k < n ? (int)lidx[e0 + k] : 0;
     wv[i] = k < n ? p.ent_wa[e0 + k] : 0.f;
   }
-  const bool tab = nl <= LOS_LMAX;  // line values of this box cached in LDS
+  const bool tab = nl * K <= YL;  // line values of this box (all vectors) cached in LDS
   if (tab) {
     for (int i = t; i < nl; i += 256) {
       const int li = p.box_lines[l0 + i];
-      double v = (double)yv[li];
-      if (cs) v *= (double)cs[li];
-      yl[i] = v;
+      const double c = cs ? (double)cs[li] : 1.0;
+#pragma unroll
+      for (int v = 0; v < K; ++v) {
+        double yy = (double)yv[v * ys + li];
+        if (cs) yy *= c;
+        yl[v * nl + i] = yy;
+      }
     }
   }
-  double acc = 0.0;
+  double acc[K];
+#pragma unroll
+  for (int v = 0; v < K; ++v) acc[v] = 0.0;
   for (int c0 = 0; c0 < n; c0 += LOS_CH_A) {  // uniform over the block
     const int cn = min(LOS_CH_A, n - c0);
     if (c0 > 0) {
@@ -175,61 +247,140 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
         wv[i] = k < cn ? p.ent_wa[e0 + c0 + k] : 0.f;
       }
     }
-    __syncthreads();
+    __syncthreads();  // previous chunk consumed (and line table written)
+    const int lo = max(a, c0), hi = min(b, c0 + cn);
+    if constexpr (K == 1) {
+      // single vector: stage the products once (the float/index buffers
+      // double as the product buffer)
+      double* prod = (double*)ew;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int k = t + i * 256;
+        if (k < cn) {
+          double yy;
+          if (tab) {
+            yy = yl[lv[i]];
+          } else {
+            const int gl = p.box_lines[l0 + lv[i]];
+            yy = (double)yv[gl];
+            if (cs) yy *= (double)cs[gl];
+          }
+          prod[k] = (double)wv[i] * yy;
+        }
+      }
+      __syncthreads();
+      for (int k = lo; k < hi; ++k) acc[0] += prod[k - c0];
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int k = t + i * 256;
       if (k < cn) {
-        double yy;
-        if (tab) {
-          yy = yl[lv[i]];
-        } else {
-          const int li = p.box_lines[l0 + lv[i]];
-          yy = (double)yv[li];
-          if (cs) yy *= (double)cs[li];
-        }
-        prod[k] = (double)wv[i] * yy;
+        ew[k] = wv[i];
+        el[k] = (unsigned short)lv[i];
       }
     }
     __syncthreads();
-    const int lo = max(a, c0), hi = min(b, c0 + cn);
-    for (int k = lo; k < hi; ++k) acc += prod[k - c0];
+    for (int k = lo; k < hi; ++k) {
+      const double w = (double)ew[k - c0];
+      const int li = el[k - c0];
+      if (tab) {
+#pragma unroll
+        for (int v = 0; v < K; ++v) acc[v] = acc[v] + w * yl[v * nl + li];
+      } else {
+        const int gl = p.box_lines[l0 + li];
+        const double cc = cs ? (double)cs[gl] : 1.0;
+#pragma unroll
+        for (int v = 0; v < K; ++v) {
+          double yy = (double)yv[v * ys + gl];
+          if (cs) yy *= cc;
+          acc[v] = acc[v] + w * yy;
+        }
+      }
+    }
   }
   bool ok;
   const long long px = g.pixel(box, t, ok);
   if (ok) {
-    acc *= scale;
-    if (rs) acc *= (double)rs[px];
-    out[px] = (T)acc;
+    const double r = rs ? (double)rs[px] : 1.0;
+#pragma unroll
+    for (int v = 0; v < K; ++v) {
+      double o = acc[v] * scale;
+      if (rs) o *= r;
+      out[v * os + px] = (T)o;
+    }
   }
 }
 
+template <typename T, int K>
+static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* part, long long xs, long long ps,
+                        hipStream_t s) {
+  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, ps);
+}
+
+template <typename T, typename IDX, int K>
+static void adj_boxes_k(const nft_los_plan* p, const IDX* li, const T* y, const T* cs, const T* rs, T* out,
+                        double scale, long long ys, long long os, hipStream_t s) {
+  hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), dim3((unsigned)p->nbox), dim3(256), 0, s, *p, li, y, cs, rs, out,
+                     scale, ys, os);
+}
+
+// vectors are processed in groups of 8 / 4 / 2 / 1 (template sizes)
+static int kgroup(int k) { return k >= 8 ? 8 : (k >= 4 ? 4 : (k >= 2 ? 2 : 1)); }
+
 template <typename T>
 static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, const void* rs, void* y, double* part,
-                         double scale, hipStream_t s) {
+                         double scale, int K, long long xs, long long ys, hipStream_t s) {
+  const long long ps = p->nseg;
   prof_mark(s, "los_fwd_items");
-  if (p->nitems > 0)
-    hipLaunchKernelGGL(los_fwd_items<T>, dim3((unsigned)p->nitems), dim3(256), 0, s, *p, (const T*)x, (const T*)cs,
-                       part);
+  if (p->nitems > 0) {
+    for (int v = 0; v < K;) {
+      const int g = kgroup(K - v);
+      const T* xv = (const T*)x + v * xs;
+      double* pv = part + v * ps;
+      switch (g) {
+        case 8: fwd_items_k<T, 8>(p, xv, (const T*)cs, pv, xs, ps, s); break;
+        case 4: fwd_items_k<T, 4>(p, xv, (const T*)cs, pv, xs, ps, s); break;
+        case 2: fwd_items_k<T, 2>(p, xv, (const T*)cs, pv, xs, ps, s); break;
+        default: fwd_items_k<T, 1>(p, xv, (const T*)cs, pv, xs, ps, s); break;
+      }
+      v += g;
+    }
+  }
   prof_mark(s, "los_fwd_reduce");
   if (p->nlos > 0)
-    hipLaunchKernelGGL(los_fwd_reduce<T>, dim3((unsigned)((p->nlos + 3) / 4)), dim3(256), 0, s, *p, part,
-                       (const T*)rs, (T*)y, scale);
+    hipLaunchKernelGGL(los_fwd_reduce<T>, dim3((unsigned)((p->nlos + 3) / 4), (unsigned)K), dim3(256), 0, s, *p,
+                       part, (const T*)rs, (T*)y, scale, ps, ys);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
 
+template <typename T, typename IDX>
+static void los_adjoint_idx(const nft_los_plan* p, const IDX* li, const void* y, const void* cs, const void* rs,
+                            void* out, double scale, int K, long long ys, long long os, hipStream_t s) {
+  for (int v = 0; v < K;) {
+    const int g = kgroup(K - v);
+    const T* yv = (const T*)y + v * ys;
+    T* ov = (T*)out + v * os;
+    switch (g) {
+      case 8: adj_boxes_k<T, IDX, 8>(p, li, yv, (const T*)cs, (const T*)rs, ov, scale, ys, os, s); break;
+      case 4: adj_boxes_k<T, IDX, 4>(p, li, yv, (const T*)cs, (const T*)rs, ov, scale, ys, os, s); break;
+      case 2: adj_boxes_k<T, IDX, 2>(p, li, yv, (const T*)cs, (const T*)rs, ov, scale, ys, os, s); break;
+      default: adj_boxes_k<T, IDX, 1>(p, li, yv, (const T*)cs, (const T*)rs, ov, scale, ys, os, s); break;
+    }
+    v += g;
+  }
+}
+
 template <typename T>
 static int los_adjoint_t(const nft_los_plan* p, const void* y, const void* cs, const void* rs, void* out, double scale,
-                         hipStream_t s) {
+                         int K, long long ys, long long os, hipStream_t s) {
   if (p->nbox <= 0) return NFT_OK;
   prof_mark(s, "los_adj_boxes");
   if (p->lidx8)
-    hipLaunchKernelGGL((los_adj_boxes<T, unsigned char>), dim3((unsigned)p->nbox), dim3(256), 0, s, *p,
-                       (const unsigned char*)p->ent_lidx, (const T*)y, (const T*)cs, (const T*)rs, (T*)out, scale);
+    los_adjoint_idx<T, unsigned char>(p, (const unsigned char*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s);
   else
-    hipLaunchKernelGGL((los_adj_boxes<T, unsigned short>), dim3((unsigned)p->nbox), dim3(256), 0, s, *p,
-                       (const unsigned short*)p->ent_lidx, (const T*)y, (const T*)cs, (const T*)rs, (T*)out, scale);
+    los_adjoint_idx<T, unsigned short>(p, (const unsigned short*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
@@ -250,24 +401,48 @@ extern "C" {
 
 size_t nft_los_workspace(const nft_los_plan* p) { return (size_t)(p ? p->nseg : 0) * sizeof(double) + 256; }
 
-int nft_los_forward(const nft_los_plan* p, const void* x, const void* colscale, const void* rowscale, void* y,
-                    void* ws, int dtype, double scale, hipStream_t stream) {
+int nft_los_forward_batched(const nft_los_plan* p, const void* x, const void* colscale, const void* rowscale,
+                            void* y, void* ws, int dtype, double scale, int nvec, int64_t x_stride,
+                            int64_t y_stride, hipStream_t stream) {
   int st = check_plan(p);
   if (st != NFT_OK) return st;
-  if (dtype == 0) return los_forward_t<double>(p, x, colscale, rowscale, y, (double*)ws, scale, stream);
-  if (dtype == 1) return los_forward_t<float>(p, x, colscale, rowscale, y, (double*)ws, scale, stream);
+  if (nvec < 1 || nvec > LOS_KMAX) {
+    set_last_error("nft_los_forward: 1 <= nvec <= %d", LOS_KMAX);
+    return NFT_ERR_ARG;
+  }
+  if (dtype == 0)
+    return los_forward_t<double>(p, x, colscale, rowscale, y, (double*)ws, scale, nvec, x_stride, y_stride, stream);
+  if (dtype == 1)
+    return los_forward_t<float>(p, x, colscale, rowscale, y, (double*)ws, scale, nvec, x_stride, y_stride, stream);
   set_last_error("nft_los_forward: bad dtype %d", dtype);
+  return NFT_ERR_ARG;
+}
+
+int nft_los_forward(const nft_los_plan* p, const void* x, const void* colscale, const void* rowscale, void* y,
+                    void* ws, int dtype, double scale, hipStream_t stream) {
+  return nft_los_forward_batched(p, x, colscale, rowscale, y, ws, dtype, scale, 1, 0, 0, stream);
+}
+
+int nft_los_adjoint_batched(const nft_los_plan* p, const void* y, const void* colscale, const void* rowscale,
+                            void* out, int dtype, double scale, int nvec, int64_t y_stride, int64_t out_stride,
+                            hipStream_t stream) {
+  int st = check_plan(p);
+  if (st != NFT_OK) return st;
+  if (nvec < 1 || nvec > LOS_KMAX) {
+    set_last_error("nft_los_adjoint: 1 <= nvec <= %d", LOS_KMAX);
+    return NFT_ERR_ARG;
+  }
+  if (dtype == 0)
+    return los_adjoint_t<double>(p, y, colscale, rowscale, out, scale, nvec, y_stride, out_stride, stream);
+  if (dtype == 1)
+    return los_adjoint_t<float>(p, y, colscale, rowscale, out, scale, nvec, y_stride, out_stride, stream);
+  set_last_error("nft_los_adjoint: bad dtype %d", dtype);
   return NFT_ERR_ARG;
 }
 
 int nft_los_adjoint(const nft_los_plan* p, const void* y, const void* colscale, const void* rowscale, void* out,
                     int dtype, double scale, hipStream_t stream) {
-  int st = check_plan(p);
-  if (st != NFT_OK) return st;
-  if (dtype == 0) return los_adjoint_t<double>(p, y, colscale, rowscale, out, scale, stream);
-  if (dtype == 1) return los_adjoint_t<float>(p, y, colscale, rowscale, out, scale, stream);
-  set_last_error("nft_los_adjoint: bad dtype %d", dtype);
-  return NFT_ERR_ARG;
+  return nft_los_adjoint_batched(p, y, colscale, rowscale, out, dtype, scale, 1, 0, 0, stream);
 }
 
 }  // extern "C"

@@ -207,6 +207,47 @@ class _AmplitudeModel:
         k.has_flex, k.has_asp, k.has_zm = int(self.has_flex), int(self.has_asp), int(self.has_zm)
         return k, keep
 
+    def _ptrs(self, D, off):
+        """base pointers of the amplitude keys of packed row 0 of D (or None)"""
+        def at(key):
+            if key not in off:
+                return None
+            return D[0, off[key]:].data_ptr()
+        return at
+
+    def native_jvp_batched(self, const, D, off, da):
+        """da[b] = J_amp D[b] for the k rows of a packed batch D (k, size)."""
+        import ctypes
+        at = self._ptrs(D, off)
+        k, size = D.shape
+        lib = _native.load()
+        ws = _native.workspace(k * lib.nft_amp_workspace(self.B), D.device, "amp")
+        P = ctypes.c_void_p
+        _native._check(lib.nft_amp_jvp_batched(
+            ctypes.byref(const), P(at(self.k_fl)), P(at(self.k_sl)), P(at(self.k_flex)), P(at(self.k_asp)),
+            P(at(self.k_zm)), P(at(self.k_spec)), P(da.data_ptr()), P(ws.data_ptr()), k, size, self.B,
+            _native.stream_ptr()))
+        return da
+
+    def native_vjp_batched(self, const, g, Q, off, D=None, shift=0.0):
+        """Q[b] amplitude keys = shift * D[b] + J_amp^T g[b]."""
+        import ctypes
+        k, size = Q.shape
+        lib = _native.load()
+        ws = _native.workspace(k * lib.nft_amp_workspace(self.B), Q.device, "amp")
+        atq = self._ptrs(Q, off)
+        atd = self._ptrs(D, off) if (D is not None and shift != 0.0) else (lambda key: None)
+        o = _native.AmpOut()
+        for short, key in (("fl", self.k_fl), ("sl", self.k_sl), ("flex", self.k_flex), ("asp", self.k_asp),
+                           ("zm", self.k_zm), ("spec", self.k_spec)):
+            setattr(o, short, atq(key))
+            setattr(o, "d" + short, atd(key))
+        o.shift = float(shift)
+        _native._check(lib.nft_amp_vjp_batched(ctypes.byref(const), ctypes.c_void_p(g.data_ptr()), ctypes.byref(o),
+                                               ctypes.c_void_p(ws.data_ptr()), k, size, self.B,
+                                               _native.stream_ptr()))
+        return Q
+
     def native_jvp(self, const, t, da):
         g = t.get
         _native.amp_jvp(const, g(self.k_fl), g(self.k_sl), g(self.k_flex), g(self.k_asp),
@@ -357,6 +398,44 @@ class CFJacobian(LinearOperator):
         res = self._adjoint_t(W(s) if callable(W) else s * W)
         return MultiField(self._domain, tuple(Field(self._domain[k], res[k].reshape(self._domain[k].shape))
                                               for k in self._domain.keys()))
+
+    def metric_flat_batch(self, D, Q, W, shift):
+        """Q[b] = shift * D[b] + J^T W J D[b] for the k rows of D (k, size),
+        every stage launched once for the whole batch (nft_*_batched; the LOS
+        matrix is streamed once for all rows).  Per row bitwise equal to
+        metric_flat."""
+        m = self._m
+        lay = self.layout
+        k, size = D.shape
+        amp = m.amp
+        B = amp.B
+        grid = tuple(self._afull.shape)
+        N = self._afull.numel()
+        off = dict(zip(lay.keys, lay.offsets))
+        xo = off[m.k_xi]
+        axes = tuple(range(1, 1 + len(grid)))
+        conv = hartley_convention_code()
+        const = self._const()
+        da = torch.empty((k, B), dtype=torch.float64, device=self.device)
+        amp.native_jvp_batched(const, D, off, da)
+        s = torch.empty((k,) + grid, dtype=self._afull.dtype, device=self.device)
+        pro = dict(a=self._afull, x=D[0, xo:], b=self._xi0, c=da, index=m.bins.pindex)
+        _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
+                              batch=dict(period=N, x=size, c=B))
+        g = W(s) if callable(W) else s * W
+        g = g.contiguous()
+        w = torch.empty((k,) + grid, dtype=self._afull.dtype, device=self.device)
+        epi = dict(a=self._afull, b=self._xi0, out2=w)
+        bt = dict(period=N, out=size, out2=N)
+        if shift != 0.0:
+            epi.update(d=D[0, xo:], shift=shift)
+            bt["d"] = size
+        _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt)
+        ga = torch.empty((k, B), dtype=w.dtype, device=self.device)
+        b = m.bins
+        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1)
+        amp.native_vjp_batched(const, ga, Q, off, D, shift)
+        return Q
 
     def metric_flat(self, d, q, W, shift):
         """q = shift * d + J^T W J d on packed latent buffers (fused CG)."""

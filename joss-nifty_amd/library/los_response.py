@@ -133,6 +133,7 @@ def los_coo(shape, distances, starts, ends, sigmas=None, truncation=3.):
 
 
 LOS_CAP_F = 2048   # entries per forward work item (csrc/nft_los.hip)
+LOS_KMAX = 8       # vectors per batched LOS launch (csrc/nft_los.hip)
 BOX = 256
 
 
@@ -324,13 +325,28 @@ class LOSResponse(LinearOperator):
 
         plan = self._box_plan()
 
+        npix = int(np.prod(shape))
+
         def middle(s):
+            if s.dim() > len(shape):
+                # batch of right-hand sides along a leading axis (batched CG):
+                # the matrix is streamed once per launch for all of them
+                k = s.shape[0]
+                v = s.reshape(k, npix).contiguous()
+                y = torch.empty((k, nlos), dtype=v.dtype, device=v.device)
+                out = torch.empty((k,) + tuple(shape), dtype=v.dtype, device=v.device)
+                for a in range(0, k, LOS_KMAX):
+                    b = min(k, a + LOS_KMAX)
+                    _native.los_forward_batched(plan, v[a:b], y[a:b], colscale=drf, rowscale=cv, scale=scale)
+                    _native.los_adjoint_batched(plan, y[a:b], out[a:b].view(b - a, npix), rowscale=drf)
+                return out
             v = s.reshape(-1).contiguous()
             y = torch.empty(nlos, dtype=v.dtype, device=v.device)
             _native.los_forward(plan, v, y, colscale=drf, rowscale=cv, scale=scale)
             out = torch.empty(shape, dtype=v.dtype, device=v.device)
             _native.los_adjoint(plan, y, out.view(-1), rowscale=drf)
             return out
+        middle.supports_batch = True
         return middle
 
     @property

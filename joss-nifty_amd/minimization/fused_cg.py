@@ -214,3 +214,199 @@ class FusedCG:
             status = ctl.check(state)
             if status != ctl.CONTINUE:
                 return self._energy(A, b_mf, x, r), status
+
+
+def batch_supported(core, W):
+    """True if the fused metric can evaluate a batch of right-hand sides."""
+    if not hasattr(core, "metric_flat_batch"):
+        return False
+    return (not callable(W)) or getattr(W, "supports_batch", False)
+
+
+def fused_cg_batch_or_none(energies, controllers, nreset):
+    """Solve several QuadraticEnergies with the SAME fused sampling metric in
+    one batched loop (FusedCGBatch), or None if that does not apply."""
+    from .quadratic_energy import QuadraticEnergy
+    if len(energies) < 2 or any(type(e) is not QuadraticEnergy for e in energies):
+        return None
+    A = energies[0].metric
+    if any(e.metric is not A for e in energies):
+        return None
+    if len({e._b is None for e in energies}) != 1:
+        return None
+    spec = fusable_metric(A)
+    if spec is None:
+        return None
+    core, W, shift = spec
+    if not batch_supported(core, W) or not core.device.type == "cuda":
+        return None
+    if any(e.position.domain != core.domain for e in energies):
+        return None
+    return FusedCGBatch(core, W, shift, controllers, nreset).run(energies)
+
+
+class FusedCGBatch(FusedCG):
+    """k independent conjugate-gradient solves with the same metric, run in
+    lock step: every iteration is ONE batched matvec (the LOS matrix, the FFT
+    passes and the amplitude kernels each launched once for all right-hand
+    sides) and ONE set of batched CG kernels.  Each right-hand side keeps its
+    own scalars, guards and controller (a deep copy of the caller's, started
+    on its own energy, exactly as a sequential solve would); once it stops,
+    sc[DONE] freezes it on the device.  Per right-hand side the arithmetic is
+    bitwise that of FusedCG (and of solving the systems one after another)."""
+
+    def __init__(self, core, W, shift, controllers, nreset=20):
+        super().__init__(core, W, shift, controllers[0], nreset)
+        self.controllers = controllers
+
+    def run(self, energies):
+        k = len(energies)
+        lay, core = self.layout, self.core
+        n = lay.size
+        results = [None] * k
+        active = []
+        for j, (e, ctl) in enumerate(zip(energies, self.controllers)):
+            st = ctl.start(e)
+            if st != ctl.CONTINUE:
+                results[j] = (e, st)
+            else:
+                active.append(j)
+        if not active:
+            return results
+        dev = core.device
+        X = torch.zeros((k, n), dtype=torch.float64, device=dev)
+        Rr = torch.zeros_like(X)
+        Bv = torch.zeros_like(X) if energies[0]._b is not None else None
+        for j, e in enumerate(energies):
+            lay.pack(e.position, out=X[j])
+            lay.pack(e.gradient, out=Rr[j])
+            if Bv is not None:
+                lay.pack(e._b, out=Bv[j])
+        D = Rr.clone()
+        Q = torch.zeros_like(X)
+        AX = None
+        NS = _native.CG_NSCALARS
+        SC = torch.zeros((k, NS), dtype=torch.float64, device=dev)
+        host = torch.zeros((k, NS), dtype=torch.float64).pin_memory()
+        lib = _native.load()
+        ws = _native.workspace(k * lib.nft_reduce_workspace(n), dev, "cgb")
+        dt = _native.dtype_code(X.dtype)
+        P = _native.ptr
+        sh = self.shift
+        A = energies[0].metric
+
+        def chk(st):
+            _native._check(st)
+
+        def energy_of(j):
+            from .quadratic_energy import QuadraticEnergy
+            return QuadraticEnergy(lay.unpack(X[j]), A, energies[j]._b, _grad=lay.unpack(Rr[j]))
+
+        def finish(j, status):
+            results[j] = (energy_of(j), status)
+            SC[j, _native.CG_DONE] = 1.0
+
+        for j in range(k):
+            if results[j] is not None:
+                SC[j, _native.CG_DONE] = 1.0
+        chk(lib.nft_dot_batched(P(Rr), P(Rr), n, n, k, dt, P(SC[:, _native.CG_GAMMA:]), NS, P(ws),
+                                _native.stream_ptr()))
+        host.copy_(SC)
+        for j in list(active):
+            g = float(host[j, _native.CG_GAMMA])
+            if np.isnan(g):
+                logger.error("Error: ConjugateGradient: previous_gamma==NaN")
+                results[j] = (energies[j], self.controllers[j].ERROR)
+            elif g == 0:
+                results[j] = (energies[j], self.controllers[j].CONVERGED)
+            if results[j] is not None:
+                SC[j, _native.CG_DONE] = 1.0
+                active.remove(j)
+        if not active:
+            return results
+
+        def body(with_dir):
+            s_ = _native.stream_ptr()
+            if with_dir:
+                chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), s_))
+            core.metric_flat_batch(D, Q, self.W, 0.0)
+            chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), s_))
+            chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bv), n, n, k, dt, sh, P(SC), P(ws), s_))
+
+        graph = None
+        ii = 0
+        first = True
+        while active:
+            self.niter += 1
+            ConjugateGradient.iterations_total += len(active)
+            ii += 1
+            sp = _native.stream_ptr()
+            if ii < self.nreset:
+                if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER:
+                    body(not first)
+                elif graph is None:
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph):
+                        body(True)
+                    graph.replay()
+                else:
+                    graph.replay()
+                first = False
+            else:
+                if not first:
+                    chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), sp))
+                first = False
+                core.metric_flat_batch(D, Q, self.W, 0.0)
+                chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), sp))
+                gp = SC[:, _native.CG_GAMMA].clone()
+                chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bv), n, n, k, dt, sh, P(SC), P(ws), sp))
+                if AX is None:
+                    AX = torch.zeros_like(X)
+                core.metric_flat_batch(X, AX, self.W, 0.0)
+                flag = SC[:, _native.CG_FLAG].clone()
+                chk(lib.nft_cg_residual_batched(P(Rr), P(AX), P(X), P(Bv), n, n, k, dt, sh, P(SC), P(ws), sp))
+                live = SC[:, _native.CG_DONE] == 0.0
+                SC[:, _native.CG_GPREV] = torch.where(live, gp, SC[:, _native.CG_GPREV])
+                SC[:, _native.CG_FLAG] = torch.where(live, flag, SC[:, _native.CG_FLAG])
+                ii = 0
+            host.copy_(SC, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            h = host.numpy()
+            for j in list(active):
+                ctl = self.controllers[j]
+                hj = h[j]
+                status = None
+                if hj[_native.CG_FLAG] != 0.0:
+                    curv = hj[_native.CG_CURV]
+                    if np.isnan(curv):
+                        logger.error("Error: ConjugateGradient: curv==NaN")
+                    elif curv == 0.:
+                        logger.error("Error: ConjugateGradient: curv==0.")
+                    else:
+                        logger.error("Error: ConjugateGradient: alpha<0.")
+                    status = ctl.ERROR
+                else:
+                    gamma = float(hj[_native.CG_GAMMA])
+                    if np.isnan(gamma):
+                        logger.error("Error: ConjugateGradient: gamma==NaN")
+                        status = ctl.ERROR
+                    elif gamma < 0:
+                        logger.error("Positive definiteness of preconditioner violated!")
+                        status = ctl.ERROR
+                    elif gamma == 0:
+                        status = ctl.CONVERGED
+                    else:
+                        cache = {}
+
+                        def lazy(j=j, cache=cache):
+                            if "v" not in cache:
+                                cache["v"] = (lay.unpack(X[j]), lay.unpack(Rr[j]))
+                            return cache["v"]
+                        value = 0.5 * (float(hj[_native.CG_XR]) - float(hj[_native.CG_XB]))
+                        st = ctl.check(_State(value, math.sqrt(gamma), lazy))
+                        if st != ctl.CONTINUE:
+                            status = st
+                if status is not None:
+                    finish(j, status)
+                    active.remove(j)
+        return results

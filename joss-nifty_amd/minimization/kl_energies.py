@@ -59,22 +59,36 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
     y = None
     ntask, rank, _ = get_MPI_params_from_comm(comm)
     lo, hi = shareRange(len(sseq), ntask, rank)
-    prefetched = False
-    for i in range(lo, hi):
+    # The local samples' linear solves are independent and share the metric:
+    # draw every right-hand side first (each in its own RNG context, as the
+    # reference does), solve them together (FusedCGBatch: one batched matvec
+    # per CG iteration for all of them), then refine / collect each sample in
+    # order.  Per sample the arithmetic is that of the reference's loop.
+    drawing = [i for i in range(lo, hi) if not (mirror_samples and i % 2 != 0) or i == lo]
+    batched = hasattr(met, "draw_rhs")
+    prepared, prefetched = {}, False
+    for i in drawing:
         ctx = random.Context(sseq[i])
         with ctx:
+            prepared[i] = met.draw_rhs(True) if batched else met.special_draw_sample(True)
+        if not prefetched:
+            # host RNG off the critical path: replay this sample's draws for
+            # the remaining local seeds and the next call's seeds
+            prefetched = True
+            nxt = random.predict_spawn(n_samples, parent)
+            if mirror_samples:
+                nxt = [ss for ss in nxt for _ in range(2)]
+            todo = _distinct([sseq[j] for j in drawing if sseq[j] is not sseq[i]]) + _distinct(nxt[lo:hi])
+            random.prefetch(todo, ctx.script)
+    if batched:
+        sols = met.solve_rhs([prepared[i] for i in drawing])
+        prepared = dict(zip(drawing, sols))
+    y = None
+    for i in range(lo, hi):
+        with random.Context(sseq[i]):
             neg = mirror_samples and (i % 2 != 0)
             if not neg or y is None:
-                y, yi = met.special_draw_sample(True)
-                if not prefetched:
-                    # host RNG off the critical path: replay this sample's draws
-                    # for the remaining local seeds and the next call's seeds
-                    prefetched = True
-                    nxt = random.predict_spawn(n_samples, parent)
-                    if mirror_samples:
-                        nxt = [ss for ss in nxt for _ in range(2)]
-                    todo = _distinct([ss for ss in sseq[i + 1:hi] if ss is not sseq[i]]) + _distinct(nxt[lo:hi])
-                    random.prefetch(todo, ctx.script)
+                y, yi = prepared[i]
             if geometric:
                 m = transformation_mean - y if neg else transformation_mean + y
                 pos = sam_position - yi if neg else sam_position + yi

@@ -20,6 +20,54 @@ class SamplingEnabler(EndomorphicOperator):
         self._capability = self._op.capability
         self.apply = self._op.apply
 
+    def draw_rhs(self, from_inverse=True):
+        """First half of special_draw_sample: the random draws and the CG
+        problem.  Returns ("done", (b, x)) when the operator samples directly,
+        else ("cg", energy)."""
+        try:
+            res = self._op.draw_sample(from_inverse)
+            return "done", (self._op(res), res)
+        except NotImplementedError:
+            if not from_inverse:
+                raise ValueError("from_inverse must be True here")
+            if self._start_from_zero:
+                b = self._op.draw_sample()
+                return "cg", QuadraticEnergy(0 * b, self._op, b)
+            s = self._prior.draw_sample(from_inverse=True)
+            nj = self._likelihood.draw_sample()
+            b = self._prior(s) + nj
+            return "cg", QuadraticEnergy(s, self._op, b, _grad=self._likelihood(s) - nj)
+
+    def solve_rhs(self, prepared):
+        """Second half for a list of draw_rhs results: the CG solves, batched
+        into one lock-step solve (minimization/fused_cg.FusedCGBatch) when the
+        metric allows, otherwise one after another.  Returns [(b, x)]."""
+        import copy
+        out = [None] * len(prepared)
+        todo = [j for j, (kind, _) in enumerate(prepared) if kind == "cg"]
+        for j, (kind, v) in enumerate(prepared):
+            if kind == "done":
+                out[j] = v
+        if not todo:
+            return out
+        energies = [prepared[j][1] for j in todo]
+        res = None
+        if self._approximation is None and len(todo) > 1:
+            from ..minimization.fused_cg import fused_cg_batch_or_none
+            ctls = [copy.deepcopy(self._ic) for _ in todo]
+            res = fused_cg_batch_or_none(energies, ctls, ConjugateGradient(self._ic)._nreset)
+        if res is None:
+            res = []
+            for e in energies:
+                inverter = ConjugateGradient(self._ic)
+                if self._approximation is not None:
+                    res.append(inverter(e, preconditioner=self._approximation.inverse))
+                else:
+                    res.append(inverter(e))
+        for j, e, (en, _) in zip(todo, energies, res):
+            out[j] = (e._b, en.position)
+        return out
+
     def special_draw_sample(self, from_inverse=False):
         try:
             res = self._op.draw_sample(from_inverse)

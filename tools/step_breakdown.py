@@ -40,6 +40,8 @@ def main(steps=3):
         return r
     R._take = take
     SE.SamplingEnabler.special_draw_sample = timed("special_draw_sample", SE.SamplingEnabler.special_draw_sample)
+    SE.SamplingEnabler.draw_rhs = timed("draw_rhs", SE.SamplingEnabler.draw_rhs)
+    SE.SamplingEnabler.solve_rhs = timed("solve_rhs (batched CG)", SE.SamplingEnabler.solve_rhs)
     DM.DescentMinimizer.__call__ = timed("newton", DM.DescentMinimizer.__call__)
     ift.random.push_sseq_from_seed(1000)
     for i in range(steps + 1):
@@ -48,7 +50,7 @@ def main(steps=3):
             hits[:] = [0, 0]
         torch.cuda.synchronize()
         t = time.perf_counter()
-        sl = ift.draw_samples(pos, H, mini, 1, True)
+        sl = ift.draw_samples(pos, H, mini, 4, True)
         ift.SampledKLEnergyClass(sl, H, [], None, True)
         torch.cuda.synchronize()
         T["step"] += time.perf_counter() - t if i else 0
