@@ -12,7 +12,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnifty_amd.so")
+LIB_PATH = os.environ.get("NFT_LIB") or os.path.join(_HERE, "libnifty_amd.so")
 
 # names and argument signatures of every exported symbol (kept in sync with
 # include/nifty_amd.h; tests/test_abi.py checks both directions)

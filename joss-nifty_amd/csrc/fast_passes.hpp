@@ -95,8 +95,14 @@ constexpr bool persist_ok() {
   return N <= 2048 && NT <= 256 && KIND != K_H1D;
 }
 
+#ifdef NFT_FFT_WPE
+#define NFT_FFT_ATTR __attribute__((amdgpu_waves_per_eu(NFT_FFT_WPE)))
+#else
+#define NFT_FFT_ATTR
+#endif
+
 template <typename T, int N, int NT, int KIND, bool ROWS>
-__global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
+__global__ __launch_bounds__(NT) NFT_FFT_ATTR void fast_kernel(FastArgs<T> a) {
   // Persistent: workgroup b processes tiles b, b + G, b + 2G, ...  The input
   // of tile t + G is loaded into registers while tile t is transformed and
   // stored, so each workgroup keeps loads, LDS work and stores in flight at

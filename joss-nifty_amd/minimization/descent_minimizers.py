@@ -73,7 +73,10 @@ class NewtonCG(DescentMinimizer):
             ic = AbsDeltaEnergyController(ediff, iteration_limit=self._max_cg_iterations, name=self._name)
         if self._history is not None:
             ic.enable_logging()
-        e = QuadraticEnergy(0 * energy.position, energy.metric, energy.gradient)
+        # CG from x0 = 0: the metric is linear, so A(x0) - b is -b and the
+        # reference's metric application on the zero vector is skipped
+        g = energy.gradient
+        e = QuadraticEnergy(0 * energy.position, energy.metric, g, _grad=-g)
         e, conv = ConjugateGradient(ic, nreset=self._nreset)(e, None)
         if self._history is not None:
             self._history += ic.history

@@ -74,6 +74,37 @@ class _State:
         return self._lazy()[1]
 
 
+_CAPTURE_STREAM = None
+
+
+def _capture(fn):
+    """HIP graph of the launches fn makes.  Same capture as the
+    torch.cuda.graph context manager, minus its device synchronize, gc.collect
+    and empty_cache preamble (milliseconds per capture, paid per CG solve)."""
+    global _CAPTURE_STREAM
+    if _CAPTURE_STREAM is None:
+        _CAPTURE_STREAM = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    cur = torch.cuda.current_stream()
+    _CAPTURE_STREAM.wait_stream(cur)
+    with torch.cuda.stream(_CAPTURE_STREAM):
+        g.capture_begin()
+        try:
+            fn()
+        finally:
+            g.capture_end()
+    cur.wait_stream(_CAPTURE_STREAM)
+    return g
+
+
+def _worth_capturing(ctl, niter, min_left=4):
+    """Capture only if the controller's iteration limit leaves at least
+    `min_left` more iterations to replay (short solves, e.g. NewtonCG's first
+    5-iteration direction, stay eager)."""
+    lim = getattr(ctl, "_iteration_limit", None)
+    return lim is None or lim - niter >= min_left
+
+
 def fused_cg_or_none(energy, controller, nreset):
     from .quadratic_energy import QuadraticEnergy
     if type(energy) is not QuadraticEnergy:
@@ -157,12 +188,13 @@ class FusedCG:
                 if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER:
                     body(not first)
                 elif graph is None:
-                    # capture dir + matvec + dot + update once (HIP graph); the
-                    # eager first iteration has warmed every workspace/twiddle cache
-                    graph = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(graph):
+                    if _worth_capturing(ctl, self.niter):
+                        # capture dir + matvec + dot + update once (HIP graph); the
+                        # eager iterations have warmed every workspace/twiddle cache
+                        graph = _capture(lambda: body(True))
+                        graph.replay()
+                    else:
                         body(True)
-                    graph.replay()
                 else:
                     graph.replay()
                 first = False
@@ -345,10 +377,11 @@ class FusedCGBatch(FusedCG):
                 if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER:
                     body(not first)
                 elif graph is None:
-                    graph = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(graph):
+                    if any(_worth_capturing(self.controllers[j], self.niter) for j in active):
+                        graph = _capture(lambda: body(True))
+                        graph.replay()
+                    else:
                         body(True)
-                    graph.replay()
                 else:
                     graph.replay()
                 first = False

@@ -9,13 +9,23 @@ class QuadraticEnergy(Energy):
         self._b = b
         if _grad is not None:
             self._grad = _grad
-            Ax = _grad if b is None else _grad + b
+            self._Ax = None
         else:
-            Ax = self._A(self._position)
-            self._grad = Ax if b is None else Ax - b
-        self._value = 0.5 * self._position.s_vdot(Ax).real
-        if b is not None:
-            self._value -= b.s_vdot(self._position).real
+            self._Ax = self._A(self._position)
+            self._grad = self._Ax if b is None else self._Ax - b
+        self._value = None
+
+    def _compute_value(self):
+        # evaluated on first use (the same expression, in the same order, as
+        # the reference evaluates eagerly): CG and NewtonCG only read the
+        # position / gradient of most energies, and each dot is a host sync
+        Ax = self._Ax
+        if Ax is None:
+            Ax = self._grad if self._b is None else self._grad + self._b
+        v = 0.5 * self._position.s_vdot(Ax).real
+        if self._b is not None:
+            v -= self._b.s_vdot(self._position).real
+        return v
 
     def at(self, position):
         return QuadraticEnergy(position, self._A, self._b)
@@ -25,6 +35,8 @@ class QuadraticEnergy(Energy):
 
     @property
     def value(self):
+        if self._value is None:
+            self._value = self._compute_value()
         return self._value
 
     @property

@@ -43,11 +43,24 @@ def main(steps=3):
     SE.SamplingEnabler.draw_rhs = timed("draw_rhs", SE.SamplingEnabler.draw_rhs)
     SE.SamplingEnabler.solve_rhs = timed("solve_rhs (batched CG)", SE.SamplingEnabler.solve_rhs)
     DM.DescentMinimizer.__call__ = timed("newton", DM.DescentMinimizer.__call__)
+    DM.NewtonCG.get_descent_direction = timed("  newton direction (CG)", DM.NewtonCG.get_descent_direction)
+    from nifty_amd.minimization import energy_adapter as EA, line_search as LS, conjugate_gradient as CGm
+    EA.EnergyAdapter.__init__ = timed("  energy evaluations", EA.EnergyAdapter.__init__)
+    LS.LineSearch.perform_line_search = timed("  line search", LS.LineSearch.perform_line_search)
+    ncall = [0]
+    orig_ea = EA.EnergyAdapter.__init__
+
+    def ea_count(*a, **k):
+        ncall[0] += 1
+        return orig_ea(*a, **k)
+    EA.EnergyAdapter.__init__ = ea_count
     ift.random.push_sseq_from_seed(1000)
     for i in range(steps + 1):
         if i == 1:
             T.clear()
             hits[:] = [0, 0]
+            ncall[0] = 0
+            it0 = CGm.ConjugateGradient.iterations_total
         torch.cuda.synchronize()
         t = time.perf_counter()
         sl = ift.draw_samples(pos, H, mini, 4, True)
@@ -57,6 +70,8 @@ def main(steps=3):
     for k, v in T.items():
         print(f"{k:24s} {v / steps * 1e3:8.1f} ms/step")
     print("prefetch misses/hits", hits)
+    print("energy evaluations/step", ncall[0] / steps,
+          "CG iterations/step", (CGm.ConjugateGradient.iterations_total - it0) / steps)
 
 
 if __name__ == "__main__":
