@@ -33,8 +33,7 @@ inline void fourstep_split(int N, int& N1, int& N2) {
 template <typename T, int N, int NT, int KIND, bool ROWS>
 static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   constexpr int L = NT * VPT / N;
-  constexpr int PITCH = ROWS ? N : N + 1;
-  size_t lds = (size_t)L * PITCH * sizeof(cplx_t<T>) + (KIND == K_UNPACK ? (size_t)L * sizeof(UnpackLine) : 0);
+  const size_t lds = pass_lds_bytes<T, N, NT, KIND, ROWS>();
   long long ntiles;
   if (ROWS) {
     long long nl = (KIND == K_R2C || KIND == K_H1D) ? (a.Ireal + 1) / 2 : a.g.O;
@@ -50,14 +49,17 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   if (lds > 65536) {
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS>,
+      (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if constexpr (persist_ok<N, NT, KIND>())
+        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
   }
   FastArgs<T> b = a;
   b.ntiles = ntiles;
-  // persistent grid: enough workgroups to fill every CU twice over
+  // persistent grid (plain R2C rows): per_cu workgroups per CU
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0, v = 0;
@@ -68,13 +70,19 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
       ncu = 256;
   }
   static const int per_cu = getenv("NFT_FFT_WG_PER_CU") ? atoi(getenv("NFT_FFT_WG_PER_CU")) : 8;
-  const long long grid = persist_ok<N, NT, KIND>()
-                             ? std::min<long long>(ntiles, (long long)ncu * std::max(1, per_cu))
-                             : ntiles;
   static const char* const kind_name[4] = {"fft_c2c", "fft_r2c", "fft_h1d", "fft_unpack"};
   static const char* const kind_fused[4] = {"fft_c2c", "fft_r2c+pro", "fft_h1d+fused", "fft_unpack+epi"};
   prof_mark(s, (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
-  hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS>), dim3((unsigned)grid), dim3(NT), lds, s, b);
+  bool launched = false;
+  if constexpr (persist_ok<N, NT, KIND>()) {
+    if (!a.f.pro) {
+      const long long grid = std::min<long long>(ntiles, (long long)ncu * std::max(1, per_cu));
+      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, true>), dim3((unsigned)grid), dim3(NT), lds, s, b);
+      launched = true;
+    }
+  }
+  if (!launched)
+    hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

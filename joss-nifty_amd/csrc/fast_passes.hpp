@@ -87,22 +87,32 @@ template <typename T> struct FastArgs {
   long long ntiles;   // tiles of the pass (set by the launcher)
 };
 
-// Persistent, prefetching tile loop only where the extra live registers fit
-// (256-thread workgroups, N <= 2048); other shapes keep one tile per
-// workgroup.  1-D Hartley rows (H1D) are not on the sampling path.
+// Persistent, prefetching tile loop: measured faster only for the plain
+// real-to-complex row pass (256-thread workgroups, N <= 2048).  Everywhere
+// else -- strided passes, and the R2C pass with a prologue, whose gathers
+// cannot be prefetched -- one tile per workgroup at the lower register count
+// (more resident waves) wins.
 template <int N, int NT, int KIND>
 constexpr bool persist_ok() {
-  return N <= 2048 && NT <= 256 && KIND != K_H1D;
+  return N <= 2048 && NT <= 256 && KIND == K_R2C;
 }
 
-#ifdef NFT_FFT_WPE
-#define NFT_FFT_ATTR __attribute__((amdgpu_waves_per_eu(NFT_FFT_WPE)))
-#else
-#define NFT_FFT_ATTR
-#endif
-
+// dynamic LDS of a pass: L lines (+ the unpack line table), then the
+// quarter twiddle table (N/4 entries) at a 16-byte aligned offset
 template <typename T, int N, int NT, int KIND, bool ROWS>
-__global__ __launch_bounds__(NT) NFT_FFT_ATTR void fast_kernel(FastArgs<T> a) {
+constexpr size_t tw_lds_offset() {
+  constexpr int L = NT * VPT / N;
+  constexpr int PITCH = ROWS ? N : N + 1;
+  return ((size_t)L * PITCH * sizeof(cplx_t<T>) + (KIND == K_UNPACK ? (size_t)L * sizeof(UnpackLine) : 0) + 15) &
+         ~(size_t)15;
+}
+template <typename T, int N, int NT, int KIND, bool ROWS>
+constexpr size_t pass_lds_bytes() {
+  return tw_lds_offset<T, N, NT, KIND, ROWS>() + (size_t)(N / 4) * sizeof(cplx_t<T>);
+}
+
+template <typename T, int N, int NT, int KIND, bool ROWS, bool PF>
+__global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   // Persistent: workgroup b processes tiles b, b + G, b + 2G, ...  The input
   // of tile t + G is loaded into registers while tile t is transformed and
   // stored, so each workgroup keeps loads, LDS work and stores in flight at
@@ -116,6 +126,8 @@ __global__ __launch_bounds__(NT) NFT_FFT_ATTR void fast_kernel(FastArgs<T> a) {
   constexpr int SHN = ilog2(N), SHL = ilog2(L);
   extern __shared__ __align__(16) unsigned char smem[];
   C* lds = (C*)smem;
+  C* twq = (C*)(smem + tw_lds_offset<T, N, NT, KIND, ROWS>());
+  for (int r = threadIdx.x; r < N / 4; r += NT) twq[r] = ((const C*)a.tw)[r];  // synced before the first stage
   const int tid = threadIdx.x;
   const Lines& g = a.g;
   const long long ntiles = a.ntiles;
@@ -182,8 +194,8 @@ __global__ __launch_bounds__(NT) NFT_FFT_ATTR void fast_kernel(FastArgs<T> a) {
     }
   };
 
-  constexpr bool PERSIST = persist_ok<N, NT, KIND>();
-  const bool prefetch = PERSIST && !((KIND == K_R2C || KIND == K_H1D) && a.f.pro);
+  constexpr bool PERSIST = PF;
+  constexpr bool prefetch = PF;  // launched persistent only without a prologue
   C rv[VPT];
   long long t = blockIdx.x;
   if (prefetch && t < ntiles) load(t, rv);
@@ -198,7 +210,7 @@ __global__ __launch_bounds__(NT) NFT_FFT_ATTR void fast_kernel(FastArgs<T> a) {
     __syncthreads();
     const long long tn = PERSIST ? t + gridDim.x : ntiles;
     if (prefetch && tn < ntiles) load(tn, rv);  // in flight during the FFT and the stores
-    fft<T, N, NT, L, PITCH>(lds, (const C*)a.tw, tid);
+    fft<T, N, NT, L, PITCH>(lds, twq, tid);
     long long o, m, i0;
     tile_of(t, o, m, i0);
 

@@ -37,6 +37,20 @@ struct Lines {
   long long out_so, out_sm, out_si, out_sn;
 };
 
+// W_N^m from the quarter table twq[r] = W_N^r (r < N/4) held in LDS:
+// W_N^(m) = (-i)^q W_N^(m mod N/4), q = m div N/4 -- swaps and negations
+// only, so the value is the full table's entry bit for bit (nft_fft.hip:
+// twiddle_host builds the table by the same rotations).
+template <typename T, int N>
+__device__ __forceinline__ cplx_t<T> tw_at(const cplx_t<T>* twq, int m) {
+  constexpr int SHQ = ilog2(N) - 2;
+  const int q = m >> SHQ;
+  cplx_t<T> w = twq[m & ((N >> 2) - 1)];
+  if (q & 1) w = cplx_t<T>{w.y, -w.x};
+  if (q & 2) w = cplx_t<T>{-w.x, -w.y};
+  return w;
+}
+
 // -------------------------------------------------------------- one stage
 template <typename T, int N, int NT, int L, int PITCH, int R, int NS>
 __device__ __forceinline__ void stage(cplx_t<T>* lds, const cplx_t<T>* __restrict__ tw, int tid) {
@@ -69,7 +83,7 @@ __device__ __forceinline__ void stage(cplx_t<T>* lds, const cplx_t<T>* __restric
       if constexpr (NS > 1) {
         const int step = k * TSTRIDE;
 #pragma unroll
-        for (int t = 1; t < R; ++t) v[i][t] = cmul(v[i][t], tw[t * step]);
+        for (int t = 1; t < R; ++t) v[i][t] = cmul(v[i][t], tw_at<T, N>(tw, t * step));
       }
       dftR<T, R>(v[i]);
       C* dst = lds + line * PITCH + (j - k) * R + k;
@@ -89,7 +103,8 @@ __device__ __forceinline__ void stages(cplx_t<T>* lds, const cplx_t<T>* __restri
   }
 }
 
-// forward FFT of the L lines in LDS (caller synced after filling)
+// forward FFT of the L lines in LDS (caller synced after filling); tw is the
+// LDS quarter twiddle table (tw_at)
 template <typename T, int N, int NT, int L, int PITCH>
 __device__ __forceinline__ void fft(cplx_t<T>* lds, const cplx_t<T>* __restrict__ tw, int tid) {
   stages<T, N, NT, L, PITCH, 1>(lds, tw, tid);

@@ -52,26 +52,53 @@ static std::mutex g_tw_mu;
 
 // exp(-2 pi i k / n) with exact symmetries (octant reduction in long double)
 static void twiddle_host(int n, std::vector<long double>& re, std::vector<long double>& im) {
+  // W^k = exp(-2 pi i k/n), k < n.  Built from the first quadrant by exact
+  // rotations, W^(k + n/4) = -i W^k, so the device may keep only the quarter
+  // table (fft_fast.hpp: tw_at) and reproduce every entry bit for bit; inside
+  // the quadrant the octant symmetry keeps the evaluated angle <= pi/4.
   re.resize(n);
   im.resize(n);
   const long double pi = 3.141592653589793238462643383279502884L;
+  if (n % 4 != 0) {  // lengths of the generic engine: direct evaluation
+    for (int k = 0; k < n; ++k) {
+      const long double a = 2.0L * pi * (long double)k / (long double)n;
+      long double c = cosl(a), s = sinl(a);
+      if (2LL * k == n) {
+        c = -1;
+        s = 0;
+      }
+      if (k == 0) {
+        c = 1;
+        s = 0;
+      }
+      re[k] = c;
+      im[k] = -s;
+    }
+    return;
+  }
+  const int q4 = n / 4;
+  std::vector<long double> c0(q4), s0(q4);
+  for (int r = 0; r < q4; ++r) {
+    if (8LL * r <= n) {
+      const long double a = 2.0L * pi * (long double)r / (long double)n;
+      c0[r] = cosl(a);
+      s0[r] = sinl(a);
+    } else {  // pi/2 - a' with a' = 2 pi (n/4 - r)/n <= pi/4
+      const long double a = 2.0L * pi * (long double)(q4 - r) / (long double)n;
+      c0[r] = sinl(a);
+      s0[r] = cosl(a);
+    }
+  }
   for (int k = 0; k < n; ++k) {
-    // reduce k/n to [0, 1/8] using symmetries of cos/sin
-    long long num = (long long)k * 8;  // angle/(2pi) = k/n ; octant = floor(8k/n)
-    int oct = (int)(num / n);
-    long double c, s;
-    // direct evaluation is accurate to ~1e-19 in long double; symmetries keep
-    // exact zeros / ones at the axes
-    long double ang = 2.0L * pi * (long double)k / (long double)n;
-    c = cosl(ang);
-    s = sinl(ang);
-    if ((long long)4 * k == n) { c = 0; s = 1; }
-    if ((long long)2 * k == n) { c = -1; s = 0; }
-    if ((long long)4 * k == 3LL * n) { c = 0; s = -1; }
-    if (k == 0) { c = 1; s = 0; }
-    (void)oct;
-    re[k] = c;
-    im[k] = -s;
+    const int q = k / q4, r = k - q * q4;
+    long double wr = c0[r], wi = -s0[r];
+    for (int t = 0; t < q; ++t) {  // multiply by -i
+      const long double tmp = wr;
+      wr = wi;
+      wi = -tmp;
+    }
+    re[k] = wr;
+    im[k] = wi;
   }
 }
 
