@@ -91,20 +91,12 @@ def build_problem(ift, n, nlos):
     return cf, R, lh, pos, (starts, ends)
 
 
-def kernel_probe(ift, cf, R, lh, pos, reps=10):
-    """Per-kernel durations of one sampling-metric matvec M d = d + J^T W J d at
-    the bench expansion point -- the matvec the timed CG loop runs -- measured
-    with HIP events recorded on the launch stream before every hot-path launch
-    (nft_prof_*; the same kernels with the same arguments as inside the timed
-    region, run eagerly because events cannot be timed inside a HIP graph).
-
-    Returns {label: {"launches": per matvec, "avg_us", "bytes": algorithmic
-    bytes per launch, "gbs"}} with the algorithmic-byte model of DESIGN.md
-    §Measurement (every operand array counted once per launch, fp64)."""
-    from nifty_amd import _native
+def probe_setup(ift, lh, pos, k):
+    """The linear geoVI sampling metric exactly as draw_samples builds it
+    (kl_energies.py:147-153, 1 + J^T J of the likelihood's transformation),
+    its fused core, and k random right-hand-side buffers laid out like
+    FusedCGBatch's (k, latent) blocks."""
     from nifty_amd.minimization.fused_cg import fusable_metric
-    # the linear geoVI sampling metric exactly as draw_samples builds it
-    # (kl_energies.py:147-153): 1 + J^T J of the likelihood's transformation
     dtype, f_lh = lh.get_transformation()
     fl = f_lh(ift.Linearization.make_var(pos))
     met = (ift.SandwichOperator.make(fl.jac, ift.ScalingOperator(f_lh.target, 1., dtype))
@@ -113,24 +105,28 @@ def kernel_probe(ift, cf, R, lh, pos, reps=10):
     assert spec is not None, "bench metric did not fuse"
     core, W, shift = spec
     lay = core.layout
-    d = lay.pack(ift.from_random(cf.domain, "normal"))
-    q = lay.empty()
-    # FusedCG forms q' = M' d without the identity shift (its CG kernels add
-    # shift*d element-wise), so the probe does the same
-    for _ in range(3):
-        core.metric_flat(d, q, W, 0.0)
-    torch.cuda.synchronize()
-    # keep the GPU busy while the probe launches are queued, so that the
-    # events bracket kernels and not host enqueue gaps
-    torch.cuda._sleep(200_000_000)
-    with _native.LaunchProfile() as prof:
-        for _ in range(reps):
-            core.metric_flat(d, q, W, 0.0)
-    acc = {}
-    for lab, ms in prof.records:
-        a = acc.setdefault(lab, [0, 0.0])
-        a[0] += 1
-        a[1] += ms
+    X = torch.stack([lay.pack(ift.from_random(fl.domain, "normal")) for _ in range(3 * k)])
+    return core, W, shift, X
+
+
+def cg_iteration(lib, core, W, shift, bufs, k):
+    """One batched CG iteration as FusedCGBatch.body runs it inside the timed
+    loop: direction, batched matvec, curvature, update (+ their folds)."""
+    from nifty_amd import _native
+    X, R, D, Q, SC, ws = bufs
+    n = X.shape[1]
+    P = _native.ptr
+    s_ = _native.stream_ptr()
+    _native._check(lib.nft_cg_direction_batched(P(D), P(R), n, n, k, 0, P(SC), s_))
+    core.metric_flat_batch(D, Q, W, 0.0)
+    _native._check(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, 0, shift, P(SC), P(ws), s_))
+    _native._check(lib.nft_cg_update_batched(P(X), P(R), P(D), P(Q), 0, n, n, k, 0, shift, P(SC), P(ws), s_))
+
+
+def byte_model(cf, R, k, n_lat):
+    """Algorithmic bytes per launch (fp64, every operand array counted once per
+    launch; arrays shared by the k right-hand sides -- amplitude, xi0, pindex,
+    the LOS matrix and its scales -- once).  DESIGN.md §3."""
     n = cf.target.shape[0]
     N = n * n
     Hh = n * (n // 2 + 1)
@@ -138,35 +134,101 @@ def kernel_probe(ift, cf, R, lh, pos, reps=10):
     P = R._plan_np
     nnz = int(P["box_ent"][-1])
     nseg = int(P["nseg"])
-    model = {
-        "fft_r2c+pro": 3 * 8 * N + 4 * N + 8 * B + 16 * Hh,
-        "fft_r2c": 8 * N + 16 * Hh,
-        "fft_c2c": 2 * 16 * Hh,
-        "fft_unpack": 16 * Hh + 8 * N,
-        "fft_unpack+epi": 16 * Hh + 8 * N + 2 * 8 * N + 8 * N,
-        "los_fwd_items": 5 * nnz + 12 * nseg + 2 * 8 * N + 8 * nseg,
-        "los_fwd_reduce": 8 * nseg + 8 * R.target.shape[0],
-        "los_adj_boxes": 5 * nnz + 4 * nseg + 2 * 257 * int(P["nbox"]) + 2 * 8 * N,
-        "bin_scatter": 4 * N + 8 * N + 4 * B + 8 * B,
+    nbox = int(P["nbox"])
+    nlos = R.target.shape[0]
+    return {
+        # prologue A*x + xi0*dA[pindex]: x (k), A, xi0, pindex, dA (k); half spectrum out (k)
+        "fft_r2c+pro": 8 * k * N + 8 * N + 8 * N + 4 * N + 8 * k * B + 16 * k * Hh,
+        "fft_r2c": 8 * k * N + 16 * k * Hh,
+        "fft_c2c": 2 * 16 * k * Hh,
+        "fft_unpack": 16 * k * Hh + 8 * k * N,
+        # epilogue: out = A*v (k), out2 = xi0*v (k), reads A, xi0
+        "fft_unpack+epi": 16 * k * Hh + 16 * N + 16 * k * N,
+        # 5 B per nonzero, 12 B segment descriptors, x (k) and the column scale, partials (k)
+        "los_fwd_items": 5 * nnz + 12 * nseg + 8 * (k + 1) * N + 8 * k * nseg,
+        "los_fwd_reduce": 8 * k * nseg + 8 * k * nlos,
+        "los_adj_boxes": 5 * nnz + 4 * nseg + 2 * 257 * nbox + 8 * (k + 1) * N,
+        "bin_scatter": 4 * N + 8 * k * N + 4 * B + 8 * k * B,
+        "cg_dir_kernel": 3 * 8 * k * n_lat,
+        "curv_partial": 2 * 8 * k * n_lat,
+        "cg_update_kernel": 7 * 8 * k * n_lat,
     }
+
+
+def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
+    """Per-kernel durations of the batched CG iteration of the timed loop
+    (k right-hand sides = the local linear solves of one draw_samples call),
+    measured with HIP events recorded on the launch stream before every
+    hot-path launch (nft_prof_*; the same kernels with the same arguments as
+    inside the timed region, run eagerly because events cannot be timed inside
+    a HIP graph).
+
+    Returns ({label: {"launches": per iteration, "avg_us", "bytes": algorithmic
+    bytes per launch, "gbs"}}, iteration summary)."""
+    from nifty_amd import _native
+    lib = _native.load()
+    core, W, shift, XS = probe_setup(ift, lh, pos, k)
+    n_lat = XS.shape[1]
+    X, Rr, D = XS[:k].clone(), XS[k:2 * k].clone(), XS[2 * k:].clone()
+    Q = torch.zeros_like(X)
+    SC = torch.zeros((k, _native.CG_NSCALARS), dtype=torch.float64, device=X.device)
+    SC[:, _native.CG_GAMMA] = 1.0
+    SC[:, _native.CG_GPREV] = 1.0
+    ws = _native.workspace(k * lib.nft_reduce_workspace(n_lat), X.device, "cgb")
+    bufs = (X, Rr, D, Q, SC, ws)
+    for _ in range(3):
+        cg_iteration(lib, core, W, shift, bufs, k)
+    torch.cuda.synchronize()
+    # keep the GPU busy while the probe launches are queued, so that the
+    # events bracket kernels and not host enqueue gaps
+    torch.cuda._sleep(200_000_000)
+    with _native.LaunchProfile() as prof:
+        for _ in range(reps):
+            cg_iteration(lib, core, W, shift, bufs, k)
+    acc = {}
+    for lab, ms in prof.records:
+        a = acc.setdefault(lab, [0, 0.0])
+        a[0] += 1
+        a[1] += ms
+    model = byte_model(cf, R, k, n_lat)
     out = {}
+    tot_us, tot_b = 0.0, 0
     for lab, (cnt, tot) in acc.items():
         avg = tot / cnt * 1e3
         by = model.get(lab)
         out[lab] = {"launches": cnt // reps, "avg_us": round(avg, 2), "bytes": by,
                     "gbs": round(by / (avg * 1e-6) / 1e9, 1) if by else None}
-    return out
+        tot_us += tot * 1e3 / reps
+        tot_b += (by or 0) * (cnt // reps)
+    it = {"rhs": k, "us_per_iteration": round(tot_us, 1), "algorithmic_bytes": tot_b,
+          "gbs": round(tot_b / (tot_us * 1e-6) / 1e9, 1),
+          "frac": round(tot_b / (tot_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+    return out, it
+
+
+def load_pmc(label):
+    """Per-launch HBM traffic of `label` from the committed PMC summary
+    (tools/pmc_probe.py under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE,
+    calibrated as MI355X_MICROARCH.md §HBM prescribes), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = d.get("kernels", {}).get(label)
+    return None if e is None else e.get("traffic_bytes")
 
 
 def roofline_of(kp):
-    """roofline object for the kernel with the largest time per matvec"""
+    """roofline object for the kernel with the largest time per CG iteration"""
     lab = max(kp, key=lambda k: kp[k]["avg_us"] * kp[k]["launches"])
     k = kp[lab]
     if k["bytes"] is None:
         return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel": lab, "avg_launch_us": k["avg_us"]}
     return {"bound": "hbm", "achieved": k["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(k["gbs"] / HBM_PEAK_GBS, 4), "traffic": None, "kernel": lab,
+            "frac": round(k["gbs"] / HBM_PEAK_GBS, 4), "traffic": load_pmc(lab), "kernel": lab,
             "avg_launch_us": k["avg_us"], "algorithmic_bytes_per_launch": k["bytes"]}
 
 
@@ -235,7 +297,8 @@ def main():
     samples = 2 * nsamp * args.steps
     sps = samples / el
     cgps = iters / el
-    kp = kernel_probe(ift, cf, R, lh, pos) if torch.cuda.is_available() else None
+    kp, cgit = kernel_probe(ift, cf, R, lh, pos, args.samples_per_gpu) if torch.cuda.is_available() \
+        else (None, None)
     roof = roofline_of(kp) if kp else None
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
@@ -258,7 +321,7 @@ def main():
                                        f"(inner CG <= {args.newton_cg_max})",
                            "global_batch": samples // args.steps, "parallelism": f"sample-dp{ws}"},
                 "cg_iter_per_s": round(cgps, 3), "cg_iters": int(iters),
-                "roofline": roof, "cpu_baseline": cpu, "kernels": kp}
+                "roofline": roof, "cpu_baseline": cpu, "cg_iteration": cgit, "kernels": kp}
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist

@@ -1,0 +1,59 @@
+"""Short GPU program for the rocprofv3 PMC passes (HBM traffic of the CG
+iteration kernels, bench.py roofline `traffic`).
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 tools/pmc_probe.py
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 tools/pmc_probe.py
+    python tools/pmc_summary.py gpurun_out
+
+Runs (1) a calibration: nft_scale over a 1 GiB fp64 buffer (known bytes: 1 GiB
+read + 1 GiB written, 8 B per lane, larger than the 256 MiB Infinity Cache),
+then (2) `reps` batched CG iterations of the bench problem exactly as
+bench.kernel_probe runs them, writing the launch labels (in dispatch order) to
+gpurun_out/pmc_labels.json so the summary can name every dispatch."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main(reps=3, k=4):
+    import nifty_amd as ift
+    from nifty_amd import _native
+    ift.config.set_device("cuda:0")
+    lib = _native.load()
+    cf, R, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
+    ift.random.push_sseq_from_seed(5)
+    core, W, shift, XS = bench.probe_setup(ift, lh, pos, k)
+    n_lat = XS.shape[1]
+    X, Rr, D = XS[:k].clone(), XS[k:2 * k].clone(), XS[2 * k:].clone()
+    Q = torch.zeros_like(X)
+    SC = torch.zeros((k, _native.CG_NSCALARS), dtype=torch.float64, device=X.device)
+    SC[:, _native.CG_GAMMA] = 1.0
+    SC[:, _native.CG_GPREV] = 1.0
+    ws = _native.workspace(k * lib.nft_reduce_workspace(n_lat), X.device, "cgb")
+    bufs = (X, Rr, D, Q, SC, ws)
+    cal_n = 1 << 27
+    cal = torch.ones(cal_n, dtype=torch.float64, device=X.device)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        _native._check(lib.nft_scale(_native.ptr(cal), cal_n, 0, 1.0000001, _native.stream_ptr()))
+    torch.cuda.synchronize()
+    with _native.LaunchProfile(capacity=4096) as p:
+        for _ in range(reps):
+            bench.cg_iteration(lib, core, W, shift, bufs, k)
+    torch.cuda.synchronize()
+    model = bench.byte_model(cf, R, k, n_lat)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "pmc_labels.json"), "w") as f:
+        json.dump({"labels": [lab for lab, _ in p.records], "calibration_bytes": 8 * cal_n,
+                   "calibration_launches": 2, "rhs": k, "model": model}, f)
+    print("pmc probe done:", len(p.records), "labelled launches")
+
+
+if __name__ == "__main__":
+    main()
