@@ -173,6 +173,10 @@ typedef struct nft_hartley_fuse {
    * pro_index, epi_a, epi_b are shared by all items. */
   int64_t batch_period;
   int64_t x_bstride, c_bstride, out_bstride, d_bstride, out2_bstride;
+  /* element stride of pro_c (0: 1).  A batch may interleave its dA vectors
+   * (c_bstride = 1, c_estride = nitems): the bin gather of element j then
+   * reads one contiguous run pro_c[pindex[j] * nitems ...] for all items. */
+  int64_t c_estride;
 } nft_hartley_fuse;
 
 int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes,
@@ -263,12 +267,15 @@ int nft_amp_jvp(const nft_amp_const* c, const double* t_fl, const double* t_sl,
 int nft_amp_vjp(const nft_amp_const* c, const double* g, const nft_amp_out* out, double* ws,
                 hipStream_t stream);
 /* Batched: nrhs right-hand sides; tangent / cotangent pointers (and d) advance
- * by lat_stride elements per RHS, da / g by da_stride (g_stride); workspace
- * nrhs * nft_amp_workspace(B).  Per RHS identical to the single forms. */
+ * by lat_stride elements per RHS, da / g by da_stride (g_stride); bin b of
+ * RHS r is written to da[r * da_stride + b * da_elem_stride] (da_elem_stride
+ * 0: 1; da_stride 1 with da_elem_stride nrhs interleaves the RHS, see
+ * nft_hartley_fuse.c_estride); workspace nrhs * nft_amp_workspace(B).  Per
+ * RHS identical to the single forms. */
 int nft_amp_jvp_batched(const nft_amp_const* c, const double* t_fl, const double* t_sl,
                         const double* t_flex, const double* t_asp, const double* t_zm,
                         const double* t_spec, double* da, double* ws, int nrhs, int64_t lat_stride,
-                        int64_t da_stride, hipStream_t stream);
+                        int64_t da_stride, int64_t da_elem_stride, hipStream_t stream);
 int nft_amp_vjp_batched(const nft_amp_const* c, const double* g, const nft_amp_out* out,
                         double* ws, int nrhs, int64_t lat_stride, int64_t g_stride,
                         hipStream_t stream);

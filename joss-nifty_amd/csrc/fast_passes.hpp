@@ -16,7 +16,7 @@ enum Kind { K_C2C = 0, K_R2C = 1, K_H1D = 2, K_UNPACK = 3 };
 
 // Optional elementwise work fused into the first / last pass of a transform
 // (flat real indices of the input / output array):
-//   prologue  u[i] = (pa ? pa[j] : 1) * px[b*sx + j] + (pb ? pb[j] * pc[b*sc + pidx[j]] : 0)
+//   prologue  u[i] = (pa ? pa[j] : 1) * px[b*sx + j] + (pb ? pb[j] * pc[b*sc + pidx[j]*ce] : 0)
 //   epilogue  out[b*so + j] = (ea ? ea[j] : 1) * h + (ed ? eshift * ed[b*sd + j] : 0);
 //             out2[b*s2 + j] = eb[j] * h   (if out2)
 // For a batch of transforms (leading batch axis, P elements per item) b = i / P
@@ -31,7 +31,9 @@ struct FuseArgs {
   int pro, epi;
   long long P;
   int pshift;  // log2(P) if P is a power of two, else -1
+  int nb;      // number of batch items (P > 0)
   long long sx, sc, so, sd, s2;
+  long long ce;  // element stride of pc (>= 1)
 };
 
 __device__ __forceinline__ void fuse_split(const FuseArgs& f, long long i, long long& b, long long& j) {
@@ -53,7 +55,7 @@ __device__ __forceinline__ T fuse_pro(const FuseArgs& f, long long i) {
   fuse_split(f, i, b, j);
   T v = ((const T*)f.px)[b * f.sx + j];
   if (f.pa) v *= ((const T*)f.pa)[j];
-  if (f.pb) v += ((const T*)f.pb)[j] * ((const T*)f.pc)[b * f.sc + f.pidx[j]];
+  if (f.pb) v += ((const T*)f.pb)[j] * ((const T*)f.pc)[b * f.sc + f.pidx[j] * f.ce];
   return v;
 }
 
@@ -85,7 +87,23 @@ template <typename T> struct FastArgs {
   LineDesc desc;      // UNPACK: (o, i) -> real output line / mirror line
   FuseArgs f;         // R2C/H1D: prologue; UNPACK/H1D: epilogue
   long long ntiles;   // tiles of the pass (set by the launcher)
+  int bgroup;         // > 1: batch-aware XCD tile remap over this many items (set by the launcher)
 };
+
+// Batch-aware XCD remap.  Tiles are numbered batch-major (t = b * TR + r) and
+// the operands shared by the batch (amplitude, xi0, pindex) are indexed by r
+// only.  Workgroups are observed to be dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md §Workgroup dispatch), so workgroup w runs on XCD group
+// w % 8 at slot w / 8: giving the K items of one tile r consecutive slots of
+// one XCD group makes the K reads of r's shared operands hit that XCD's L2
+// instead of all going to HBM.  A bijection on [0, ntiles) when TR % 8 == 0
+// (the launcher checks); placement is a speed choice only.
+__device__ __forceinline__ long long batch_tile(long long w, long long ntiles, int K) {
+  const long long TR = ntiles / K;
+  const long long xg = w & 7, slot = w >> 3;
+  const long long rl = slot / K, b = slot - rl * K;
+  return b * TR + rl * 8 + xg;
+}
 
 // Persistent, prefetching tile loop: measured faster only for the plain
 // real-to-complex row pass (256-thread workgroups, N <= 2048).  Everywhere
@@ -198,6 +216,9 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   constexpr bool prefetch = PF;  // launched persistent only without a prologue
   C rv[VPT];
   long long t = blockIdx.x;
+  if constexpr (!PERSIST) {
+    if (a.bgroup > 1) t = batch_tile(t, ntiles, a.bgroup);
+  }
   if (prefetch && t < ntiles) load(t, rv);
   while (t < ntiles) {
     if (!prefetch) load(t, rv);

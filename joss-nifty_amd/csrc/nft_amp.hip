@@ -64,42 +64,44 @@ __device__ __forceinline__ double block_total(double v, double* sh) {
   return t;
 }
 
-// inclusive block scan of AE values per thread (thread-contiguous chunks);
-// REV scans from the end.  Returns the block total.
+// inclusive block scan of AE values per thread in STRIPED layout: v[k] is
+// element k*AT + threadIdx.x of the block (so every global access of a block
+// is a coalesced 2 KB run per k).  REV scans from the end.  Wave scans by
+// shuffles, then one fixed-order pass over the AE*AT/64 wave totals.
+// Returns the block total.
 template <bool REV>
 __device__ __forceinline__ double block_scan(double (&v)[AE], double* sh) {
-  // thread-local inclusive scan
-  if (REV) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int NW = AT / 64;
 #pragma unroll
-    for (int k = AE - 2; k >= 0; --k) v[k] += v[k + 1];
-  } else {
+  for (int k = 0; k < AE; ++k) {
+    double x = v[k];
 #pragma unroll
-    for (int k = 1; k < AE; ++k) v[k] += v[k - 1];
-  }
-  double mine = REV ? v[0] : v[AE - 1];
-  sh[threadIdx.x] = mine;
-  __syncthreads();
-  // Hillis-Steele over AT thread totals (in a second buffer half)
-  double* a = sh;
-  double* b = sh + AT;
-  for (int off = 1; off < AT; off <<= 1) {
-    double x = a[threadIdx.x];
-    if (!REV) {
-      if (threadIdx.x >= off) x += a[threadIdx.x - off];
-    } else {
-      if (threadIdx.x + off < AT) x += a[threadIdx.x + off];
+    for (int off = 1; off < 64; off <<= 1) {
+      const double y = REV ? __shfl_down(x, off, 64) : __shfl_up(x, off, 64);
+      if (REV ? (lane + off < 64) : (lane >= off)) x += y;
     }
-    b[threadIdx.x] = x;
-    __syncthreads();
-    double* t = a;
-    a = b;
-    b = t;
+    v[k] = x;
+    if (lane == (REV ? 0 : 63)) sh[k * NW + w] = x;
   }
-  const double incl = a[threadIdx.x];
-  const double total = REV ? a[0] : a[AT - 1];
-  const double excl = incl - mine;
+  __syncthreads();
+  double total = 0.0;
 #pragma unroll
-  for (int k = 0; k < AE; ++k) v[k] += excl;
+  for (int k = 0; k < AE; ++k) {
+    const int me = k * NW + w;
+    double off = 0.0;
+    if (!REV) {
+      for (int i = 0; i < me; ++i) off += sh[i];
+    } else {
+      for (int i = AE * NW - 1; i > me; --i) off += sh[i];
+    }
+    v[k] += off;
+  }
+  if (!REV) {
+    for (int i = 0; i < AE * NW; ++i) total += sh[i];
+  } else {
+    for (int i = AE * NW - 1; i >= 0; --i) total += sh[i];
+  }
   __syncthreads();
   return total;
 }
@@ -125,17 +127,17 @@ __global__ __launch_bounds__(AT) void amp_jvp_1(AmpConst c, const double* __rest
   tot1 += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
   const long long M = c.B - 2;
-  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x;
   double v[AE];
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
-    long long j = j0 + k;
+    long long j = j0 + (long long)k * AT;
     v[k] = j < M ? tspec[M + j] * c.sf[j] : 0.0;
   }
   double t = block_scan<false>(v, sh);
 #pragma unroll
   for (int k = 0; k < AE; ++k)
-    if (j0 + k < M) loc[j0 + k] = v[k];
+    if (j0 + (long long)k * AT < M) loc[j0 + (long long)k * AT] = v[k];
   if (threadIdx.x == 0) tot1[blockIdx.x] = t;
 }
 
@@ -151,11 +153,11 @@ __global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c, const double* __rest
   const long long M = c.B - 2;
   const int nb = (int)((M + ABLK - 1) / ABLK);
   const double carry = carry_in<false>(tot1, blockIdx.x, nb, sh);
-  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x;
   double v[AE];
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
-    long long j = j0 + k;
+    long long j = j0 + (long long)k * AT;
     if (j < M) {
       const double cj = loc[j] + carry;
       const double u1 = tspec[M + j] * c.sf[j];
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c, const double* __rest
   double t = block_scan<false>(v, sh);
 #pragma unroll
   for (int k = 0; k < AE; ++k)
-    if (j0 + k < M) loc[j0 + k] = v[k];
+    if (j0 + (long long)k * AT < M) loc[j0 + (long long)k * AT] = v[k];
   if (threadIdx.x == 0) tot2[blockIdx.x] = t;
 }
 
@@ -225,7 +227,8 @@ __global__ __launch_bounds__(AT) void amp_jvp_5(AmpConst c, const double* tfl, c
 // J7: da from dapre and dS = sum(part)
 __global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c, const double* tfl, const double* tzm,
                                                 const double* __restrict__ dapre, const double* __restrict__ part,
-                                                int npart, double* __restrict__ da, long long ls, long long vs, long long wsd) {
+                                                int npart, double* __restrict__ da, long long ls, long long vs, long long wsd,
+                                                long long des) {
   if (tfl) tfl += blockIdx.y * ls;
   if (tzm) tzm += blockIdx.y * ls;
   dapre += blockIdx.y * wsd;
@@ -245,7 +248,7 @@ __global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c, const double* tfl, c
       const double An = c.An[b];
       v = dfl * An + c.fl * An * (dapre[b] / 2. - dS / (2. * c.S));
     }
-    da[b] = v * c.total_volume;
+    da[b * des] = v * c.total_volume;
   }
 }
 
@@ -311,17 +314,17 @@ __global__ __launch_bounds__(AT) void amp_vjp_3(AmpConst c, const double* __rest
   for (int i = threadIdx.x; i < np; i += AT) s += part23[2 * i + 1];
   const double R3 = block_total(s, sh);
   const long long M = c.B - 2;
-  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x;
   double v[AE];
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
-    long long j = j0 + k;
+    long long j = j0 + (long long)k * AT;
     v[k] = j < M ? gtl_at(c, gapre, j, R3) : 0.0;
   }
   double t = block_scan<true>(v, sh);
 #pragma unroll
   for (int k = 0; k < AE; ++k)
-    if (j0 + k < M) loc[j0 + k] = v[k];
+    if (j0 + (long long)k * AT < M) loc[j0 + (long long)k * AT] = v[k];
   if (threadIdx.x == 0) tot[blockIdx.x] = t;
 }
 
@@ -343,11 +346,11 @@ __global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c, const double* __rest
   const long long M = c.B - 2;
   const int nb = (int)((M + ABLK - 1) / ABLK);
   const double carry = carry_in<true>(tot3, blockIdx.x, nb, sh);
-  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x;
   double v[AE];
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
-    long long j = j0 + k;
+    long long j = j0 + (long long)k * AT;
     if (j < M) {
       const double yj = y[j] = loc[j] + carry;
       const double zj = yj * c.lv[j] / 2.;
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c, const double* __rest
   double t = block_scan<true>(v, sh);
 #pragma unroll
   for (int k = 0; k < AE; ++k)
-    if (j0 + k < M) loc[j0 + k] = v[k];
+    if (j0 + (long long)k * AT < M) loc[j0 + (long long)k * AT] = v[k];
   if (threadIdx.x == 0) tot4[blockIdx.x] = t;
 }
 
@@ -380,11 +383,11 @@ __global__ __launch_bounds__(AT) void amp_vjp_5(AmpConst c, AmpOut o, const doub
   const long long M = c.B - 2;
   const int nb = (int)((M + ABLK - 1) / ABLK);
   const double carry = carry_in<true>(tot4, blockIdx.x, nb, sh);
-  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x * AE;
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x;
   double r4 = 0, r5 = 0;
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
-    long long j = j0 + k;
+    long long j = j0 + (long long)k * AT;
     if (j < M) {
       const double g0 = y[j];
       const double g1 = loc[j] + carry;
@@ -451,7 +454,7 @@ size_t nft_amp_workspace(int64_t B) { return (size_t)(3 * B + 16 * (B / 256 + 16
 
 int nft_amp_jvp_batched(const nft_amp_const* cst, const double* tfl, const double* tsl, const double* tflex,
                         const double* tasp, const double* tzm, const double* tspec, double* da, double* ws, int nrhs,
-                        int64_t lat_stride, int64_t da_stride, hipStream_t s) {
+                        int64_t lat_stride, int64_t da_stride, int64_t da_elem_stride, hipStream_t s) {
   const AmpConst& c = *cst;
   const long long B = c.B, M = B - 2;
   const long long wsd = (long long)(nft_amp_workspace(B) / sizeof(double));
@@ -475,14 +478,14 @@ int nft_amp_jvp_batched(const nft_amp_const* cst, const double* tfl, const doubl
                      vs, wsd);
   prof_mark(s, "amp_jvp_7");
   hipLaunchKernelGGL(amp_jvp_7, dim3(nblk(B, AT) < 1024 ? nblk(B, AT) : 1024, ny), dim3(AT), 0, s, c, tfl, tzm,
-                     dapre, part, nbB, da, ls, vs, wsd);
+                     dapre, part, nbB, da, ls, vs, wsd, (long long)(da_elem_stride > 0 ? da_elem_stride : 1));
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
 
 int nft_amp_jvp(const nft_amp_const* cst, const double* tfl, const double* tsl, const double* tflex,
                 const double* tasp, const double* tzm, const double* tspec, double* da, double* ws, hipStream_t s) {
-  return nft_amp_jvp_batched(cst, tfl, tsl, tflex, tasp, tzm, tspec, da, ws, 1, 0, 0, s);
+  return nft_amp_jvp_batched(cst, tfl, tsl, tflex, tasp, tzm, tspec, da, ws, 1, 0, 0, 1, s);
 }
 
 int nft_amp_vjp_batched(const nft_amp_const* cst, const double* g, const nft_amp_out* out, double* ws, int nrhs,

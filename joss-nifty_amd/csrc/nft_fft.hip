@@ -24,6 +24,8 @@
 
 #include "fast_dispatch.hpp"
 #include "fft_passes.hpp"
+#include <type_traits>
+
 #include "nft_api_internal.hpp"
 
 namespace nft {
@@ -635,6 +637,8 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
   }
 }
 
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
 // unfused fallback of nft_hartley_fused: prologue / epilogue as elementwise passes
 template <typename T>
 __global__ void fuse_pro_kernel(fast::FuseArgs f, T* __restrict__ dst, long long n) {
@@ -648,13 +652,79 @@ __global__ void fuse_epi_kernel(fast::FuseArgs f, const T* __restrict__ h, T* __
     fast::fuse_store<T>(f, out, i, h[i]);
 }
 
-static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+// Prologue of a batch of items sharing pa / pb / pidx (the CF Jacobian's
+// A_full, xi0 and bin index), as its own streaming pass: thread j reads the
+// shared operands of element j once and forms u[b][j] for every item b.
+// Inside the R2C row pass the same prologue is latency-bound (dependent bin
+// gathers at 4 workgroups per CU, shared operands re-read per item: 196 us
+// for 4 items at 2048^2 vs 67 us for the plain pass); split, the plain pass
+// runs persistent and prefetching.  Same arithmetic per element as
+// fast::fuse_pro (bitwise).
+template <typename T>
+__global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __restrict__ u, long long P,
+                                                        int nb) {
+  const T* px = (const T*)f.px;
+  const T* pa = (const T*)f.pa;
+  const T* pb = (const T*)f.pb;
+  const T* pc = (const T*)f.pc;
+  using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
+  // interleaved dA (ce == nb, sc == 1): each pixel's gather is one contiguous
+  // run; read it with 2-wide vector loads (half the divergent load
+  // instructions: the gather is bound by distinct lines per instruction)
+  const bool vec = pb && f.ce == nb && f.sc == 1 && (nb & 1) == 0;
+  for (long long j = (long long)blockIdx.x * 256 + threadIdx.x; j < P; j += (long long)gridDim.x * 256) {
+    const T a = pa ? pa[j] : (T)1;
+    const T bj = pb ? pb[j] : (T)0;
+    const int ix = pb ? f.pidx[j] : 0;
+    if (vec) {
+      const V2* q = (const V2*)(pc + (long long)ix * nb);
+#pragma unroll 2
+      for (int bp = 0; bp < nb / 2; ++bp) {
+        const V2 c2 = q[bp];
+        T v0 = px[(2 * bp) * f.sx + j], v1 = px[(2 * bp + 1) * f.sx + j];
+        if (pa) {
+          v0 *= a;
+          v1 *= a;
+        }
+        v0 += bj * c2.x;
+        v1 += bj * c2.y;
+        u[(2 * bp) * P + j] = v0;
+        u[(2 * bp + 1) * P + j] = v1;
+      }
+      continue;
+    }
+#pragma unroll 4
+    for (int b = 0; b < nb; ++b) {
+      T v = px[b * f.sx + j];
+      if (pa) v *= a;
+      if (pb) v += bj * pc[b * f.sc + ix * f.ce];
+      u[b * P + j] = v;
+    }
+  }
+}
 
 template <typename T>
 static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out, const Geo& g,
                               const std::vector<int>& ax, int sigma, double scale, void* ws, size_t ws_bytes,
                               size_t hws, hipStream_t s) {
   static const bool v1_only = getenv("NFT_ENGINE_V1") != nullptr;
+  static const bool no_split = getenv("NFT_NO_PRO_SPLIT") != nullptr;
+  const long long ntot = prod(g.shape, 0, g.nd);
+  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.P > 0 && f.nb > 1 && (long long)f.nb * f.P == ntot &&
+      ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
+    T* u = (T*)((char*)ws + align256(hws));
+    const unsigned nblk = (unsigned)std::min<long long>((f.P + 255) / 256, 8192);
+    prof_mark(s, "pro_batch");
+    hipLaunchKernelGGL(pro_batch_kernel<T>, dim3(nblk), dim3(256), 0, s, f, u, f.P, f.nb);
+    NFT_HIP_CHECK(hipGetLastError());
+    fast::FuseArgs f2 = f;
+    f2.pro = 0;
+    f2.px = f2.pa = f2.pb = f2.pc = nullptr;
+    f2.pidx = nullptr;
+    int st = hartley_v2<T>(u, out, g, ax, sigma, scale, ws, hws, s, &f2);
+    if (st != NFT_FALLBACK) return st;
+    return hartley_fused_impl<T>(f2, u, out, g, ax, sigma, scale, ws, ws_bytes, hws, s);
+  }
   if (!v1_only) {
     int st = hartley_v2<T>(in, out, g, ax, sigma, scale, ws, ws_bytes, s, &f);
     if (st != NFT_FALLBACK) return st;
@@ -799,6 +869,12 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     f.pro = f.px != nullptr;
     f.epi = (f.ea || f.ed || f.out2) ? 1 : 0;
     f.P = fz->batch_period;
+    f.nb = 0;
+    if (f.P > 0) {
+      long long tot = 1;
+      for (int d = 0; d < ndim; ++d) tot *= shape[d];
+      f.nb = (int)(tot / f.P);
+    }
     f.pshift = -1;
     if (f.P > 0 && (f.P & (f.P - 1)) == 0) {
       int sh = 0;
@@ -807,6 +883,7 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     }
     f.sx = fz->x_bstride ? fz->x_bstride : f.P;
     f.sc = fz->c_bstride;
+    f.ce = fz->c_estride > 0 ? fz->c_estride : 1;
     f.so = fz->out_bstride ? fz->out_bstride : f.P;
     f.sd = fz->d_bstride ? fz->d_bstride : f.P;
     f.s2 = fz->out2_bstride ? fz->out2_bstride : f.P;

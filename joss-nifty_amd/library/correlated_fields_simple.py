@@ -215,8 +215,9 @@ class _AmplitudeModel:
             return D[0, off[key]:].data_ptr()
         return at
 
-    def native_jvp_batched(self, const, D, off, da):
-        """da[b] = J_amp D[b] for the k rows of a packed batch D (k, size)."""
+    def native_jvp_batched(self, const, D, off, da, interleave=False):
+        """da[b] = J_amp D[b] for the k rows of a packed batch D (k, size);
+        interleave: da is (B, k), bin-major (one contiguous run per bin)."""
         import ctypes
         at = self._ptrs(D, off)
         k, size = D.shape
@@ -225,8 +226,8 @@ class _AmplitudeModel:
         P = ctypes.c_void_p
         _native._check(lib.nft_amp_jvp_batched(
             ctypes.byref(const), P(at(self.k_fl)), P(at(self.k_sl)), P(at(self.k_flex)), P(at(self.k_asp)),
-            P(at(self.k_zm)), P(at(self.k_spec)), P(da.data_ptr()), P(ws.data_ptr()), k, size, self.B,
-            _native.stream_ptr()))
+            P(at(self.k_zm)), P(at(self.k_spec)), P(da.data_ptr()), P(ws.data_ptr()), k, size,
+            1 if interleave else self.B, k if interleave else 1, _native.stream_ptr()))
         return da
 
     def native_vjp_batched(self, const, g, Q, off, D=None, shift=0.0):
@@ -416,12 +417,14 @@ class CFJacobian(LinearOperator):
         axes = tuple(range(1, 1 + len(grid)))
         conv = hartley_convention_code()
         const = self._const()
-        da = torch.empty((k, B), dtype=torch.float64, device=self.device)
-        amp.native_jvp_batched(const, D, off, da)
+        # dA interleaved bin-major: the prologue's bin gather reads one
+        # contiguous run per pixel for all k right-hand sides
+        da = torch.empty((B, k), dtype=torch.float64, device=self.device)
+        amp.native_jvp_batched(const, D, off, da, interleave=True)
         s = torch.empty((k,) + grid, dtype=self._afull.dtype, device=self.device)
         pro = dict(a=self._afull, x=D[0, xo:], b=self._xi0, c=da, index=m.bins.pindex)
         _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
-                              batch=dict(period=N, x=size, c=B))
+                              batch=dict(period=N, x=size, c=1, c_elem=k))
         g = W(s) if callable(W) else s * W
         g = g.contiguous()
         w = torch.empty((k,) + grid, dtype=self._afull.dtype, device=self.device)
