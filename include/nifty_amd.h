@@ -177,6 +177,9 @@ typedef struct nft_hartley_fuse {
    * (c_bstride = 1, c_estride = nitems): the bin gather of element j then
    * reads one contiguous run pro_c[pindex[j] * nitems ...] for all items. */
   int64_t c_estride;
+  /* per-item strides of pro_a, pro_b, epi_a, epi_b (0: shared by the batch,
+   * the default) -- a batch of different linearisation points */
+  int64_t a_bstride, b_bstride, ea_bstride, eb_bstride;
 } nft_hartley_fuse;
 
 int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes,
@@ -271,14 +274,17 @@ int nft_amp_vjp(const nft_amp_const* c, const double* g, const nft_amp_out* out,
  * RHS r is written to da[r * da_stride + b * da_elem_stride] (da_elem_stride
  * 0: 1; da_stride 1 with da_elem_stride nrhs interleaves the RHS, see
  * nft_hartley_fuse.c_estride); workspace nrhs * nft_amp_workspace(B).  Per
- * RHS identical to the single forms. */
-int nft_amp_jvp_batched(const nft_amp_const* c, const double* t_fl, const double* t_sl,
-                        const double* t_flex, const double* t_asp, const double* t_zm,
-                        const double* t_spec, double* da, double* ws, int nrhs, int64_t lat_stride,
-                        int64_t da_stride, int64_t da_elem_stride, hipStream_t stream);
-int nft_amp_vjp_batched(const nft_amp_const* c, const double* g, const nft_amp_out* out,
-                        double* ws, int nrhs, int64_t lat_stride, int64_t g_stride,
+ * RHS identical to the single forms.  item_consts: NULL (every RHS uses *c)
+ * or a DEVICE array of nrhs nft_amp_const, one linearisation point per RHS
+ * (same B and flags as *c; batched geoVI refinement of several samples). */
+int nft_amp_jvp_batched(const nft_amp_const* c, const nft_amp_const* item_consts, const double* t_fl,
+                        const double* t_sl, const double* t_flex, const double* t_asp,
+                        const double* t_zm, const double* t_spec, double* da, double* ws, int nrhs,
+                        int64_t lat_stride, int64_t da_stride, int64_t da_elem_stride,
                         hipStream_t stream);
+int nft_amp_vjp_batched(const nft_amp_const* c, const nft_amp_const* item_consts, const double* g,
+                        const nft_amp_out* out, double* ws, int nrhs, int64_t lat_stride,
+                        int64_t g_stride, hipStream_t stream);
 
 /* ---- launch profiler (HIP events) -------------------------------------- */
 /* Between nft_prof_begin and nft_prof_end every hot-path kernel launch

@@ -54,8 +54,8 @@ SIGNATURES = {
     "nft_amp_workspace": (_sz, [_i64]),
     "nft_amp_jvp": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "nft_amp_vjp": (_i, [_p, _p, _p, _p, _p]),
-    "nft_amp_jvp_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _p]),
-    "nft_amp_vjp_batched": (_i, [_p, _p, _p, _p, _i, _i64, _i64, _p]),
+    "nft_amp_jvp_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _p]),
+    "nft_amp_vjp_batched": (_i, [_p, _p, _p, _p, _p, _i, _i64, _i64, _p]),
 }
 
 
@@ -64,7 +64,8 @@ class HartleyFuse(ctypes.Structure):
     _fields_ = [(n, _p) for n in ("pro_a", "pro_x", "pro_b", "pro_c", "pro_index", "epi_a", "epi_d", "epi_b",
                                   "epi_out2")] + [("epi_shift", _d)] + \
                [(n, _i64) for n in ("batch_period", "x_bstride", "c_bstride", "out_bstride", "d_bstride",
-                                    "out2_bstride", "c_estride")]
+                                    "out2_bstride", "c_estride", "a_bstride", "b_bstride", "ea_bstride",
+                                    "eb_bstride")]
 
 
 class LosPlan(ctypes.Structure):
@@ -290,7 +291,8 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
     if batch:
         f.batch_period = int(batch["period"])
         for k, fld in (("x", "x_bstride"), ("c", "c_bstride"), ("out", "out_bstride"), ("d", "d_bstride"),
-                       ("out2", "out2_bstride"), ("c_elem", "c_estride")):
+                       ("out2", "out2_bstride"), ("c_elem", "c_estride"), ("a", "a_bstride"),
+                       ("b", "b_bstride"), ("ea", "ea_bstride"), ("eb", "eb_bstride")):
             setattr(f, fld, int(batch.get(k, 0)))
     tens = [out, x]
     if pro:

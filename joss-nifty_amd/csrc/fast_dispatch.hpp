@@ -63,7 +63,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   {
     // batch items sharing prologue / epilogue operands: keep one tile's items on one XCD
     const FuseArgs& f = a.f;
-    const bool shared = (f.pro && (f.pa || f.pb)) || (f.epi && (f.ea || f.eb));
+    const bool shared = (f.pro && ((f.pa && !f.sa) || (f.pb && !f.sb))) || (f.epi && ((f.ea && !f.sea) || (f.eb && !f.seb)));
     // measured slower at 2048^2 with 4 items (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us): opt-in
     static const bool on = getenv("NFT_BATCH_REMAP") != nullptr;
     if (on && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) b.bgroup = f.nb;

@@ -20,8 +20,9 @@ enum Kind { K_C2C = 0, K_R2C = 1, K_H1D = 2, K_UNPACK = 3 };
 //   epilogue  out[b*so + j] = (ea ? ea[j] : 1) * h + (ed ? eshift * ed[b*sd + j] : 0);
 //             out2[b*s2 + j] = eb[j] * h   (if out2)
 // For a batch of transforms (leading batch axis, P elements per item) b = i / P
-// and j = i mod P: pa, pb, pidx, ea, eb are shared by the batch, the other
-// operands advance by their own batch stride.  P = 0: one item (b = 0, j = i).
+// and j = i mod P: pidx is shared by the batch, pa, pb, ea, eb too unless
+// given a per-item stride, the other operands advance by their own batch
+// stride.  P = 0: one item (b = 0, j = i).
 struct FuseArgs {
   const void *pa, *px, *pb, *pc;
   const int* pidx;
@@ -34,6 +35,7 @@ struct FuseArgs {
   int nb;      // number of batch items (P > 0)
   long long sx, sc, so, sd, s2;
   long long ce;  // element stride of pc (>= 1)
+  long long sa, sb, sea, seb;  // per-item strides of pa, pb, ea, eb (0: shared)
 };
 
 __device__ __forceinline__ void fuse_split(const FuseArgs& f, long long i, long long& b, long long& j) {
@@ -54,8 +56,8 @@ __device__ __forceinline__ T fuse_pro(const FuseArgs& f, long long i) {
   long long b, j;
   fuse_split(f, i, b, j);
   T v = ((const T*)f.px)[b * f.sx + j];
-  if (f.pa) v *= ((const T*)f.pa)[j];
-  if (f.pb) v += ((const T*)f.pb)[j] * ((const T*)f.pc)[b * f.sc + f.pidx[j] * f.ce];
+  if (f.pa) v *= ((const T*)f.pa)[b * f.sa + j];
+  if (f.pb) v += ((const T*)f.pb)[b * f.sb + j] * ((const T*)f.pc)[b * f.sc + f.pidx[j] * f.ce];
   return v;
 }
 
@@ -67,10 +69,10 @@ __device__ __forceinline__ void fuse_store(const FuseArgs& f, T* out, long long 
   }
   long long b, j;
   fuse_split(f, i, b, j);
-  T r = f.ea ? ((const T*)f.ea)[j] * h : h;
+  T r = f.ea ? ((const T*)f.ea)[b * f.sea + j] * h : h;
   if (f.ed) r += (T)f.eshift * ((const T*)f.ed)[b * f.sd + j];
   out[b * f.so + j] = r;
-  if (f.out2) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[j] * h;
+  if (f.out2) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
 }
 
 template <typename T> struct FastArgs {

@@ -120,8 +120,9 @@ __device__ __forceinline__ double carry_in(const double* tot, int blk, int nb, d
 
 // ------------------------------------------------------------------ JVP
 // J1: cs1 = local scan of t1*sf over j < B-2
-__global__ __launch_bounds__(AT) void amp_jvp_1(AmpConst c, const double* __restrict__ tspec,
+__global__ __launch_bounds__(AT) void amp_jvp_1(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ tspec,
                                                 double* __restrict__ loc, double* __restrict__ tot1, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   if (tspec) tspec += blockIdx.y * ls;
   loc += blockIdx.y * wsd;
   tot1 += blockIdx.y * wsd;
@@ -142,9 +143,10 @@ __global__ __launch_bounds__(AT) void amp_jvp_1(AmpConst c, const double* __rest
 }
 
 // J3: c = loc + carry; t = (c + c_prev)/2*lv + t0*c0; local scan of t
-__global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c, const double* __restrict__ tspec,
+__global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ tspec,
                                                 const double* __restrict__ tot1, double* __restrict__ loc,
                                                 double* __restrict__ tot2, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   if (tspec) tspec += blockIdx.y * ls;
   tot1 += blockIdx.y * wsd;
   loc += blockIdx.y * wsd;
@@ -175,10 +177,11 @@ __global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c, const double* __rest
 }
 
 // J5: tl = [0,0, loc + carry]; dapre; partial sums of mspec*dapre
-__global__ __launch_bounds__(AT) void amp_jvp_5(AmpConst c, const double* tfl, const double* tsl,
+__global__ __launch_bounds__(AT) void amp_jvp_5(AmpConst c_, const AmpConst* __restrict__ dcs, const double* tfl, const double* tsl,
                                                 const double* tflex, const double* tasp,
                                                 const double* __restrict__ loc, const double* __restrict__ tot2,
                                                 double* __restrict__ dapre, double* __restrict__ part, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   if (tfl) tfl += blockIdx.y * ls;
   if (tsl) tsl += blockIdx.y * ls;
   if (tflex) tflex += blockIdx.y * ls;
@@ -225,10 +228,11 @@ __global__ __launch_bounds__(AT) void amp_jvp_5(AmpConst c, const double* tfl, c
 }
 
 // J7: da from dapre and dS = sum(part)
-__global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c, const double* tfl, const double* tzm,
+__global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c_, const AmpConst* __restrict__ dcs, const double* tfl, const double* tzm,
                                                 const double* __restrict__ dapre, const double* __restrict__ part,
                                                 int npart, double* __restrict__ da, long long ls, long long vs, long long wsd,
                                                 long long des) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   if (tfl) tfl += blockIdx.y * ls;
   if (tzm) tzm += blockIdx.y * ls;
   dapre += blockIdx.y * wsd;
@@ -254,7 +258,8 @@ __global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c, const double* tfl, c
 
 // ------------------------------------------------------------------ VJP
 // V1: partials of R1 = sum_{b>=1} TV*g_b*An_b
-__global__ __launch_bounds__(AT) void amp_vjp_1(AmpConst c, const double* __restrict__ g, double* __restrict__ part, long long ls, long long vs, long long wsd) {
+__global__ __launch_bounds__(AT) void amp_vjp_1(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ g, double* __restrict__ part, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   g += blockIdx.y * vs;
   part += blockIdx.y * wsd;
   __shared__ double sh[2 * AT];
@@ -266,9 +271,10 @@ __global__ __launch_bounds__(AT) void amp_vjp_1(AmpConst c, const double* __rest
 }
 
 // V2: gapre; partials R2 = sum vslope*gapre, R3 = sum gapre*sc
-__global__ __launch_bounds__(AT) void amp_vjp_2(AmpConst c, const double* __restrict__ g,
+__global__ __launch_bounds__(AT) void amp_vjp_2(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ g,
                                                 const double* __restrict__ part1, int np1,
                                                 double* __restrict__ gapre, double* __restrict__ part23, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   g += blockIdx.y * vs;
   part1 += blockIdx.y * wsd;
   gapre += blockIdx.y * wsd;
@@ -302,9 +308,10 @@ __device__ __forceinline__ double gtl_at(const AmpConst& c, const double* gapre,
 }
 
 // V3: reverse local scan of gtl[2:] -> y (local) ; totals
-__global__ __launch_bounds__(AT) void amp_vjp_3(AmpConst c, const double* __restrict__ gapre,
+__global__ __launch_bounds__(AT) void amp_vjp_3(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ gapre,
                                                 const double* __restrict__ part23, int np,
                                                 double* __restrict__ loc, double* __restrict__ tot, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   gapre += blockIdx.y * wsd;
   part23 += blockIdx.y * wsd;
   loc += blockIdx.y * wsd;
@@ -329,10 +336,11 @@ __global__ __launch_bounds__(AT) void amp_vjp_3(AmpConst c, const double* __rest
 }
 
 // V4: y = loc + suffix carry (g0); z = y*lv/2; w = z_j + z_{j+1}; reverse local scan of w
-__global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c, const double* __restrict__ gapre,
+__global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ gapre,
                                                 const double* __restrict__ part23, int np,
                                                 const double* __restrict__ tot3, double* __restrict__ y,
                                                 double* __restrict__ loc, double* __restrict__ tot4, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   gapre += blockIdx.y * wsd;
   part23 += blockIdx.y * wsd;
   tot3 += blockIdx.y * wsd;
@@ -371,9 +379,10 @@ __global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c, const double* __rest
 
 
 // V5: g1 = loc + carry; spectrum cotangents; partials R4, R5
-__global__ __launch_bounds__(AT) void amp_vjp_5(AmpConst c, AmpOut o, const double* __restrict__ y,
+__global__ __launch_bounds__(AT) void amp_vjp_5(AmpConst c_, const AmpConst* __restrict__ dcs, AmpOut o, const double* __restrict__ y,
                                                 const double* __restrict__ loc, const double* __restrict__ tot4,
                                                 double* __restrict__ part45, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   amp_out_offset(o, blockIdx.y * ls);
   y += blockIdx.y * wsd;
   loc += blockIdx.y * wsd;
@@ -411,10 +420,11 @@ __global__ __launch_bounds__(AT) void amp_vjp_5(AmpConst c, AmpOut o, const doub
 }
 
 // V6: scalar cotangents (one block)
-__global__ __launch_bounds__(AT) void amp_vjp_6(AmpConst c, AmpOut o, const double* __restrict__ g,
+__global__ __launch_bounds__(AT) void amp_vjp_6(AmpConst c_, const AmpConst* __restrict__ dcs, AmpOut o, const double* __restrict__ g,
                                                 const double* __restrict__ part1, int np1,
                                                 const double* __restrict__ part23, int np23,
                                                 const double* __restrict__ part45, int np45, long long ls, long long vs, long long wsd) {
+  const AmpConst c = dcs ? dcs[blockIdx.y] : c_;
   amp_out_offset(o, blockIdx.y * ls);
   g += blockIdx.y * vs;
   part1 += blockIdx.y * wsd;
@@ -452,9 +462,10 @@ extern "C" {
 
 size_t nft_amp_workspace(int64_t B) { return (size_t)(3 * B + 16 * (B / 256 + 16)) * sizeof(double); }
 
-int nft_amp_jvp_batched(const nft_amp_const* cst, const double* tfl, const double* tsl, const double* tflex,
-                        const double* tasp, const double* tzm, const double* tspec, double* da, double* ws, int nrhs,
-                        int64_t lat_stride, int64_t da_stride, int64_t da_elem_stride, hipStream_t s) {
+int nft_amp_jvp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, const double* tfl, const double* tsl,
+                        const double* tflex, const double* tasp, const double* tzm, const double* tspec, double* da,
+                        double* ws, int nrhs, int64_t lat_stride, int64_t da_stride, int64_t da_elem_stride,
+                        hipStream_t s) {
   const AmpConst& c = *cst;
   const long long B = c.B, M = B - 2;
   const long long wsd = (long long)(nft_amp_workspace(B) / sizeof(double));
@@ -469,15 +480,15 @@ int nft_amp_jvp_batched(const nft_amp_const* cst, const double* tfl, const doubl
   const unsigned ny = (unsigned)nrhs;
   if (c.has_flex) {
     prof_mark(s, "amp_jvp_1");
-    hipLaunchKernelGGL(amp_jvp_1, dim3(nbM, ny), dim3(AT), 0, s, c, tspec, loc, tot1, ls, vs, wsd);
+    hipLaunchKernelGGL(amp_jvp_1, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, tspec, loc, tot1, ls, vs, wsd);
     prof_mark(s, "amp_jvp_3");
-    hipLaunchKernelGGL(amp_jvp_3, dim3(nbM, ny), dim3(AT), 0, s, c, tspec, tot1, loc, tot2, ls, vs, wsd);
+    hipLaunchKernelGGL(amp_jvp_3, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, tspec, tot1, loc, tot2, ls, vs, wsd);
   }
   prof_mark(s, "amp_jvp_5");
-  hipLaunchKernelGGL(amp_jvp_5, dim3(nbB, ny), dim3(AT), 0, s, c, tfl, tsl, tflex, tasp, loc, tot2, dapre, part, ls,
+  hipLaunchKernelGGL(amp_jvp_5, dim3(nbB, ny), dim3(AT), 0, s, c, dcs, tfl, tsl, tflex, tasp, loc, tot2, dapre, part, ls,
                      vs, wsd);
   prof_mark(s, "amp_jvp_7");
-  hipLaunchKernelGGL(amp_jvp_7, dim3(nblk(B, AT) < 1024 ? nblk(B, AT) : 1024, ny), dim3(AT), 0, s, c, tfl, tzm,
+  hipLaunchKernelGGL(amp_jvp_7, dim3(nblk(B, AT) < 1024 ? nblk(B, AT) : 1024, ny), dim3(AT), 0, s, c, dcs, tfl, tzm,
                      dapre, part, nbB, da, ls, vs, wsd, (long long)(da_elem_stride > 0 ? da_elem_stride : 1));
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
@@ -485,11 +496,11 @@ int nft_amp_jvp_batched(const nft_amp_const* cst, const double* tfl, const doubl
 
 int nft_amp_jvp(const nft_amp_const* cst, const double* tfl, const double* tsl, const double* tflex,
                 const double* tasp, const double* tzm, const double* tspec, double* da, double* ws, hipStream_t s) {
-  return nft_amp_jvp_batched(cst, tfl, tsl, tflex, tasp, tzm, tspec, da, ws, 1, 0, 0, 1, s);
+  return nft_amp_jvp_batched(cst, nullptr, tfl, tsl, tflex, tasp, tzm, tspec, da, ws, 1, 0, 0, 1, s);
 }
 
-int nft_amp_vjp_batched(const nft_amp_const* cst, const double* g, const nft_amp_out* out, double* ws, int nrhs,
-                        int64_t lat_stride, int64_t g_stride, hipStream_t s) {
+int nft_amp_vjp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, const double* g, const nft_amp_out* out,
+                        double* ws, int nrhs, int64_t lat_stride, int64_t g_stride, hipStream_t s) {
   const AmpConst& c = *cst;
   const AmpOut& o = *out;
   const long long B = c.B, M = B - 2;
@@ -507,27 +518,27 @@ int nft_amp_vjp_batched(const nft_amp_const* cst, const double* g, const nft_amp
   double* part45 = tot4 + nbM + 1;
   const unsigned ny = (unsigned)nrhs;
   prof_mark(s, "amp_vjp_1");
-  hipLaunchKernelGGL(amp_vjp_1, dim3(nr, ny), dim3(AT), 0, s, c, g, part1, ls, vs, wsd);
+  hipLaunchKernelGGL(amp_vjp_1, dim3(nr, ny), dim3(AT), 0, s, c, dcs, g, part1, ls, vs, wsd);
   prof_mark(s, "amp_vjp_2");
-  hipLaunchKernelGGL(amp_vjp_2, dim3(nr, ny), dim3(AT), 0, s, c, g, part1, nr, gapre, part23, ls, vs, wsd);
+  hipLaunchKernelGGL(amp_vjp_2, dim3(nr, ny), dim3(AT), 0, s, c, dcs, g, part1, nr, gapre, part23, ls, vs, wsd);
   if (c.has_flex) {
     prof_mark(s, "amp_vjp_3");
-    hipLaunchKernelGGL(amp_vjp_3, dim3(nbM, ny), dim3(AT), 0, s, c, gapre, part23, nr, loc, tot3, ls, vs, wsd);
+    hipLaunchKernelGGL(amp_vjp_3, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, gapre, part23, nr, loc, tot3, ls, vs, wsd);
     prof_mark(s, "amp_vjp_4");
-    hipLaunchKernelGGL(amp_vjp_4, dim3(nbM, ny), dim3(AT), 0, s, c, gapre, part23, nr, tot3, y, loc, tot4, ls, vs,
+    hipLaunchKernelGGL(amp_vjp_4, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, gapre, part23, nr, tot3, y, loc, tot4, ls, vs,
                        wsd);
     prof_mark(s, "amp_vjp_5");
-    hipLaunchKernelGGL(amp_vjp_5, dim3(nbM, ny), dim3(AT), 0, s, c, o, y, loc, tot4, part45, ls, vs, wsd);
+    hipLaunchKernelGGL(amp_vjp_5, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, o, y, loc, tot4, part45, ls, vs, wsd);
   }
   prof_mark(s, "amp_vjp_6");
-  hipLaunchKernelGGL(amp_vjp_6, dim3(1, ny), dim3(AT), 0, s, c, o, g, part1, nr, part23, nr, part45,
+  hipLaunchKernelGGL(amp_vjp_6, dim3(1, ny), dim3(AT), 0, s, c, dcs, o, g, part1, nr, part23, nr, part45,
                      c.has_flex ? nbM : 0, ls, vs, wsd);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
 
 int nft_amp_vjp(const nft_amp_const* cst, const double* g, const nft_amp_out* out, double* ws, hipStream_t s) {
-  return nft_amp_vjp_batched(cst, g, out, ws, 1, 0, 0, s);
+  return nft_amp_vjp_batched(cst, nullptr, g, out, ws, 1, 0, 0, s);
 }
 
 }  // extern "C"

@@ -710,7 +710,8 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
   static const bool v1_only = getenv("NFT_ENGINE_V1") != nullptr;
   static const bool no_split = getenv("NFT_NO_PRO_SPLIT") != nullptr;
   const long long ntot = prod(g.shape, 0, g.nd);
-  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.P > 0 && f.nb > 1 && (long long)f.nb * f.P == ntot &&
+  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && f.nb > 1 &&
+      (long long)f.nb * f.P == ntot &&
       ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
     T* u = (T*)((char*)ws + align256(hws));
     const unsigned nblk = (unsigned)std::min<long long>((f.P + 255) / 256, 8192);
@@ -884,6 +885,11 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     f.sx = fz->x_bstride ? fz->x_bstride : f.P;
     f.sc = fz->c_bstride;
     f.ce = fz->c_estride > 0 ? fz->c_estride : 1;
+    f.sa = fz->a_bstride;
+    f.sb = fz->b_bstride;
+    f.sea = fz->ea_bstride;
+    f.seb = fz->eb_bstride;
+    if (f.P == 0) f.sa = f.sb = f.sea = f.seb = 0;
     f.so = fz->out_bstride ? fz->out_bstride : f.P;
     f.sd = fz->d_bstride ? fz->d_bstride : f.P;
     f.s2 = fz->out2_bstride ? fz->out2_bstride : f.P;

@@ -215,7 +215,7 @@ class _AmplitudeModel:
             return D[0, off[key]:].data_ptr()
         return at
 
-    def native_jvp_batched(self, const, D, off, da, interleave=False):
+    def native_jvp_batched(self, const, D, off, da, interleave=False, item_consts=None):
         """da[b] = J_amp D[b] for the k rows of a packed batch D (k, size);
         interleave: da is (B, k), bin-major (one contiguous run per bin)."""
         import ctypes
@@ -225,12 +225,12 @@ class _AmplitudeModel:
         ws = _native.workspace(k * lib.nft_amp_workspace(self.B), D.device, "amp")
         P = ctypes.c_void_p
         _native._check(lib.nft_amp_jvp_batched(
-            ctypes.byref(const), P(at(self.k_fl)), P(at(self.k_sl)), P(at(self.k_flex)), P(at(self.k_asp)),
+            ctypes.byref(const), P(item_consts), P(at(self.k_fl)), P(at(self.k_sl)), P(at(self.k_flex)), P(at(self.k_asp)),
             P(at(self.k_zm)), P(at(self.k_spec)), P(da.data_ptr()), P(ws.data_ptr()), k, size,
             1 if interleave else self.B, k if interleave else 1, _native.stream_ptr()))
         return da
 
-    def native_vjp_batched(self, const, g, Q, off, D=None, shift=0.0):
+    def native_vjp_batched(self, const, g, Q, off, D=None, shift=0.0, item_consts=None):
         """Q[b] amplitude keys = shift * D[b] + J_amp^T g[b]."""
         import ctypes
         k, size = Q.shape
@@ -244,7 +244,8 @@ class _AmplitudeModel:
             setattr(o, short, atq(key))
             setattr(o, "d" + short, atd(key))
         o.shift = float(shift)
-        _native._check(lib.nft_amp_vjp_batched(ctypes.byref(const), ctypes.c_void_p(g.data_ptr()), ctypes.byref(o),
+        _native._check(lib.nft_amp_vjp_batched(ctypes.byref(const), ctypes.c_void_p(item_consts),
+                                               ctypes.c_void_p(g.data_ptr()), ctypes.byref(o),
                                                ctypes.c_void_p(ws.data_ptr()), k, size, self.B,
                                                _native.stream_ptr()))
         return Q

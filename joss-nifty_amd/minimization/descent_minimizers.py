@@ -15,6 +15,24 @@ class DescentMinimizer(Minimizer):
         self.line_searcher = line_searcher
 
     def __call__(self, energy):
+        gen = self.minimize_gen(energy)
+        try:
+            req = next(gen)
+            while True:
+                req = gen.send(self.serve(req))
+        except StopIteration as e:
+            return e.value
+
+    def serve(self, req):
+        """Synchronous evaluation of one request of minimize_gen."""
+        if req[0] == "dir":
+            return self.get_descent_direction(req[1], req[2])
+        return self.line_searcher.serve(req)
+
+    def minimize_gen(self, energy):
+        """DescentMinimizer.__call__ (descent_minimizers.py:52-108) as a
+        generator of requests: ("dir", energy, f_k_minus_1) -> descent
+        direction, plus the line search's ("dd", ...) / ("at", ...)."""
         f_k_minus_1 = None
         controller = self._controller
         status = controller.start(energy)
@@ -23,8 +41,9 @@ class DescentMinimizer(Minimizer):
         while True:
             if energy.gradient_norm == 0:
                 return energy, controller.CONVERGED
-            new_energy, success = self.line_searcher.perform_line_search(
-                energy=energy, pk=self.get_descent_direction(energy, f_k_minus_1), f_k_minus_1=f_k_minus_1)
+            pk = yield ("dir", energy, f_k_minus_1)
+            new_energy, success = yield from self.line_searcher.perform_line_search_gen(
+                energy=energy, pk=pk, f_k_minus_1=f_k_minus_1)
             if not success:
                 self.reset()
             f_k_minus_1 = energy.value

@@ -295,16 +295,6 @@ class FusedCGBatch(FusedCG):
         k = len(energies)
         lay, core = self.layout, self.core
         n = lay.size
-        results = [None] * k
-        active = []
-        for j, (e, ctl) in enumerate(zip(energies, self.controllers)):
-            st = ctl.start(e)
-            if st != ctl.CONTINUE:
-                results[j] = (e, st)
-            else:
-                active.append(j)
-        if not active:
-            return results
         dev = core.device
         X = torch.zeros((k, n), dtype=torch.float64, device=dev)
         Rr = torch.zeros_like(X)
@@ -314,6 +304,38 @@ class FusedCGBatch(FusedCG):
             lay.pack(e.gradient, out=Rr[j])
             if Bv is not None:
                 lay.pack(e._b, out=Bv[j])
+        A = energies[0].metric
+        X, status = self.run_packed(X, Rr, Bv, energies)
+        from .quadratic_energy import QuadraticEnergy
+        results = []
+        for j, e in enumerate(energies):
+            st, moved = status[j]
+            if moved is None:
+                results.append((e, st))
+            else:
+                results.append((QuadraticEnergy(lay.unpack(X[j]), A, e._b, _grad=lay.unpack(Rr[j])), st))
+        return results
+
+    def run_packed(self, X, Rr, Bv, starts):
+        """The batched loop on packed (k, n) buffers: X (iterates) and Rr
+        (gradients A x - b) are updated in place, Bv is b (or None).
+        `starts`: per RHS an energy-like object (value, gradient_norm) for the
+        controller's start().  Returns (X, [(status, moved)]) -- moved is None
+        for a RHS returned in its initial state."""
+        k = X.shape[0]
+        lay, core = self.layout, self.core
+        n = lay.size
+        results = [None] * k
+        active = []
+        for j, (e, ctl) in enumerate(zip(starts, self.controllers)):
+            st = ctl.start(e)
+            if st != ctl.CONTINUE:
+                results[j] = (st, None)
+            else:
+                active.append(j)
+        if not active:
+            return X, results
+        dev = core.device
         D = Rr.clone()
         Q = torch.zeros_like(X)
         AX = None
@@ -325,17 +347,12 @@ class FusedCGBatch(FusedCG):
         dt = _native.dtype_code(X.dtype)
         P = _native.ptr
         sh = self.shift
-        A = energies[0].metric
 
         def chk(st):
             _native._check(st)
 
-        def energy_of(j):
-            from .quadratic_energy import QuadraticEnergy
-            return QuadraticEnergy(lay.unpack(X[j]), A, energies[j]._b, _grad=lay.unpack(Rr[j]))
-
         def finish(j, status):
-            results[j] = (energy_of(j), status)
+            results[j] = (status, True)
             SC[j, _native.CG_DONE] = 1.0
 
         for j in range(k):
@@ -348,14 +365,14 @@ class FusedCGBatch(FusedCG):
             g = float(host[j, _native.CG_GAMMA])
             if np.isnan(g):
                 logger.error("Error: ConjugateGradient: previous_gamma==NaN")
-                results[j] = (energies[j], self.controllers[j].ERROR)
+                results[j] = (self.controllers[j].ERROR, None)
             elif g == 0:
-                results[j] = (energies[j], self.controllers[j].CONVERGED)
+                results[j] = (self.controllers[j].CONVERGED, None)
             if results[j] is not None:
                 SC[j, _native.CG_DONE] = 1.0
                 active.remove(j)
         if not active:
-            return results
+            return X, results
 
         def body(with_dir):
             s_ = _native.stream_ptr()
@@ -442,4 +459,4 @@ class FusedCGBatch(FusedCG):
                 if status is not None:
                     finish(j, status)
                     active.remove(j)
-        return results
+        return X, results

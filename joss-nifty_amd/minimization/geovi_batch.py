@@ -1,0 +1,517 @@
+"""Lock-step geoVI refinement of the local samples (batched NewtonCG).
+
+The reference refines every sample of draw_samples on its own
+(src/minimization/kl_energies.py:147-155):
+
+    en = EnergyAdapter(pos_i, GaussianEnergy(m_i) @ transformation,
+                       nanisinf=True, want_metric=True)
+    en, _ = minimizer(en)                 # NewtonCG + LineSearch
+
+with transformation = 1 + J0^T f_lh, J0 the Jacobian of the likelihood's
+whitening map f_lh at the expansion point.  Here the k local samples run the
+SAME minimizer code -- one DescentMinimizer.minimize_gen generator per sample
+(descent_minimizers.py / line_search.py: its own controllers, every decision
+on its own host floats) -- and their requests are served in batches:
+
+  ("at", e, alpha, pk)  value, gradient, |gradient| at e.x + alpha * pk
+  ("dd", e, pk)         directional derivative  e.gradient . pk
+  ("dir", e, f_prev)    NewtonCG direction: CG on the sample's metric
+
+Energy of a batch X (k, latent) of positions, everything on the device:
+
+  F  = f_lh(X)                 batched pipeline: CF model, pointwise maps,
+                               LOSResponse / GeometryRemover, scalings
+  T  = X + J0^T F              J0 shared by the batch (expansion point)
+  R  = T - M;  value_i = R_i . R_i / 2
+  G  = R + J_f(X)^T (J0 R)     per-sample Jacobians: the batched kernels with
+                               per-item constants (nft_amp_*_batched
+                               item_consts, nft_hartley_fuse a/b strides)
+
+Newton metric of sample i (GaussianEnergy's metric is 1, so J_T^T J_T):
+
+  M_i v = u + J_i^T J0 u,   u = v + J0^T J_i v
+
+and the descent directions of all requesting samples come from one
+FusedCGBatch loop whose matvec applies every sample's own M_i.
+
+Supported f_lh: chains (outermost first) of ScalingOperator, DiagonalOperator,
+GeometryRemover, LOSResponse and pointwise functions (ptw_dict) ending in a
+SimpleCorrelatedField model; anything else returns None from ``plan`` and
+draw_samples keeps the per-sample path."""
+import copy
+import math
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..logger import logger
+from .energy import Energy
+
+NS = _native.CG_NSCALARS
+ENABLED = True   # tests compare against the per-sample path with ENABLED = False
+
+
+# ------------------------------------------------------------------ stages
+class _CFStage:
+    """The fused correlated-field model (library/correlated_fields_simple.py)
+    evaluated on a batch of packed latent rows."""
+
+    def __init__(self, model):
+        self.m = model
+        self.lay = model.layout
+        self.off = dict(zip(self.lay.keys, self.lay.offsets))
+        self.grid = tuple(model.harmonic_partner.shape)
+        self.N = int(np.prod(self.grid))
+        self.axes = tuple(range(1, 1 + len(self.grid)))
+        self.xo = self.off[model.k_xi]
+
+    def _xi(self, X):
+        return X[:, self.xo:self.xo + self.N].reshape((X.shape[0],) + self.grid)
+
+    def fwd(self, X):
+        m, lay = self.m, self.lay
+        k = X.shape[0]
+        amp = m.amp
+        a_list, consts, keeps = [], [], []
+        for i in range(k):
+            v = lay.views(X[i])
+            a, c = amp.forward({kk: v[kk] for kk in amp.domain_dict})
+            const, keep = amp.native_const(c)
+            a_list.append(a)
+            consts.append(const)
+            keeps.append(keep)
+        A = torch.stack(a_list)
+        afull = torch.empty((k,) + self.grid, dtype=A.dtype, device=A.device)
+        b = m.bins
+        _native.bin_gather(A, b.pindex, afull, k, b.npix, b.nbin, 1)
+        u = afull * self._xi(X)
+        s = torch.empty_like(u)
+        from ..ducc_dispatch import hartley_convention_code
+        _native.hartley_fused(s, self.axes, m.c_h, x=u, convention=hartley_convention_code(), shape=s.shape)
+        if m.offset_mean is not None:
+            s = s + m.offset_mean
+        raw = b"".join(bytes(c) for c in consts)
+        dconst = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(X.device)
+        return s, dict(afull=afull, X=X, consts=consts, keeps=keeps, dconst=dconst, k=k)
+
+    @staticmethod
+    def stack(states):
+        """one batch state from per-sample (state, row) pairs"""
+        if len(states) == 1 and states[0][0]["k"] == 1:
+            return states[0][0]
+        afull = torch.stack([st["afull"][r] for st, r in states])
+        X = torch.stack([st["X"][r] for st, r in states])
+        consts = [st["consts"][r] for st, r in states]
+        keeps = [st["keeps"][r] for st, r in states]
+        raw = b"".join(bytes(c) for c in consts)
+        dconst = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(X.device)
+        return dict(afull=afull, X=X, consts=consts, keeps=keeps, dconst=dconst, k=len(states))
+
+    def jvp(self, st, V):
+        """(k, grid) = J_cf(x_b) V[b]; st shared (k = 1) or per item"""
+        from ..ducc_dispatch import hartley_convention_code
+        m = self.m
+        k, size = V.shape
+        B = m.amp.B
+        N = self.N
+        shared = st["k"] == 1
+        out = torch.empty((k,) + self.grid, dtype=V.dtype, device=V.device)
+        Xs = st["X"]
+        if shared:
+            da = torch.empty((B, k), dtype=torch.float64, device=V.device)
+            m.amp.native_jvp_batched(st["consts"][0], V, self.off, da, interleave=True)
+            batch = dict(period=N, x=size, c=1, c_elem=k)
+        else:
+            da = torch.empty((k, B), dtype=torch.float64, device=V.device)
+            m.amp.native_jvp_batched(st["consts"][0], V, self.off, da, item_consts=st["dconst"].data_ptr())
+            batch = dict(period=N, x=size, c=B, a=N, b=Xs.shape[1])
+        pro = dict(a=st["afull"], x=V[0, self.xo:], b=Xs[0, self.xo:], c=da, index=m.bins.pindex)
+        _native.hartley_fused(out, self.axes, m.c_h, pro=pro, convention=hartley_convention_code(),
+                              shape=out.shape, batch=batch)
+        return out
+
+    def vjp(self, st, G, Q):
+        """Q[b] (packed rows, padding zero) = J_cf(x_b)^T G[b]"""
+        from ..ducc_dispatch import hartley_convention_code
+        m = self.m
+        k = G.shape[0]
+        size = Q.shape[1]
+        N = self.N
+        shared = st["k"] == 1
+        Xs = st["X"]
+        w = torch.empty((k,) + self.grid, dtype=G.dtype, device=G.device)
+        epi = dict(a=st["afull"], b=Xs[0, self.xo:], out2=w)
+        batch = dict(period=N, out=size, out2=N)
+        if not shared:
+            batch.update(ea=N, eb=Xs.shape[1])
+        _native.hartley_fused(Q[0, self.xo:], self.axes, m.c_h, x=G.contiguous(), epi=epi,
+                              convention=hartley_convention_code(), shape=(k,) + self.grid, batch=batch)
+        ga = torch.empty((k, m.amp.B), dtype=G.dtype, device=G.device)
+        b = m.bins
+        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1)
+        m.amp.native_vjp_batched(st["consts"][0], ga, Q, self.off,
+                                 item_consts=None if shared else st["dconst"].data_ptr())
+        return Q
+
+
+class _PtwStage:
+    def __init__(self, name, args, kwargs):
+        from ..pointwise import ptw_dict
+        self.f = ptw_dict[name][1]
+        self.args, self.kwargs = args, kwargs
+
+    def fwd(self, U):
+        v, d = self.f(U, *self.args, **self.kwargs)
+        return v, d
+
+    @staticmethod
+    def stack(states):
+        if len(states) == 1 and states[0][0].shape[0] == 1:
+            return states[0][0]
+        return torch.stack([st[r] for st, r in states])
+
+    def jvp(self, d, V):
+        return V * d
+
+    def vjp(self, d, G):
+        return G * d
+
+
+class _LinStage:
+    """linear stage without state: ('scale', s) | ('diag', t) | ('reshape',) | ('los', R)"""
+
+    def __init__(self, kind, v, dom_shape, tgt_shape):
+        self.kind, self.v = kind, v
+        self.dshape, self.tshape = tuple(dom_shape), tuple(tgt_shape)
+
+    def fwd(self, U):
+        return self.jvp(None, U), None
+
+    @staticmethod
+    def stack(states):
+        return None
+
+    def jvp(self, _, V):
+        k = V.shape[0]
+        if self.kind == "scale":
+            return (V * self.v).reshape((k,) + self.tshape)
+        if self.kind == "diag":
+            return (V.reshape((k,) + self.dshape) * self.v).reshape((k,) + self.tshape)
+        if self.kind == "reshape":
+            return V.reshape((k,) + self.tshape)
+        return _los_fwd(self.v, V.reshape(k, -1))
+
+    def vjp(self, _, G):
+        k = G.shape[0]
+        if self.kind == "scale":
+            return (G * self.v).reshape((k,) + self.dshape)
+        if self.kind == "diag":
+            return (G.reshape((k,) + self.tshape) * self.v).reshape((k,) + self.dshape)
+        if self.kind == "reshape":
+            return G.reshape((k,) + self.dshape)
+        return _los_adj(self.v, G.reshape(k, -1)).reshape((k,) + self.dshape)
+
+
+def _los_fwd(R, V):
+    from ..library.los_response import LOS_KMAX
+    plan = R._box_plan()
+    k = V.shape[0]
+    V = V.contiguous()
+    y = torch.empty((k, R.target.shape[0]), dtype=V.dtype, device=V.device)
+    for a in range(0, k, LOS_KMAX):
+        b = min(k, a + LOS_KMAX)
+        _native.los_forward_batched(plan, V[a:b], y[a:b])
+    return y
+
+
+def _los_adj(R, Y):
+    from ..library.los_response import LOS_KMAX
+    plan = R._box_plan()
+    k = Y.shape[0]
+    Y = Y.contiguous()
+    npix = int(np.prod(R.domain.shape))
+    out = torch.empty((k, npix), dtype=Y.dtype, device=Y.device)
+    for a in range(0, k, LOS_KMAX):
+        b = min(k, a + LOS_KMAX)
+        _native.los_adjoint_batched(plan, Y[a:b], out[a:b])
+    return out
+
+
+class Pipeline:
+    """f_lh on batches of packed latent rows; stages innermost first."""
+
+    def __init__(self, stages, layout):
+        self.stages = stages
+        self.layout = layout
+
+    @classmethod
+    def parse(cls, f_lh):
+        from ..library.correlated_fields_simple import _CorrelatedFieldModel
+        from ..library.los_response import LOSResponse
+        from ..operators.diagonal_operator import DiagonalOperator
+        from ..operators.operator import _FunctionApplier, _OpChain
+        from ..operators.scaling_operator import ScalingOperator
+        from ..operators.simple_linear_operators import GeometryRemover
+        from ..pointwise import ptw_dict
+        ops = list(f_lh._ops) if isinstance(f_lh, _OpChain) else [f_lh]
+        if not ops or not isinstance(ops[-1], _CorrelatedFieldModel):
+            return None
+        stages = [_CFStage(ops[-1])]
+        for op in reversed(ops[:-1]):
+            if isinstance(op, ScalingOperator) and np.isreal(op._factor):
+                f = float(np.real(op._factor))
+                stages.append(_LinStage("scale", f, op.domain.shape, op.target.shape))
+            elif isinstance(op, DiagonalOperator) and not op._complex:
+                stages.append(_LinStage("diag", op.diagonal_tensor, op.domain.shape, op.target.shape))
+            elif isinstance(op, GeometryRemover):
+                stages.append(_LinStage("reshape", None, op.domain.shape, op.target.shape))
+            elif isinstance(op, LOSResponse):
+                stages.append(_LinStage("los", op, op.domain.shape, op.target.shape))
+            elif isinstance(op, _FunctionApplier) and op._funcname in ptw_dict:
+                stages.append(_PtwStage(op._funcname, op._args, op._kwargs))
+            else:
+                return None
+        return cls(stages, ops[-1].layout)
+
+    def fwd(self, X):
+        states = []
+        U = X
+        for s in self.stages:
+            U, st = s.fwd(U)
+            states.append(st)
+        return U, states
+
+    def stack(self, rows):
+        """batch state from [(states, row), ...]"""
+        return [type(s).stack([(st[j], r) for st, r in rows]) for j, s in enumerate(self.stages)]
+
+    def jvp(self, states, V):
+        U = self.stages[0].jvp(states[0], V)
+        for s, st in zip(self.stages[1:], states[1:]):
+            U = s.jvp(st, U)
+        return U
+
+    def vjp(self, states, G, Q):
+        """Q (k, size) zero-padded packed rows = J^T G"""
+        U = G
+        for s, st in zip(reversed(self.stages[1:]), reversed(states[1:])):
+            U = s.vjp(st, U)
+        return self.stages[0].vjp(states[0], U, Q)
+
+
+# ------------------------------------------------------------------ energies
+class _BEnergy(Energy):
+    """Energy of one sample at a packed position (value / gradient on the
+    device, value and |gradient| already on the host)."""
+
+    def __init__(self, ctx, x, g, value, gnorm, states, row):
+        super().__init__(None)
+        self.ctx, self.x, self.g = ctx, x, g
+        self._val, self._gradnorm = value, gnorm
+        self.states, self.row = states, row
+
+    @property
+    def position(self):
+        return self.ctx.layout.unpack(self.x)
+
+    @property
+    def value(self):
+        return self._val
+
+    @property
+    def gradient(self):
+        return self.ctx.layout.unpack(self.g)
+
+    @property
+    def gradient_norm(self):
+        return self._gradnorm
+
+    def at(self, position):
+        raise NotImplementedError("batched geoVI energies are evaluated by their driver")
+
+
+class _Dir:
+    """packed descent direction (what the line search's pk is here)"""
+
+    def __init__(self, v):
+        self.v = v
+
+    def norm(self):
+        return float(torch.linalg.vector_norm(self.v))
+
+
+class GeoVIBatch:
+    """Batched refinement of k samples around one expansion point."""
+
+    def __init__(self, pipe, x0, minimizer):
+        self.pipe = pipe
+        self.layout = pipe.layout
+        self.minimizer = minimizer
+        X0 = x0.reshape(1, -1)
+        F0, st0 = pipe.fwd(X0)
+        self.st0 = st0                   # J0: shared by every sample
+        self.x0 = X0
+        # transformation_mean = x0 + J0^T f(x0)  (kl_energies.py:118)
+        self.tmean = (X0 + self._J0T(F0))[0]
+
+    # J0 / J0^T (shared) and J / J^T (per item) on packed rows
+    def _J0(self, V):
+        return self.pipe.jvp(self.st0, V)
+
+    def _J0T(self, F):
+        Q = torch.zeros((F.shape[0], self.layout.size), dtype=torch.float64, device=F.device)
+        return self.pipe.vjp(self.st0, F, Q)
+
+    def _JT(self, states, G):
+        Q = torch.zeros((G.shape[0], self.layout.size), dtype=torch.float64, device=G.device)
+        return self.pipe.vjp(states, G, Q)
+
+    def evaluate(self, X, M):
+        """values, |gradient|, gradients and per-sample states at the rows of X"""
+        F, states = self.pipe.fwd(X)
+        Rr = X + self._J0T(F) - M
+        G = Rr + self._JT(states, self._J0(Rr))
+        k = X.shape[0]
+        sc = torch.stack([(Rr * Rr).sum(1), (G * G).sum(1)], 1)
+        h = sc.cpu().numpy()
+        vals = [0.5 * float(h[i, 0]) for i in range(k)]
+        gn = [math.sqrt(float(h[i, 1])) for i in range(k)]
+        return vals, gn, G, states
+
+    def metric_batch(self, states):
+        """callable (D, Q) -> Q = M_b D for the stacked per-sample states"""
+        def mv(D, Q):
+            U = D + self._J0T(self.pipe.jvp(states, D))
+            Q.copy_(U + self._JT(states, self._J0(U)))
+            return Q
+        return mv
+
+    def refine(self, starts, means):
+        """starts, means: lists of packed latent vectors.  Returns the final
+        packed positions (one per sample)."""
+        k = len(starts)
+        X = torch.stack(starts)
+        M = torch.stack(means)
+        self._M = {i: M[i] for i in range(k)}
+        vals, gn, G, states = self.evaluate(X, M)
+        gens, pending, results = [], {}, [None] * k
+        for i in range(k):
+            v = vals[i]
+            if np.isnan(v):   # EnergyAdapter(nanisinf=True)
+                v = np.inf
+            e = _BEnergy(self, X[i], G[i], v, gn[i], states, i)
+            e.sample = i
+            # one minimizer per sample: controllers are stateful (the reference
+            # reuses one minimizer sample after sample, start() resetting it)
+            mz = copy.copy(self.minimizer)
+            mz._controller = copy.deepcopy(self.minimizer._controller)
+            gen = mz.minimize_gen(e)
+            gens.append(gen)
+            self._advance(i, gen, None, pending, results, first=True)
+        while pending:
+            kinds = {}
+            for i, req in pending.items():
+                kinds.setdefault(req[0], []).append(i)
+            answers = {}
+            if "dir" in kinds:
+                answers.update(self._serve_dir([(i, pending[i]) for i in kinds["dir"]]))
+            if "at" in kinds:
+                answers.update(self._serve_at([(i, pending[i]) for i in kinds["at"]]))
+            if "dd" in kinds:
+                answers.update(self._serve_dd([(i, pending[i]) for i in kinds["dd"]]))
+            for i, ans in answers.items():
+                self._advance(i, gens[i], ans, pending, results)
+        return [r[0].x for r in results]
+
+    @staticmethod
+    def _advance(i, gen, ans, pending, results, first=False):
+        try:
+            pending[i] = next(gen) if first else gen.send(ans)
+        except StopIteration as e:
+            pending.pop(i, None)
+            results[i] = e.value
+
+    def _serve_at(self, reqs):
+        X = torch.stack([r[1].x + r[2] * r[3].v for _, r in reqs])
+        M = torch.stack([self._M[r[1].sample] for _, r in reqs])
+        vals, gn, G, states = self.evaluate(X, M)
+        out = {}
+        for j, (i, r) in enumerate(reqs):
+            v = vals[j]
+            if np.isnan(v):
+                v = np.inf
+            e = _BEnergy(self, X[j], G[j], v, gn[j], states, j)
+            e.sample = r[1].sample
+            out[i] = e
+        return out
+
+    def _serve_dd(self, reqs):
+        G = torch.stack([r[1].g for _, r in reqs])
+        P = torch.stack([r[2].v for _, r in reqs])
+        h = (G * P).sum(1).cpu().numpy()
+        return {i: float(h[j]) for j, (i, _) in enumerate(reqs)}
+
+    def _serve_dir(self, reqs):
+        from .conjugate_gradient import ConjugateGradient  # noqa: F401
+        from .fused_cg import FusedCGBatch, _State
+        from .iteration_controllers import AbsDeltaEnergyController, GradientNormController
+        mz = self.minimizer
+        ctls = []
+        for _, (_, e, old) in reqs:
+            if old is None:
+                ctls.append(GradientNormController(iteration_limit=5))
+            else:
+                ediff = mz._alpha * (old - e.value)
+                ctls.append(AbsDeltaEnergyController(ediff, iteration_limit=mz._max_cg_iterations, name=mz._name))
+        states = self.pipe.stack([(r[1].states, r[1].row) for _, r in reqs])
+        G = torch.stack([r[1].g for _, r in reqs])
+        core = _MetricCore(self.metric_batch(states), self.layout)
+        cg = FusedCGBatch(core, None, 0.0, ctls, mz._nreset)
+        # QuadraticEnergy(0 * x, metric, g, _grad=-g) of NewtonCG.get_descent_direction:
+        # value 0, |gradient| = |g|
+        starts = [_State(0.0, r[1].gradient_norm, lambda: None) for _, r in reqs]
+        X, status = cg.run_packed(torch.zeros_like(G), -G, G, starts)
+        out = {}
+        for j, (i, _) in enumerate(reqs):
+            if status[j][0] == ctls[j].ERROR:
+                raise ValueError("Cannot find descent direction")
+            out[i] = _Dir(-X[j])
+        return out
+
+
+class _MetricCore:
+    """metric_flat_batch adapter of per-sample Newton metrics for FusedCGBatch"""
+
+    def __init__(self, mv, layout):
+        self.mv = mv
+        self.layout = layout
+        self.device = layout.device
+
+    def metric_flat_batch(self, D, Q, W, shift):
+        self.mv(D, Q)
+        if shift != 0.0:
+            Q.add_(D, alpha=shift)
+        return Q
+
+
+def plan(minimizer, f_lh, _unused, position):
+    """GeoVIBatch for this draw_samples call (expansion point `position`, a
+    latent MultiField), or None if the refinement has to run per sample
+    (unsupported model chain or minimizer)."""
+    from .descent_minimizers import NewtonCG
+    from .line_search import LineSearch
+    if not ENABLED:
+        return None
+    if type(minimizer) is not NewtonCG or type(minimizer.line_searcher) is not LineSearch:
+        return None
+    if minimizer._napprox != 0 or minimizer._history is not None:
+        return None
+    pipe = Pipeline.parse(f_lh)
+    if pipe is None or pipe.layout.device.type != "cuda" or pipe.layout.domain != position.domain:
+        return None
+    try:
+        return GeoVIBatch(pipe, pipe.layout.pack(position), minimizer)
+    except NotImplementedError as e:
+        logger.info(f"batched geoVI refinement unavailable: {e}")
+        return None

@@ -84,6 +84,26 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
         sols = met.solve_rhs([prepared[i] for i in drawing])
         prepared = dict(zip(drawing, sols))
     y = None
+    gb = None
+    if geometric and hi - lo > 1 and isinstance(sam_position, MultiField):
+        from . import geovi_batch
+        gb = geovi_batch.plan(minimizer, f_lh, None, sam_position)
+    if gb is not None:
+        # all local samples' NewtonCG refinements in lock step (geovi_batch):
+        # per sample the reference's minimizer logic, requests batched
+        lay = gb.layout
+        starts, means = [], []
+        for i in range(lo, hi):
+            neg = mirror_samples and (i % 2 != 0)
+            if not neg or y is None:
+                y, yi = prepared[i]
+                yp, yip = lay.pack(y), lay.pack(yi)
+            means.append(gb.tmean - yp if neg else gb.tmean + yp)
+            starts.append(gb.x0[0] - yip if neg else gb.x0[0] + yip)
+        for xf in gb.refine(starts, means):
+            local_samples.append(lay.unpack(xf - gb.x0[0]))
+            local_neg.append(False)
+        return ResidualSampleList(position, local_samples, local_neg, comm)
     for i in range(lo, hi):
         with random.Context(sseq[i]):
             neg = mirror_samples and (i % 2 != 0)

@@ -1,4 +1,5 @@
-"""Strong-Wolfe line search (src/minimization/line_search.py:24-420)."""
+"""Strong-Wolfe line search (src/minimization/line_search.py:24-420), written as a
+generator of evaluation requests (see LineSearch.perform_line_search_gen)."""
 import numpy as np
 
 from ..logger import logger
@@ -43,15 +44,41 @@ class LineSearch:
         self.max_iterations = int(max_iterations)
         self.max_zoom_iterations = int(max_zoom_iterations)
 
+    # The search is written as a generator of evaluation requests so that the
+    # geoVI refinement of several samples can serve them in batches
+    # (minimization/geovi_batch.py) with exactly this per-sample logic:
+    #   ("dd", energy, pk)        -> directional derivative  energy.gradient . pk
+    #   ("at", energy0, alpha, pk) -> the energy at energy0.position + alpha * pk
+    # (LineEnergy, line_search.py:24-80: le_0.at(alpha) with offset 0).
+    # perform_line_search drives it with immediate evaluations.
+
+    @staticmethod
+    def serve(req):
+        """Synchronous evaluation of one request (LineEnergy semantics)."""
+        if req[0] == "dd":
+            return LineEnergy(0., req[1], req[2], 0.).directional_derivative
+        if req[0] == "at":
+            return LineEnergy(0., req[1], req[3], 0.).at(req[2]).energy
+        raise ValueError(req[0])
+
     def perform_line_search(self, energy, pk, f_k_minus_1=None):
-        le_0 = LineEnergy(0., energy, pk, 0.)
+        gen = self.perform_line_search_gen(energy, pk, f_k_minus_1)
+        try:
+            req = next(gen)
+            while True:
+                req = gen.send(self.serve(req))
+        except StopIteration as e:
+            return e.value
+
+    def perform_line_search_gen(self, energy, pk, f_k_minus_1=None):
+        le_0 = energy
         maxstepsize = energy.longest_step(pk)
         if maxstepsize is None:
             maxstepsize = self.max_step_size
         maxstepsize = min(maxstepsize, self.max_step_size)
         old_phi_0 = f_k_minus_1
         phi_0 = le_0.value
-        phiprime_0 = le_0.directional_derivative
+        phiprime_0 = yield ("dd", le_0, pk)
         if phiprime_0 == 0:
             logger.warning("Directional derivative is zero; assuming convergence")
             return energy, False
@@ -71,12 +98,13 @@ class LineSearch:
             alpha1 = 1.0 / pk.norm()
         alpha1 = min(alpha1, 0.99 * maxstepsize)
         iteration_number = 0
+        le_alpha1 = None
         while iteration_number < self.max_iterations:
             iteration_number += 1
             if alpha1 == 0:
-                return le_0.energy, False
+                return le_0, False
             try:
-                le_alpha1 = le_0.at(alpha1)
+                le_alpha1 = yield ("at", le_0, alpha1, pk)
                 phi_alpha1 = le_alpha1.value
             except FloatingPointError:
                 alpha1 = (alpha0 + alpha1) / 2
@@ -86,24 +114,24 @@ class LineSearch:
                 continue
             if (phi_alpha1 > phi_0 + self.c1 * alpha1 * phiprime_0) or \
                     ((phi_alpha1 >= phi_alpha0) and (iteration_number > 1)):
-                return self._zoom(alpha0, alpha1, phi_0, phiprime_0, phi_alpha0, phiprime_alpha0,
-                                  phi_alpha1, le_0)
-            phiprime_alpha1 = le_alpha1.directional_derivative
+                return (yield from self._zoom(alpha0, alpha1, phi_0, phiprime_0, phi_alpha0, phiprime_alpha0,
+                                              phi_alpha1, le_0, pk))
+            phiprime_alpha1 = yield ("dd", le_alpha1, pk)
             if abs(phiprime_alpha1) <= -self.c2 * phiprime_0:
-                return le_alpha1.energy, True
+                return le_alpha1, True
             if phiprime_alpha1 >= 0:
-                return self._zoom(alpha1, alpha0, phi_0, phiprime_0, phi_alpha1, phiprime_alpha1,
-                                  phi_alpha0, le_0)
+                return (yield from self._zoom(alpha1, alpha0, phi_0, phiprime_0, phi_alpha1, phiprime_alpha1,
+                                              phi_alpha0, le_0, pk))
             alpha0, alpha1 = alpha1, min(2 * alpha1, maxstepsize)
             if alpha1 == maxstepsize:
                 logger.warning("max step size reached")
-                return le_alpha1.energy, False
+                return le_alpha1, False
             phi_alpha0 = phi_alpha1
             phiprime_alpha0 = phiprime_alpha1
         logger.warning("max iterations reached")
-        return le_alpha1.energy, False
+        return le_alpha1, False
 
-    def _zoom(self, alpha_lo, alpha_hi, phi_0, phiprime_0, phi_lo, phiprime_lo, phi_hi, le_0):
+    def _zoom(self, alpha_lo, alpha_hi, phi_0, phiprime_0, phi_lo, phiprime_lo, phi_hi, le_0, pk):
         cubic_delta = 0.2
         quad_delta = 0.1
         alpha_recent = None
@@ -123,15 +151,15 @@ class LineSearch:
                 alpha_j = self._quadmin(alpha_lo, phi_lo, phiprime_lo, alpha_hi, phi_hi)
                 if (alpha_j is None) or (alpha_j > b - quad_check) or (alpha_j < a + quad_check):
                     alpha_j = alpha_lo + 0.5 * delta_alpha
-            le_alphaj = le_0.at(alpha_j)
+            le_alphaj = yield ("at", le_0, alpha_j, pk)
             phi_alphaj = le_alphaj.value
             if (phi_alphaj > phi_0 + self.c1 * alpha_j * phiprime_0) or (phi_alphaj >= phi_lo):
                 alpha_recent, phi_recent = alpha_hi, phi_hi
                 alpha_hi, phi_hi = alpha_j, phi_alphaj
             else:
-                phiprime_alphaj = le_alphaj.directional_derivative
+                phiprime_alphaj = yield ("dd", le_alphaj, pk)
                 if abs(phiprime_alphaj) <= -self.c2 * phiprime_0:
-                    return le_alphaj.energy, True
+                    return le_alphaj, True
                 if phiprime_alphaj * delta_alpha >= 0:
                     alpha_recent, phi_recent = alpha_hi, phi_hi
                     alpha_hi, phi_hi = alpha_lo, phi_lo
@@ -140,7 +168,7 @@ class LineSearch:
                 alpha_lo, phi_lo, phiprime_lo = alpha_j, phi_alphaj, phiprime_alphaj
         else:
             logger.warning("The line search algorithm (zoom) did not converge.")
-            return le_alphaj.energy, False
+            return le_alphaj, False
 
     def _cubicmin(self, a, fa, fpa, b, fb, c, fc):
         with np.errstate(divide="raise", over="raise", invalid="raise"):
