@@ -1,0 +1,150 @@
+"""BASELINE.json configs C2-C5 at full size on one MI355X, checked through
+size-independent properties (the oracle does not finish at these sizes in
+seconds; the small-size parity against the reference's golden vectors is in
+test_parity_gpu.py):
+
+  C2  1024^2 CorrelatedField + Poisson, geoVI n_samples=4 (8 mirrored)
+  C3  2048^2 LOSResponse(16384) + sigmoid + Gaussian (the bench workload)
+  C4  512^3 3-D CorrelatedField + GeometryRemover Gaussian
+  C5  4096^2 CorrelatedField + Gaussian
+
+Properties: symmetry of the sampling metric <u, M v> = <M u, v> and its
+positivity, adjointness of the LOS box kernels and of the CF Jacobian,
+Hartley round trips, CG energy decrease, mirrored-sample structure and
+finiteness of a full geoVI draw (C2)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CF_ARGS = dict(offset_mean=0, offset_std=(1e-3, 1e-6), fluctuations=(1., 0.8),
+               loglogavgslope=(-3., 1), flexibility=(2, 1.), asperity=(0.5, 0.4))
+
+
+@pytest.fixture(scope="module")
+def ift(dev):
+    import nifty_amd
+    return nifty_amd
+
+
+def _dot(a, b):
+    return sum(float(torch.sum(a[k].val * b[k].val)) for k in a.keys())
+
+
+def _metric(ift, lh, pos):
+    dtype, f_lh = lh.get_transformation()
+    fl = f_lh(ift.Linearization.make_var(pos))
+    return (ift.SandwichOperator.make(fl.jac, ift.ScalingOperator(f_lh.target, 1., dtype))
+            + ift.ScalingOperator(fl.domain, 1., float)), fl
+
+
+def _check_metric(ift, met, dom, tol=1e-10):
+    u = ift.from_random(dom, "normal")
+    v = ift.from_random(dom, "normal")
+    mu, mv = met(u), met(v)
+    a, b = _dot(u, mv), _dot(mu, v)
+    assert abs(a - b) <= tol * max(abs(a), abs(b)), (a, b)
+    assert _dot(u, mu) >= _dot(u, u) * (1 - 1e-12)   # M = 1 + J^T W J >= 1
+
+
+def _gauss_problem(ift, shape, var=0.01, seed=17):
+    sp = ift.RGSpace(shape)
+    cf = ift.SimpleCorrelatedField(sp, **dict(CF_ARGS, asperity=None) if len(shape) == 3 else CF_ARGS)
+    R = ift.GeometryRemover(sp)
+    ift.random.push_sseq_from_seed(seed)
+    N = ift.ScalingOperator(R.target, var, np.float64)
+    data = R(cf(ift.from_random(cf.domain, "normal"))) + N.draw_sample()
+    pos = 0.1 * ift.from_random(cf.domain, "normal")
+    ift.random.pop_sseq()
+    lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ (R @ cf)
+    return cf, lh, pos
+
+
+def test_c2_poisson_geovi_1024(ift):
+    sp = ift.RGSpace((1024, 1024))
+    cf = ift.SimpleCorrelatedField(sp, **CF_ARGS)
+    sig = cf.exp()
+    ift.random.push_sseq_from_seed(27)
+    lam = sig(ift.from_random(cf.domain, "normal")).val.cpu().numpy()
+    counts = ift.random.current_rng().poisson(lam).astype(np.int64)
+    pos = 0.1 * ift.from_random(cf.domain, "normal")
+    ift.random.pop_sseq()
+    lh = ift.PoissonianEnergy(ift.makeField(sp, counts)) @ sig
+    met, _ = _metric(ift, lh, pos)
+    ift.random.push_sseq_from_seed(1)
+    _check_metric(ift, met, cf.domain)
+    ift.random.pop_sseq()
+    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=20))
+    mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=2), max_cg_iterations=10)
+    ift.random.push_sseq_from_seed(5)
+    sl = ift.draw_samples(pos, H, mini, 4, True)
+    ift.random.pop_sseq()
+    assert sl.n_samples == 8
+    for r in sl._r:
+        for k in cf.domain.keys():
+            assert torch.isfinite(r[k].val).all()
+    kl = ift.SampledKLEnergyClass(sl, H, [], None, True)
+    assert np.isfinite(kl.value)
+
+
+def test_c3_los_2048_adjoint_and_metric(ift):
+    sp = ift.RGSpace((2048, 2048))
+    cf = ift.SimpleCorrelatedField(sp, **CF_ARGS)
+    ift.random.push_sseq_from_seed(27)
+    rng = ift.random.current_rng()
+    nlos = 16384
+    starts = list(rng.random((nlos, 2)).T)
+    ends = list(rng.random((nlos, 2)).T)
+    R = ift.LOSResponse(sp, starts=starts, ends=ends)
+    x = ift.from_random(R.domain, "normal")
+    y = ift.from_random(R.target, "normal")
+    a = float(torch.sum(R(x).val * y.val))
+    b = float(torch.sum(x.val * R.adjoint(y).val))
+    assert abs(a - b) <= 1e-11 * abs(a)
+    sr = R @ ift.sigmoid(cf)
+    N = ift.ScalingOperator(R.target, 1e-3, np.float64)
+    data = sr(ift.from_random(cf.domain, "normal")) + N.draw_sample()
+    pos = 0.1 * ift.from_random(cf.domain, "normal")
+    lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ sr
+    met, fl = _metric(ift, lh, pos)
+    _check_metric(ift, met, cf.domain)
+    # CF Jacobian adjointness at full size
+    u = ift.from_random(cf.domain, "normal")
+    g = ift.from_random(fl.target, "normal")
+    a = float(torch.sum(fl.jac(u).val * g.val))
+    b = _dot(u, fl.jac.adjoint(g))
+    assert abs(a - b) <= 1e-10 * abs(a)
+    ift.random.pop_sseq()
+
+
+def test_c4_cube_512(ift):
+    shape = (512, 512, 512)
+    sp = ift.RGSpace(shape)
+    ht = ift.HartleyOperator(sp.get_default_codomain(), sp)
+    ift.random.push_sseq_from_seed(2)
+    x = ift.Field(ht.domain, torch.randn(shape, dtype=torch.float64, device="cuda"))
+    y = ht.inverse_times(ht.times(x))
+    err = float(torch.linalg.vector_norm(y.val - x.val) / torch.linalg.vector_norm(x.val))
+    assert err < 1e-12
+    del y
+    cf, lh, pos = _gauss_problem(ift, shape)
+    met, _ = _metric(ift, lh, pos)
+    _check_metric(ift, met, cf.domain)
+    b = ift.from_random(cf.domain, "normal")
+    ic = ift.GradientNormController(iteration_limit=3)
+    en, st = ift.ConjugateGradient(ic)(ift.QuadraticEnergy(0 * b, met, b))
+    assert st == ic.CONVERGED and en.value < 0
+    ift.random.pop_sseq()
+
+
+def test_c5_4096(ift):
+    cf, lh, pos = _gauss_problem(ift, (4096, 4096))
+    met, _ = _metric(ift, lh, pos)
+    ift.random.push_sseq_from_seed(9)
+    _check_metric(ift, met, cf.domain)
+    b = ift.from_random(cf.domain, "normal")
+    ic = ift.GradientNormController(iteration_limit=3)
+    en, st = ift.ConjugateGradient(ic)(ift.QuadraticEnergy(0 * b, met, b))
+    assert st == ic.CONVERGED and en.value < 0
+    ift.random.pop_sseq()
