@@ -9,6 +9,10 @@ import torch
 
 _config = dict(hartley_convention="non_canonical_hartley")
 _device = None
+# storage precision of the fused CG loops (build extension, BASELINE config
+# C5): "fp64" (default, the reference's arithmetic) or "fp32" (vectors and
+# grid operands in fp32, every reduction and all CG scalars in fp64)
+_cg_precision = "fp64"
 
 
 def update(key, value, /):
@@ -28,6 +32,17 @@ def update(key, value, /):
     else:
         raise ValueError(f"invalid key; got {key!r}")
     _config[key] = value
+
+
+def set_cg_precision(p):
+    global _cg_precision
+    if p not in ("fp64", "fp32"):
+        raise ValueError(f"cg precision must be 'fp64' or 'fp32'; got {p!r}")
+    _cg_precision = p
+
+
+def cg_dtype():
+    return torch.float32 if _cg_precision == "fp32" else torch.float64
 
 
 def hartley_convention_code():

@@ -406,6 +406,8 @@ class CFJacobian(LinearOperator):
         every stage launched once for the whole batch (nft_*_batched; the LOS
         matrix is streamed once for all rows).  Per row bitwise equal to
         metric_flat."""
+        if D.dtype == torch.float32:
+            return self._metric_flat_batch32(D, Q, W, shift)
         m = self._m
         lay = self.layout
         k, size = D.shape
@@ -439,6 +441,66 @@ class CFJacobian(LinearOperator):
         b = m.bins
         _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1)
         amp.native_vjp_batched(const, ga, Q, off, D, shift)
+        return Q
+
+    supports_fp32 = True
+
+    def _metric_flat_batch32(self, D, Q, W, shift):
+        """metric_flat_batch on fp32 storage (config.set_cg_precision("fp32")):
+        grid operands (A_full, xi0, the transforms, W, the bin sums) in fp32,
+        the B-sized amplitude Jacobian in fp64 on fp64 copies of the (small)
+        amplitude segments; every reduction accumulates in fp64."""
+        m = self._m
+        lay = self.layout
+        k, size = D.shape
+        amp = m.amp
+        B = amp.B
+        grid = tuple(self._afull.shape)
+        N = self._afull.numel()
+        off = dict(zip(lay.keys, lay.offsets))
+        xo = off[m.k_xi]
+        axes = tuple(range(1, 1 + len(grid)))
+        conv = hartley_convention_code()
+        const = self._const()
+        c32 = getattr(self, "_c32", None)
+        if c32 is None:
+            c32 = self._c32 = dict(afull=self._afull.float(), xi0=self._xi0.float(), W={})
+        segs = [(o, n) for kk, o, n in zip(lay.keys, lay.offsets, lay.sizes) if kk != m.k_xi]
+        D64 = torch.zeros((k, size), dtype=torch.float64, device=D.device)
+        for o, n in segs:
+            D64[:, o:o + n] = D[:, o:o + n]
+        da = torch.empty((B, k), dtype=torch.float64, device=self.device)
+        amp.native_jvp_batched(const, D64, off, da, interleave=True)
+        da32 = da.float()
+        s = torch.empty((k,) + grid, dtype=torch.float32, device=self.device)
+        pro = dict(a=c32["afull"], x=D[0, xo:], b=c32["xi0"], c=da32, index=m.bins.pindex)
+        _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
+                              batch=dict(period=N, x=size, c=1, c_elem=k))
+        if callable(W):
+            g = W(s)
+        else:
+            if torch.is_tensor(W):
+                key = W.data_ptr()
+                if key not in c32["W"]:
+                    c32["W"][key] = W.float()
+                g = s * c32["W"][key]
+            else:
+                g = s * float(W)
+        g = g.contiguous()
+        w = torch.empty((k,) + grid, dtype=torch.float32, device=self.device)
+        epi = dict(a=c32["afull"], b=c32["xi0"], out2=w)
+        bt = dict(period=N, out=size, out2=N)
+        if shift != 0.0:
+            epi.update(d=D[0, xo:], shift=shift)
+            bt["d"] = size
+        _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt)
+        ga = torch.empty((k, B), dtype=torch.float32, device=self.device)
+        b = m.bins
+        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1)
+        Q64 = torch.zeros((k, size), dtype=torch.float64, device=D.device)
+        amp.native_vjp_batched(const, ga.double(), Q64, off, D64, shift)
+        for o, n in segs:
+            Q[:, o:o + n] = Q64[:, o:o + n]
         return Q
 
     def metric_flat(self, d, q, W, shift):

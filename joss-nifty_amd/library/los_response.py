@@ -326,8 +326,18 @@ class LOSResponse(LinearOperator):
         plan = self._box_plan()
 
         npix = int(np.prod(shape))
+        cast = {}
+
+        def scales(dt):
+            # fp32 CG storage (config.set_cg_precision): scales in the input's dtype
+            if dt == torch.float64:
+                return drf, cv
+            if dt not in cast:
+                cast[dt] = (None if drf is None else drf.to(dt), None if cv is None else cv.to(dt))
+            return cast[dt]
 
         def middle(s):
+            drf, cv = scales(s.dtype)
             if s.dim() > len(shape):
                 # batch of right-hand sides along a leading axis (batched CG):
                 # the matrix is streamed once per launch for all of them
@@ -347,6 +357,7 @@ class LOSResponse(LinearOperator):
             _native.los_adjoint(plan, y, out.view(-1), rowscale=drf)
             return out
         middle.supports_batch = True
+        middle.supports_fp32 = True
         return middle
 
     @property

@@ -119,7 +119,19 @@ def fused_cg_or_none(energy, controller, nreset):
     core, W, shift = spec
     if energy.position.domain != core.domain or not core.device.type == "cuda":
         return None
+    if mixed_precision(core, W):
+        # fp32 storage runs in the batched loop (one right-hand side)
+        return FusedCGBatch(core, W, shift, [controller], nreset).run([energy])[0]
     return FusedCG(core, W, shift, controller, nreset).run(energy)
+
+
+def mixed_precision(core, W):
+    """fp32 CG storage requested (config.set_cg_precision) and supported by
+    the metric's native pipeline (else the solve stays fp64)."""
+    from .. import config
+    if config.cg_dtype() != torch.float32 or not getattr(core, "supports_fp32", False):
+        return False
+    return (not callable(W)) or getattr(W, "supports_fp32", False)
 
 
 class FusedCG:
@@ -296,7 +308,8 @@ class FusedCGBatch(FusedCG):
         lay, core = self.layout, self.core
         n = lay.size
         dev = core.device
-        X = torch.zeros((k, n), dtype=torch.float64, device=dev)
+        dt = torch.float32 if mixed_precision(core, self.W) else torch.float64
+        X = torch.zeros((k, n), dtype=dt, device=dev)
         Rr = torch.zeros_like(X)
         Bv = torch.zeros_like(X) if energies[0]._b is not None else None
         for j, e in enumerate(energies):
@@ -313,7 +326,8 @@ class FusedCGBatch(FusedCG):
             if moved is None:
                 results.append((e, st))
             else:
-                results.append((QuadraticEnergy(lay.unpack(X[j]), A, e._b, _grad=lay.unpack(Rr[j])), st))
+                results.append((QuadraticEnergy(lay.unpack(X[j].double()), A, e._b,
+                                                _grad=lay.unpack(Rr[j].double())), st))
         return results
 
     def run_packed(self, X, Rr, Bv, starts):
@@ -450,7 +464,7 @@ class FusedCGBatch(FusedCG):
 
                         def lazy(j=j, cache=cache):
                             if "v" not in cache:
-                                cache["v"] = (lay.unpack(X[j]), lay.unpack(Rr[j]))
+                                cache["v"] = (lay.unpack(X[j].double()), lay.unpack(Rr[j].double()))
                             return cache["v"]
                         value = 0.5 * (float(hj[_native.CG_XR]) - float(hj[_native.CG_XB]))
                         st = ctl.check(_State(value, math.sqrt(gamma), lazy))

@@ -148,3 +148,52 @@ def test_c5_4096(ift):
     en, st = ift.ConjugateGradient(ic)(ift.QuadraticEnergy(0 * b, met, b))
     assert st == ic.CONVERGED and en.value < 0
     ift.random.pop_sseq()
+
+
+@pytest.mark.parametrize("shape", [(256, 256), (4096, 4096), "los"])
+def test_c5_fp32_mixed_precision_cg(ift, shape):
+    """C5's fp32 storage / fp64-accumulated CG (config.set_cg_precision("fp32"))
+    against the fp64 solve of the same system: rtol 1e-4 (BASELINE.json C5)."""
+    from nifty_amd import config
+    from nifty_amd.minimization.fused_cg import fusable_metric, mixed_precision
+    if shape == "los":
+        sp = ift.RGSpace((512, 512))
+        cf = ift.SimpleCorrelatedField(sp, **CF_ARGS)
+        ift.random.push_sseq_from_seed(8)
+        rng = ift.random.current_rng()
+        R = ift.LOSResponse(sp, starts=list(rng.random((2000, 2)).T), ends=list(rng.random((2000, 2)).T))
+        sr = R @ ift.sigmoid(cf)
+        N = ift.ScalingOperator(R.target, 1e-3, np.float64)
+        data = sr(ift.from_random(cf.domain, "normal")) + N.draw_sample()
+        pos = 0.1 * ift.from_random(cf.domain, "normal")
+        ift.random.pop_sseq()
+        lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ sr
+    else:
+        cf, lh, pos = _gauss_problem(ift, shape)
+    met, _ = _metric(ift, lh, pos)
+    config.set_cg_precision("fp32")
+    try:
+        core, W, _ = fusable_metric(met)
+        assert mixed_precision(core, W)   # the fp32 pipeline is the one that runs
+    finally:
+        config.set_cg_precision("fp64")
+    ift.random.push_sseq_from_seed(4)
+    b = ift.from_random(cf.domain, "normal")
+    ift.random.pop_sseq()
+    res = {}
+    for prec in ("fp64", "fp32"):
+        config.set_cg_precision(prec)
+        try:
+            ic = ift.GradientNormController(iteration_limit=8)
+            en, st = ift.ConjugateGradient(ic)(ift.QuadraticEnergy(0 * b, met, b))
+        finally:
+            config.set_cg_precision("fp64")
+        assert st == ic.CONVERGED
+        res[prec] = en
+    for k in cf.domain.keys():
+        a = res["fp32"].position[k].val
+        r = res["fp64"].position[k].val
+        assert a.dtype == torch.float64
+        err = float(torch.linalg.vector_norm(a - r) / torch.linalg.vector_norm(r))
+        assert err < 1e-4, (k, err)
+    assert abs(res["fp32"].value - res["fp64"].value) < 1e-4 * abs(res["fp64"].value)
