@@ -128,6 +128,19 @@ int nft_bin_gather(const void* in, const int* pindex, void* out, int64_t pre, in
  * ascending j (perm = stable argsort of pindex: np.bincount order, bit-exact) */
 int nft_bin_scatter(const void* in, const int* perm, const int* offsets, void* out, int64_t pre,
                     int64_t npix, int64_t nbins, int64_t post, int dtype, hipStream_t stream);
+/* Same result (bitwise), faster gathers for post == 1: the sorted positions are
+ * processed in chunks of nft_bin_chunk() entries; gpix / gslot list every
+ * chunk's entries in ascending PIXEL order (gpix = the pixel, gslot = its
+ * position in the chunk, uint16), so a wavefront's gathers touch nearby
+ * memory; values are staged in LDS by gslot and each bin is still summed in
+ * ascending j.  chunk_bins (nchunks + 1 entries, or NULL): first bin owned by
+ * each chunk (the first bin whose offset is >= c * chunk; the last entry
+ * nbins) -- precomputed instead of a binary search per workgroup.
+ * gpix / gslot NULL: the plain sorted gathers of nft_bin_scatter. */
+int nft_bin_chunk(void);
+int nft_bin_scatter_ordered(const void* in, const int* perm, const int* offsets, const int* gpix,
+                            const uint16_t* gslot, const int* chunk_bins, void* out, int64_t pre,
+                            int64_t npix, int64_t nbins, int64_t post, int dtype, hipStream_t stream);
 
 /* ---- sparse LOS response --------------------------------------------- */
 /* y[r] = scale * sum_j weights[j] * x[indices[j]], j in [indptr[r], indptr[r+1]) */

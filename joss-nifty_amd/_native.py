@@ -38,6 +38,8 @@ SIGNATURES = {
     "nft_cg_residual": (_i, [_p, _p, _p, _p, _i64, _i, _d, _p, _p, _p]),
     "nft_bin_gather": (_i, [_p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_bin_scatter": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
+    "nft_bin_chunk": (_i, []),
+    "nft_bin_scatter_ordered": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
     "nft_csr_rowblocks": (_i, [_p, _i64, _p, _i64, ctypes.POINTER(_i64)]),
     "nft_spmv_scaled": (_i, [_p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i, _d, _p]),
@@ -238,9 +240,17 @@ def bin_gather(src, pindex, out, pre, npix, nbins, post):
     return out
 
 
-def bin_scatter(src, perm, offsets, out, pre, npix, nbins, post):
+def bin_scatter(src, perm, offsets, out, pre, npix, nbins, post, order=None):
+    """order: BinIndex.gather_order = (gpix, gslot, chunk_bins) (pixel-ordered
+    chunk gathers, precomputed chunk bounds; gpix/gslot may be None; same
+    result bitwise) or None."""
     lib = load()
     require_device(src, perm, offsets, out)
+    if order is not None:
+        gpix, gslot, cb = order
+        _check(lib.nft_bin_scatter_ordered(ptr(src), ptr(perm), ptr(offsets), ptr(gpix), ptr(gslot), ptr(cb),
+                                           ptr(out), pre, npix, nbins, post, dtype_code(src.dtype), stream_ptr()))
+        return out
     _check(lib.nft_bin_scatter(ptr(src), ptr(perm), ptr(offsets), ptr(out), pre, npix, nbins, post,
                                dtype_code(src.dtype), stream_ptr()))
     return out

@@ -365,7 +365,7 @@ class CFJacobian(LinearOperator):
         _native.hartley_fused(oxi, range(w.ndim), m.c_h, x=g.contiguous(), epi=epi,
                               convention=hartley_convention_code())
         ga = torch.empty(m.amp.B, dtype=w.dtype, device=w.device)
-        _native.bin_scatter(w, b.perm, b.offsets, ga, 1, b.npix, b.nbin, 1)
+        _native.bin_scatter(w, b.perm, b.offsets, ga, 1, b.npix, b.nbin, 1, order=b.gather_order)
         if out is None:
             if _AMP_TORCH:
                 res = m.amp.vjp(self._c, ga)
@@ -439,7 +439,7 @@ class CFJacobian(LinearOperator):
         _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt)
         ga = torch.empty((k, B), dtype=w.dtype, device=self.device)
         b = m.bins
-        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1)
+        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1, order=b.gather_order)
         amp.native_vjp_batched(const, ga, Q, off, D, shift)
         return Q
 
@@ -496,7 +496,7 @@ class CFJacobian(LinearOperator):
         _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt)
         ga = torch.empty((k, B), dtype=torch.float32, device=self.device)
         b = m.bins
-        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1)
+        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1, order=b.gather_order)
         Q64 = torch.zeros((k, size), dtype=torch.float64, device=D.device)
         amp.native_vjp_batched(const, ga.double(), Q64, off, D64, shift)
         for o, n in segs:
