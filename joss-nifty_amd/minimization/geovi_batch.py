@@ -52,6 +52,22 @@ NS = _native.CG_NSCALARS
 ENABLED = True   # tests compare against the per-sample path with ENABLED = False
 
 
+def _rowdots(pairs):
+    """[(A, B), ...] of (k, n) row batches -> host array (len(pairs), k) of
+    the fp64 row dot products (nft_dot_batched: deterministic two-level
+    reductions, one launch pair per operand pair, one D2H copy)."""
+    lib = _native.load()
+    k, n = pairs[0][0].shape
+    out = torch.empty((len(pairs), k), dtype=torch.float64, device=pairs[0][0].device)
+    ws = _native.workspace(k * lib.nft_reduce_workspace(n), out.device, "rowdot")
+    P = _native.ptr
+    for i, (A, B) in enumerate(pairs):
+        A, B = A.contiguous(), B.contiguous()
+        _native._check(lib.nft_dot_batched(P(A), P(B), n, n, k, _native.dtype_code(A.dtype), P(out[i]), 1,
+                                           P(ws), _native.stream_ptr()))
+    return out.cpu().numpy()
+
+
 # ------------------------------------------------------------------ stages
 class _CFStage:
     """The fused correlated-field model (library/correlated_fields_simple.py)
@@ -359,31 +375,44 @@ class GeoVIBatch:
     def _J0(self, V):
         return self.pipe.jvp(self.st0, V)
 
+    def _latent(self, k, device):
+        """(k, size) buffer for a J^T output: every key segment is overwritten
+        by the adjoint, so only the alignment padding is zeroed"""
+        lay = self.layout
+        Q = torch.empty((k, lay.size), dtype=torch.float64, device=device)
+        ends = [o + n for o, n in zip(lay.offsets, lay.sizes)]
+        starts = list(lay.offsets[1:]) + [lay.size]
+        for a, b in zip(ends, starts):
+            if b > a:
+                Q[:, a:b] = 0.0
+        return Q
+
     def _J0T(self, F):
-        Q = torch.zeros((F.shape[0], self.layout.size), dtype=torch.float64, device=F.device)
-        return self.pipe.vjp(self.st0, F, Q)
+        return self.pipe.vjp(self.st0, F, self._latent(F.shape[0], F.device))
 
     def _JT(self, states, G):
-        Q = torch.zeros((G.shape[0], self.layout.size), dtype=torch.float64, device=G.device)
-        return self.pipe.vjp(states, G, Q)
+        return self.pipe.vjp(states, G, self._latent(G.shape[0], G.device))
 
     def evaluate(self, X, M):
         """values, |gradient|, gradients and per-sample states at the rows of X"""
         F, states = self.pipe.fwd(X)
-        Rr = X + self._J0T(F) - M
-        G = Rr + self._JT(states, self._J0(Rr))
+        Rr = self._J0T(F)
+        Rr.add_(X).sub_(M)
+        G = self._JT(states, self._J0(Rr))
+        G.add_(Rr)
         k = X.shape[0]
-        sc = torch.stack([(Rr * Rr).sum(1), (G * G).sum(1)], 1)
-        h = sc.cpu().numpy()
-        vals = [0.5 * float(h[i, 0]) for i in range(k)]
-        gn = [math.sqrt(float(h[i, 1])) for i in range(k)]
+        h = _rowdots([(Rr, Rr), (G, G)])
+        vals = [0.5 * float(h[0, i]) for i in range(k)]
+        gn = [math.sqrt(float(h[1, i])) for i in range(k)]
         return vals, gn, G, states
 
     def metric_batch(self, states):
         """callable (D, Q) -> Q = M_b D for the stacked per-sample states"""
         def mv(D, Q):
-            U = D + self._J0T(self.pipe.jvp(states, D))
-            Q.copy_(U + self._JT(states, self._J0(U)))
+            U = self._J0T(self.pipe.jvp(states, D))
+            U.add_(D)
+            self.pipe.vjp(states, self._J0(U), Q)   # overwrites every key segment
+            Q.add_(U)
             return Q
         return mv
 
@@ -449,7 +478,7 @@ class GeoVIBatch:
     def _serve_dd(self, reqs):
         G = torch.stack([r[1].g for _, r in reqs])
         P = torch.stack([r[2].v for _, r in reqs])
-        h = (G * P).sum(1).cpu().numpy()
+        h = _rowdots([(G, P)])[0]
         return {i: float(h[j]) for j, (i, _) in enumerate(reqs)}
 
     def _serve_dir(self, reqs):
