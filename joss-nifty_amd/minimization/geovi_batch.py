@@ -57,12 +57,15 @@ def _rowdots(pairs):
     the fp64 row dot products (nft_dot_batched: deterministic two-level
     reductions, one launch pair per operand pair, one D2H copy)."""
     lib = _native.load()
-    k, n = pairs[0][0].shape
+    k = pairs[0][0].shape[0]
+    nmax = max(A.shape[1] for A, _ in pairs)
     out = torch.empty((len(pairs), k), dtype=torch.float64, device=pairs[0][0].device)
-    ws = _native.workspace(k * lib.nft_reduce_workspace(n), out.device, "rowdot")
+    ws = _native.workspace(k * lib.nft_reduce_workspace(nmax), out.device, "rowdot")
     P = _native.ptr
     for i, (A, B) in enumerate(pairs):
         A, B = A.contiguous(), B.contiguous()
+        n = A.shape[1]
+        assert A.shape == B.shape and A.shape[0] == k
         _native._check(lib.nft_dot_batched(P(A), P(B), n, n, k, _native.dtype_code(A.dtype), P(out[i]), 1,
                                            P(ws), _native.stream_ptr()))
     return out.cpu().numpy()
@@ -270,7 +273,10 @@ class Pipeline:
         from ..operators.scaling_operator import ScalingOperator
         from ..operators.simple_linear_operators import GeometryRemover
         from ..pointwise import ptw_dict
-        ops = list(f_lh._ops) if isinstance(f_lh, _OpChain) else [f_lh]
+        if isinstance(f_lh, (list, tuple)):
+            ops = [o for op in f_lh for o in (op._ops if isinstance(op, _OpChain) else (op,))]
+        else:
+            ops = list(f_lh._ops) if isinstance(f_lh, _OpChain) else [f_lh]
         if not ops or not isinstance(ops[-1], _CorrelatedFieldModel):
             return None
         stages = [_CFStage(ops[-1])]
@@ -544,3 +550,79 @@ def plan(minimizer, f_lh, _unused, position):
     except NotImplementedError as e:
         logger.info(f"batched geoVI refinement unavailable: {e}")
         return None
+
+
+# ------------------------------------------------------------------ KL terms
+def kl_batch(hamiltonian, positions):
+    """Hamiltonian values and gradients at a list of latent MultiFields in one
+    batched pass (SampledKLEnergyClass, kl_energies.py:295-356: its per
+    sample H(Linearization.make_var(s)) evaluations), or None if the
+    likelihood is not a GaussianEnergy(data, scaling / diagonal inverse
+    covariance) or PoissonianEnergy applied to a supported model chain.
+
+    Returns ([value_i], [gradient_i MultiField])."""
+    if not ENABLED or len(positions) < 2:
+        return None
+    from ..operators.diagonal_operator import DiagonalOperator
+    from ..operators.energy_operators import GaussianEnergy, PoissonianEnergy, _LikelihoodChain
+    from ..operators.scaling_operator import ScalingOperator
+    lh = hamiltonian.likelihood_energy
+    if not isinstance(lh, _LikelihoodChain):
+        return None
+    ops = list(lh._op._ops)
+    scale = 1.0
+    if isinstance(ops[0], ScalingOperator):      # scaled likelihood (lh.scale(f))
+        scale = float(np.real(ops[0]._factor))
+        ops = ops[1:]
+    E = ops[0]
+    if isinstance(E, GaussianEnergy):
+        if E._data is None:
+            return None
+        ic = E._icov
+        if isinstance(ic, ScalingOperator) and np.isreal(ic._factor):
+            icv = float(np.real(ic._factor))
+        elif isinstance(ic, DiagonalOperator) and not ic._complex:
+            icv = ic.diagonal_tensor.reshape(-1)
+        else:
+            return None
+        kind = "gauss"
+    elif isinstance(E, PoissonianEnergy):
+        kind = "poisson"
+    else:
+        return None
+    pipe = Pipeline.parse(ops[1:])
+    if pipe is None or pipe.layout.device.type != "cuda" or pipe.layout.domain != positions[0].domain:
+        return None
+    lay = pipe.layout
+    X = torch.stack([lay.pack(p) for p in positions])
+    k = X.shape[0]
+    Sf, states = pipe.fwd(X)
+    S = Sf.reshape(k, -1)
+    if kind == "gauss":
+        d = E._data.val.reshape(1, -1).to(S.dtype)
+        R = S - d
+        W = R * icv
+        h = _rowdots([(R, W), (X, X)])
+        lval = 0.5 * h[0]
+        gs = W
+    else:
+        d = E._dfloat.val.reshape(1, -1)
+        D = d.expand_as(S).contiguous()
+        ones = torch.ones_like(S)
+        h = _rowdots([(S, ones), (torch.log(S), D), (X, X)])
+        lval = h[0] - h[1]
+        h = h[[0, 2]]
+        gs = 1. - D / S
+    if scale != 1.0:
+        lval = scale * lval
+        gs = gs * scale
+    Q = torch.empty((k, lay.size), dtype=torch.float64, device=X.device)
+    ends = [o + n for o, n in zip(lay.offsets, lay.sizes)]
+    starts = list(lay.offsets[1:]) + [lay.size]
+    for a, b in zip(ends, starts):
+        if b > a:
+            Q[:, a:b] = 0.0
+    G = pipe.vjp(states, gs.reshape(Sf.shape).contiguous(), Q)
+    G.add_(X)                                      # prior: 0.5 x.x
+    vals = [float(lval[i]) + 0.5 * float(h[1, i]) for i in range(k)]
+    return vals, [lay.unpack(G[i]) for i in range(k)]

@@ -160,7 +160,15 @@ class SampledKLEnergyClass(Energy):
         def _func(inp):
             tmp = hamiltonian(Linearization.make_var(inp))
             return tmp.val.val.real.item(), tmp.gradient
-        self._val, self._grad = sample_list._average_tuple(_func)
+        # all local samples' H value / gradient in one batched pass where the
+        # likelihood allows (geovi_batch.kl_batch), else per sample
+        from . import geovi_batch
+        pos = list(sample_list.local_iterator())
+        kb = geovi_batch.kl_batch(hamiltonian, pos) if isinstance(sample_list._m, MultiField) else None
+        if kb is not None:
+            self._val, self._grad = sample_list._average_results(list(zip(*kb)))
+        else:
+            self._val, self._grad = sample_list._average_tuple(_func)
         if np.isnan(self._val) and self._nanisinf:
             self._val = np.inf
 

@@ -66,7 +66,10 @@ class ResidualSampleList:
 
     def _average_tuple(self, func):
         """Average a tuple-valued function over all samples (sample_list.py:312-341)."""
-        res = [func(s) for s in self.local_iterator()]
+        return self._average_results([func(s) for s in self.local_iterator()])
+
+    def _average_results(self, res):
+        """The reduction of _average_tuple on precomputed per-sample tuples."""
         n = self._ntotal
         out = []
         for k in range(len(res[0]) if res else 0):

@@ -98,3 +98,29 @@ def test_batched_path_is_taken(ift):
     dtype, f_lh = lh.get_transformation()
     mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=1))
     assert geovi_batch.plan(mini, f_lh, None, pos) is not None
+
+
+@pytest.mark.parametrize("kind", ["los", "gauss", "poisson"])
+def test_batched_kl_matches_per_sample(ift, kind):
+    """SampledKLEnergyClass value / gradient through geovi_batch.kl_batch vs
+    the per-sample Hamiltonian evaluations (rtol 1e-12)."""
+    from nifty_amd.minimization import geovi_batch
+    cf, lh, pos = _problem(ift, kind)
+    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=5))
+    ift.random.push_sseq_from_seed(7)
+    sl = ift.draw_samples(pos, H, None, 2, True)
+    ift.random.pop_sseq()
+    dtype, _ = lh.get_transformation()
+    assert geovi_batch.kl_batch(H, list(sl.local_iterator())) is not None
+    kls = {}
+    for enabled in (True, False):
+        geovi_batch.ENABLED = enabled
+        try:
+            kls[enabled] = ift.SampledKLEnergyClass(sl, H, [], None, True)
+        finally:
+            geovi_batch.ENABLED = True
+    a, b = kls[True], kls[False]
+    assert abs(a.value - b.value) <= 1e-12 * abs(b.value)
+    for k in cf.domain.keys():
+        ga, gb = a.gradient[k].val.cpu().numpy(), b.gradient[k].val.cpu().numpy()
+        assert np.linalg.norm(ga - gb) <= 1e-11 * max(np.linalg.norm(gb), 1e-300), k
