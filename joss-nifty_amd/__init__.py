@@ -30,6 +30,7 @@ from .minimization.kl_energies import SampledKLEnergy, SampledKLEnergyClass, dra
 from .minimization.line_search import LineSearch
 from .minimization.quadratic_energy import QuadraticEnergy
 from .minimization.sample_list import ResidualSampleList
+from .probing import StatCalculator, approximation2endo, probe_diagonal
 from .multi_domain import MultiDomain
 from .multi_field import MultiField
 from .operators.adder import Adder

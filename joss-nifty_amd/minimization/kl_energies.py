@@ -31,8 +31,6 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
         raise TypeError
     if not isinstance(H, StandardHamiltonian):
         raise TypeError
-    if napprox != 0:
-        raise NotImplementedError("napprox preconditioning is a 'next' item (SURVEY.md §8(f))")
     sam_position = position.extract(H.domain) if isinstance(position, MultiField) else position
 
     geometric = minimizer is not None
@@ -49,6 +47,13 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
                               ScalingOperator(fl.domain, 1., float), H.iteration_controller)
     else:
         met = H(Linearization.make_var(sam_position, want_metric=True)).metric
+    if napprox >= 1:
+        # diagonal preconditioner from napprox metric samples
+        # (kl_energies.py:127-128, probing.py:142-152); the draws use the
+        # current RNG state before the sample seeds are spawned
+        from ..probing import approximation2endo
+        from ..sugar import makeOp
+        met._approximation = makeOp(approximation2endo(met, napprox))
 
     parent = random._sseq[-1]
     sseq = random.spawn_sseq(n_samples)
@@ -132,17 +137,62 @@ def _distinct(seqs):
     return out
 
 
+def _reduce_field(field, keys):
+    """kl_energies.py:41-44"""
+    if isinstance(field, MultiField) and len(keys) > 0:
+        return field.extract_by_keys(set(field.keys()) - set(keys))
+    return field
+
+
+def _reduce_by_keys(field, operator, keys):
+    """Partially insert the constant keys of ``field`` into ``operator``
+    (kl_energies.py:47-75): returns the variable part and the contracted
+    operator."""
+    if isinstance(field, MultiField):
+        cst_field = field.extract_by_keys(keys)
+        var_field = field.extract_by_keys(set(field.keys()) - set(keys))
+        _, operator = operator.simplify_for_constant_input(cst_field)
+        return var_field, operator
+    myassert(len(keys) == 0)
+    return field, operator
+
+
 def SampledKLEnergy(position, hamiltonian, n_samples, minimizer_sampling, mirror_samples=True,
                     constants=[], point_estimates=[], napprox=0, comm=None, nanisinf=True):
+    """kl_energies.py:161-292.  ``constants`` are kept fixed during the KL
+    minimisation, ``point_estimates`` are not sampled; a key in both is
+    inserted into the Hamiltonian and removed from the KL (``invariants``)."""
+    from .descent_minimizers import DescentMinimizer
     if not isinstance(hamiltonian, StandardHamiltonian):
         raise TypeError
     if hamiltonian.domain is not position.domain:
         raise ValueError
-    if len(constants) or len(point_estimates):
-        raise NotImplementedError("constants/point_estimates are a 'next' item (SURVEY.md §8(f))")
-    sample_list = draw_samples(position, hamiltonian, minimizer_sampling, n_samples, mirror_samples,
+    if not isinstance(n_samples, int):
+        raise TypeError
+    if not isinstance(mirror_samples, bool):
+        raise TypeError
+    if not (minimizer_sampling is None or isinstance(minimizer_sampling, DescentMinimizer)):
+        raise TypeError
+    if isinstance(position, MultiField):
+        if not set(constants).issubset(set(position.keys())):
+            raise ValueError("Constants are not a subset of the keys of the latent space\n"
+                             f"Latent space keys: {position.keys()}\nConstants keys: {constants}")
+        if not set(point_estimates).issubset(set(position.keys())):
+            raise ValueError("Point estimates are not a subset of the keys of the latent space\n"
+                             f"Latent space keys: {position.keys()}\n"
+                             f"Point estimate keys: {point_estimates}")
+        if set(point_estimates) == set(position.keys()):
+            raise RuntimeError("Point estimates for whole domain. Use EnergyAdapter instead.")
+    invariant = list(set(constants).intersection(point_estimates))
+    if isinstance(position, MultiField) and len(invariant) > 0:
+        inv_pos = position.extract_by_keys(invariant)
+    else:
+        inv_pos = None
+    position, hamiltonian = _reduce_by_keys(position, hamiltonian, invariant)
+    _, ham_sampling = _reduce_by_keys(position, hamiltonian, point_estimates)
+    sample_list = draw_samples(position, ham_sampling, minimizer_sampling, n_samples, mirror_samples,
                                napprox=napprox, comm=comm)
-    return SampledKLEnergyClass(sample_list, hamiltonian, constants, None, nanisinf)
+    return SampledKLEnergyClass(sample_list, hamiltonian, constants, inv_pos, nanisinf)
 
 
 class SampledKLEnergyClass(Energy):
@@ -150,7 +200,11 @@ class SampledKLEnergyClass(Energy):
 
     def __init__(self, sample_list, hamiltonian, constants, invariants, nanisinf):
         myassert(isinstance(sample_list, ResidualSampleList))
-        super().__init__(sample_list._m)
+        myassert(sample_list.domain is hamiltonian.domain)
+        if isinstance(sample_list._m, MultiField):
+            if not (invariants is None or isinstance(invariants, MultiField)):
+                raise TypeError
+        super().__init__(_reduce_field(sample_list._m, constants))
         self._sample_list = sample_list
         self._hamiltonian = hamiltonian
         self._nanisinf = bool(nanisinf)
@@ -158,13 +212,15 @@ class SampledKLEnergyClass(Energy):
         self._invariants = invariants
 
         def _func(inp):
-            tmp = hamiltonian(Linearization.make_var(inp))
+            inp, tmp = _reduce_by_keys(inp, hamiltonian, constants)
+            tmp = tmp(Linearization.make_var(inp))
             return tmp.val.val.real.item(), tmp.gradient
         # all local samples' H value / gradient in one batched pass where the
         # likelihood allows (geovi_batch.kl_batch), else per sample
         from . import geovi_batch
-        pos = list(sample_list.local_iterator())
-        kb = geovi_batch.kl_batch(hamiltonian, pos) if isinstance(sample_list._m, MultiField) else None
+        kb = None
+        if isinstance(sample_list._m, MultiField) and len(constants) == 0:
+            kb = geovi_batch.kl_batch(hamiltonian, list(sample_list.local_iterator()))
         if kb is not None:
             self._val, self._grad = sample_list._average_results(list(zip(*kb)))
         else:
@@ -186,7 +242,8 @@ class SampledKLEnergyClass(Energy):
 
     def apply_metric(self, x):
         def _func(inp):
-            tmp = self._hamiltonian(Linearization.make_var(inp, want_metric=True))
+            inp, tmp = _reduce_by_keys(inp, self._hamiltonian, self._constants)
+            tmp = tmp(Linearization.make_var(inp, want_metric=True))
             return tmp.metric(x)
         return self._sample_list.average(_func)
 
@@ -197,4 +254,6 @@ class SampledKLEnergyClass(Energy):
 
     @property
     def samples(self):
-        return self._sample_list
+        if self._invariants is None:
+            return self._sample_list
+        return self._sample_list.at(self._invariants)

@@ -41,18 +41,19 @@ class ResidualSampleList:
 
     @property
     def domain(self):
-        return self._r[0].domain if self._nlocal > 0 else self._m.domain
+        return self._m.domain
 
     @property
     def mean(self):
         return self._m
 
     def local_item(self, i):
+        # residuals may live on a sub-domain of the mean (point estimates):
+        # the missing keys get a zero residual (sample_list.py:486-487)
         r = self._r[i]
-        m = self._m if isinstance(self._m, MultiField) and not isinstance(r, MultiField) else self._m
-        if isinstance(m, MultiField) and isinstance(r, MultiField) and m.domain is not r.domain:
-            m = m.extract(r.domain)
-        return m - r if self._n[i] else m + r
+        if isinstance(self._m, MultiField) and self._m.domain is not r.domain:
+            return self._m.flexible_addsub(r, self._n[i])
+        return self._m - r if self._n[i] else self._m + r
 
     def local_iterator(self):
         for i in range(self._nlocal):
@@ -83,6 +84,10 @@ class ResidualSampleList:
         return utilities.allreduce_sum(res, self._comm) / self._ntotal
 
     def at(self, mean):
+        """sample_list.py:489-507: only the keys present in ``mean`` are
+        updated."""
+        if isinstance(self._m, MultiField) and self.domain is not mean.domain:
+            mean = MultiField.union([self._m, mean])
         return ResidualSampleList(mean, self._r, self._n, self._comm)
 
     def sample_stat(self, op=None):

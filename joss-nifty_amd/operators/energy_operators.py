@@ -243,3 +243,9 @@ class StandardHamiltonian(EnergyOperator):
 
     def __repr__(self):
         return "StandardHamiltonian:\n" + utilities.indent(repr(self._lh))
+
+    def _simplify_for_constant_input_nontrivial(self, c_inp):
+        # energy_operators.py:829-831: the prior of the constant keys is a
+        # constant and drops out; the likelihood gets the constants inserted
+        out, lh1 = self._lh.simplify_for_constant_input(c_inp)
+        return out, StandardHamiltonian(lh1, self._ic_samp)

@@ -198,8 +198,13 @@ class Operator:
 
     def simplify_for_constant_input(self, c_inp):
         from ..multi_field import MultiField
-        if c_inp is None:
+        if c_inp is None or (isinstance(c_inp, MultiField) and len(c_inp.keys()) == 0):
             return None, self
+        if isinstance(c_inp.domain, MultiDomain) and len(c_inp.domain) == 0:
+            return None, self
+        if isinstance(self.domain, MultiDomain) and isinstance(c_inp.domain, MultiDomain):
+            if not set(c_inp.keys()) <= set(self.domain.keys()):
+                raise ValueError("constant keys are not a subset of the operator's domain")
         if c_inp.domain == self.domain:
             op = _ConstantOperator(self.force(c_inp))
             return op(c_inp), op

@@ -389,7 +389,96 @@ def gen_random():
     _save("random.npz", d)
 
 
+KL_CASES = (((), ()), (("fluctuations", "zeromode"), ()), ((), ("loglogavgslope", "spectrum")),
+            (("fluctuations", "zeromode"), ("zeromode", "asperity")), (("xi",), ("xi",)))
+
+
+def gen_kl_constants():
+    """SampledKLEnergy with constants / point estimates / invariants
+    (kl_energies.py:161-356, sample_list.py:486-507) on the 32^2 Gaussian
+    problem: MGVI (6 CG steps) and geoVI (one short Newton step), one mirrored
+    pair, seed 41.  Records the KL position keys, value, gradient and the
+    residual samples."""
+    cf, lh, data, mock, pos = _gaussian_problem(32)
+    d = {"data": data.val}
+    for k, v in _flat(pos).items():
+        d["pos_" + k] = v
+    # the reference's own rounding sensitivity: the same draw at an expansion
+    # point whose xi is perturbed by 1e-15 (relative); tests allow 10x this
+    pos_p = ift.MultiField.from_dict({k: (v * (1 + 1e-15) if k == "xi" else v) for k, v in pos.items()})
+
+    def _rel(a, b):
+        return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+    for ci, (cst, pe) in enumerate(KL_CASES):
+        for geo in (False, True):
+            kls = []
+            for p in (pos, pos_p):
+                H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=6))
+                mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=1)) if geo else None
+                ift.random.push_sseq_from_seed(41)
+                kls.append(ift.SampledKLEnergy(p, H, 1, mini, True, constants=list(cst),
+                                               point_estimates=list(pe)))
+                ift.random.pop_sseq()
+            kl, klp = kls
+            tag = f"c{ci}{'g' if geo else 'm'}_"
+            d[tag + "sens_grad"] = np.array(max(_rel(klp.gradient[k].val, kl.gradient[k].val)
+                                                for k in kl.gradient.keys()))
+            d[tag + "sens_samples"] = np.array(max(
+                _rel(klp.samples.local_item(i)[k].val, kl.samples.local_item(i)[k].val)
+                for i in range(kl.samples.n_samples) for k in pos.keys() if k != "xi" or "xi" not in pe))
+            d[tag + "value"] = np.array(kl.value)
+            d[tag + "keys"] = np.array(sorted(kl.position.keys()))
+            for k, v in _flat(kl.gradient).items():
+                d[tag + "grad_" + k] = v
+            sl = kl.samples
+            for i in range(sl.n_samples):
+                for k, v in _flat(sl.local_item(i)).items():
+                    d[tag + f"s{i}_" + k] = v
+    _save("kl32_constants.npz", d)
+
+
+def gen_napprox():
+    """draw_samples with the napprox diagonal preconditioner
+    (kl_energies.py:127-128, probing.py:142-152): MGVI and geoVI on the 32^2
+    Gaussian problem, napprox=3, seed 43, 6 preconditioned CG steps."""
+    cf, lh, data, mock, pos = _gaussian_problem(32)
+    d = {}
+    pos_p = ift.MultiField.from_dict({k: (v * (1 + 1e-15) if k == "xi" else v) for k, v in pos.items()})
+    for geo in (False, True):
+        sls = []
+        for p in (pos, pos_p):
+            H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=6))
+            mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=1)) if geo else None
+            ift.random.push_sseq_from_seed(43)
+            sls.append(ift.minimization.kl_energies.draw_samples(p, H, mini, 1, True, napprox=3))
+            ift.random.pop_sseq()
+        sl = sls[0]
+        tag = "g_" if geo else "m_"
+        # the reference's own change under a 1e-15 perturbation of xi
+        d[tag + "sens"] = np.array(max(
+            np.linalg.norm(b[k].val - a[k].val) / max(np.linalg.norm(a[k].val), 1e-300)
+            for a, b in zip(sls[0]._r, sls[1]._r) for k in pos.keys()))
+        for i, (r, neg) in enumerate(zip(sl._r, sl._n)):
+            for k, v in _flat(r).items():
+                d[tag + f"r{i}_" + k] = v
+            d[tag + f"neg{i}"] = np.array(neg)
+    # the preconditioner diagonal itself (MGVI metric, same seed)
+    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=6))
+    ift.random.push_sseq_from_seed(43)
+    met = H(ift.Linearization.make_var(pos, want_metric=True)).metric
+    diag = ift.probing.approximation2endo(met, 3)
+    ift.random.pop_sseq()
+    for k, v in _flat(diag).items():
+        d["diag_" + k] = v
+    _save("napprox32.npz", d)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()["gen_" + name]()
+        sys.exit(0)
     gen_dispatch()
     gen_geometry()
     gen_cf()
@@ -399,3 +488,5 @@ if __name__ == "__main__":
     gen_los()
     gen_los_metric()
     gen_random()
+    gen_kl_constants()
+    gen_napprox()

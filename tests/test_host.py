@@ -250,3 +250,15 @@ def test_rng_prefetch_bit_identical():
         np.testing.assert_array_equal(u, np.random.default_rng(ss).uniform(0., 1., (4,)))
     finally:
         R.pop_sseq()
+
+
+def test_stat_calculator():
+    """probing.StatCalculator (probing.py:24-71): Welford mean / unbiased var."""
+    from nifty_amd.probing import StatCalculator
+    rng = np.random.default_rng(3)
+    xs = rng.normal(size=(7, 5))
+    sc = StatCalculator()
+    for x in xs:
+        sc.add(x)
+    np.testing.assert_allclose(sc.mean, xs.mean(0), rtol=1e-14)
+    np.testing.assert_allclose(sc.var, xs.var(0, ddof=1), rtol=1e-13)
