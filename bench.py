@@ -142,6 +142,9 @@ def byte_model(cf, R, k, n_lat):
     nseg = int(P["nseg"])
     nbox = int(P["nbox"])
     nlos = R.target.shape[0]
+    # the Jacobian adjoint's bin sums run over the mirror-folded cell (N_f)
+    fold = getattr(getattr(cf, "jbins", None), "fold", None)
+    Nf = fold["nf"] if fold else N
     return {
         # prologue A*x + xi0*dA[pindex]: x (k), A, xi0, pindex, dA (k); half spectrum out (k)
         "fft_r2c+pro": 8 * k * N + 8 * N + 8 * N + 4 * N + 8 * k * B + 16 * k * Hh,
@@ -156,7 +159,10 @@ def byte_model(cf, R, k, n_lat):
         "los_fwd_items": 5 * nnz + 12 * nseg + 8 * (k + 1) * N + 8 * k * nseg,
         "los_fwd_reduce": 8 * k * nseg + 8 * k * nlos,
         "los_adj_boxes": 5 * nnz + 4 * nseg + 2 * 257 * nbox + 8 * (k + 1) * N,
-        "bin_scatter": 4 * N + 8 * k * N + 4 * B + 8 * k * B,
+        # mirror fold: w (k) in, folded cell (k) out
+        "bin_fold": 8 * k * N + 8 * k * Nf,
+        # perm over the cell, cell values (k), bin offsets, sums (k)
+        "bin_scatter": 4 * Nf + 8 * k * Nf + 4 * B + 8 * k * B,
         "cg_dir_kernel": 3 * 8 * k * n_lat,
         "curv_partial": 2 * 8 * k * n_lat,
         "cg_update_kernel": 7 * 8 * k * n_lat,

@@ -141,6 +141,16 @@ int nft_bin_chunk(void);
 int nft_bin_scatter_ordered(const void* in, const int* perm, const int* offsets, const int* gpix,
                             const uint16_t* gslot, const int* chunk_bins, void* out, int64_t pre,
                             int64_t npix, int64_t nbins, int64_t post, int dtype, hipStream_t stream);
+/* Mirror fold onto the fundamental cell of a harmonic grid (replaces, with
+ * nft_bin_scatter on the folded grid, DOFDistributor._adjoint_times for
+ * PowerSpace bins, src/operators/distributors.py:105-112: |k| and hence the bin
+ * is invariant under k_a -> -k_a, rg_space.py:101-121):
+ *   out[p, q] = sum of in[p, i] over the distinct images i_a in {q_a, n_a - q_a}
+ * in: (pre, shape[0..ndim-1]); out: (pre, shape[a]/2 + 1 ...); 1 <= ndim <= 3.
+ * Fixed summation order (deterministic), not np.bincount's order: the bin sums
+ * agree with the reference to rounding (rtol ~1e-15), not bitwise. */
+int nft_bin_fold(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
+                 hipStream_t stream);
 
 /* ---- sparse LOS response --------------------------------------------- */
 /* y[r] = scale * sum_j weights[j] * x[indices[j]], j in [indptr[r], indptr[r+1]) */
@@ -211,7 +221,8 @@ int nft_hartley_fused(const nft_hartley_fuse* fuse, const void* in, void* out, i
  *             a segment is the run of one line of sight inside one box:
  *             entries seg_ent[s]..[s+1] with 8-bit local pixel ent_loc and fp32
  *             weight ent_wf; its partial goes to slot seg_slot[s]; line l owns
- *             slots los_ptr[l]..[l+1] (in box order).
+ *             slots los_ptr[l]..[l+1] (in box order).  The forward workspace
+ *             holds the partial of vector v in slot k at ws[k * nvec + v].
  *   adjoint:  box b owns entries box_ent[b]..[b+1], sorted by local pixel;
  *             pixel t of the box owns pix_off[257*b+t]..[257*b+t+1] (uint16,
  *             relative to box_ent[b]); the lines crossing box b are

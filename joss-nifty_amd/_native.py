@@ -39,6 +39,7 @@ SIGNATURES = {
     "nft_bin_gather": (_i, [_p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_bin_scatter": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_bin_chunk": (_i, []),
+    "nft_bin_fold": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_scatter_ordered": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
     "nft_csr_rowblocks": (_i, [_p, _i64, _p, _i64, ctypes.POINTER(_i64)]),
@@ -253,6 +254,15 @@ def bin_scatter(src, perm, offsets, out, pre, npix, nbins, post, order=None):
         return out
     _check(lib.nft_bin_scatter(ptr(src), ptr(perm), ptr(offsets), ptr(out), pre, npix, nbins, post,
                                dtype_code(src.dtype), stream_ptr()))
+    return out
+
+
+def bin_fold(src, out, pre, shape):
+    """Mirror fold of (pre, *shape) onto (pre, *[n//2+1]) (nft_bin_fold)."""
+    lib = load()
+    require_device(src, out)
+    sh = (ctypes.c_int64 * len(shape))(*shape)
+    _check(lib.nft_bin_fold(ptr(src), ptr(out), pre, len(shape), sh, dtype_code(src.dtype), stream_ptr()))
     return out
 
 

@@ -168,6 +168,69 @@ __global__ __launch_bounds__(256) void bin_scatter_chunk(const T* __restrict__ i
   }
 }
 
+
+// Mirror fold of a harmonic-grid array (pre, n_0, ..., n_{d-1}) onto its
+// fundamental cell (pre, h_0, ..., h_{d-1}), h_a = n_a/2 + 1:
+//   out[p, q] = sum over the distinct mirror images i of q (i_a = q_a or
+//               n_a - q_a) of in[p, i]
+// |k| -- hence the power bin -- is invariant under k_a -> -k_a on every axis
+// (RGSpace.get_k_length_array, rg_space.py:101-121), so the bin sums of the
+// grid equal the bin sums of the folded cell (2^d fewer scattered gathers).
+// Each output sums its <= 2^d images in a fixed order (deterministic); the
+// last axis is the fastest thread index: the reads of q and n - q are two
+// coalesced runs (one ascending, one descending).
+constexpr int FOLD_MAXD = 3;
+struct FoldShape {
+  int d;
+  long long n[FOLD_MAXD], h[FOLD_MAXD];
+  long long nin, nout;  // elements per pre item
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void bin_fold_kernel(const T* __restrict__ in, T* __restrict__ out, FoldShape fs,
+                                                       long long pre) {
+  const long long tot = pre * fs.nout;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += stride) {
+    long long r = e % fs.nout;
+    const long long p = e / fs.nout;
+    long long q[FOLD_MAXD], m[FOLD_MAXD];
+    bool two[FOLD_MAXD];
+#pragma unroll
+    for (int a = FOLD_MAXD - 1; a >= 0; --a) {
+      if (a < fs.d) {
+        q[a] = r % fs.h[a];
+        r /= fs.h[a];
+        m[a] = fs.n[a] - q[a];
+        two[a] = q[a] != 0 && m[a] != q[a];
+      } else {
+        q[a] = m[a] = 0;
+        two[a] = false;
+      }
+    }
+    const T* src = in + p * fs.nin;
+    T acc = (T)0;
+#pragma unroll
+    for (int s = 0; s < (1 << FOLD_MAXD); ++s) {
+      bool ok = true;
+      long long idx = 0;
+#pragma unroll
+      for (int a = 0; a < FOLD_MAXD; ++a) {
+        if (a >= fs.d) {
+          ok = ok && !((s >> (FOLD_MAXD - 1 - a)) & 1);
+          continue;
+        }
+        const bool hi = (s >> (FOLD_MAXD - 1 - a)) & 1;
+        ok = ok && (!hi || two[a]);
+        idx = idx * fs.n[a] + (hi ? m[a] : q[a]);
+      }
+      if (ok) acc += src[idx];
+    }
+    out[e] = acc;
+  }
+}
+
+
 static int nblocks(long long tot) {
   long long b = (tot + 255) / 256;
   if (b < 1) b = 1;
@@ -260,4 +323,41 @@ int nft_bin_scatter_ordered(const void* in, const int* perm, const int* offsets,
   return NFT_OK;
 }
 
+int nft_bin_fold(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
+                 hipStream_t stream) {
+  if (ndim < 1 || ndim > FOLD_MAXD || pre < 0) {
+    set_last_error("nft_bin_fold: need 1 <= ndim <= 3 and pre >= 0");
+    return NFT_ERR_ARG;
+  }
+  FoldShape fs{};
+  fs.d = ndim;
+  fs.nin = fs.nout = 1;
+  for (int a = 0; a < ndim; ++a) {
+    if (shape[a] < 1) {
+      set_last_error("nft_bin_fold: bad shape");
+      return NFT_ERR_ARG;
+    }
+    fs.n[a] = shape[a];
+    fs.h[a] = shape[a] / 2 + 1;
+    fs.nin *= fs.n[a];
+    fs.nout *= fs.h[a];
+  }
+  const long long tot = pre * fs.nout;
+  if (tot <= 0) return NFT_OK;
+  prof_mark(stream, "bin_fold");
+  if (dtype == 0)
+    hipLaunchKernelGGL(bin_fold_kernel<double>, dim3(nblocks(tot)), dim3(256), 0, stream, (const double*)in,
+                       (double*)out, fs, (long long)pre);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(bin_fold_kernel<float>, dim3(nblocks(tot)), dim3(256), 0, stream, (const float*)in,
+                       (float*)out, fs, (long long)pre);
+  else {
+    set_last_error("nft_bin_fold: bad dtype");
+    return NFT_ERR_ARG;
+  }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
 }  // extern "C"
+

@@ -11,8 +11,10 @@
 //        segments): stage cs*x of the box in LDS (16 rows of 128 B), form
 //        w * u[loc] for the item's entries (8-bit local pixel index + fp32
 //        weight per nonzero), and sum each segment in storage order; the
-//        partial goes to its slot in LOS-major order.
-//    K2 (one wave per line of sight): fixed-order sum of its partials.
+//        partial goes to its slot in LOS-major order, the K vectors of a
+//        slot adjacent (one 8K-byte store per segment).
+//    K2 (one wave per line of sight): fixed-order sum of its slots, read
+//        contiguously for all K vectors.
 //  adjoint  out = rs * R^T (cs * y):
 //    K3 (one workgroup per box): the values cs*y of the ~100 lines crossing
 //        the box are cached in LDS once; w * y[line] for the box's entries
@@ -29,6 +31,7 @@ constexpr int LOS_CAP_F = 2048;  // entries per forward work item (host-guarante
 constexpr int LOS_CH_A = 2048;   // adjoint: entries staged in LDS per chunk
 constexpr int LOS_YL = 2048;     // adjoint: LDS slots for the line values of a box (all batch vectors)
 constexpr int LOS_KMAX = 8;      // vectors per batched launch
+constexpr int LOS_SEG_ROUNDS = 4;  // forward: <= 256 segments per item = 4 rounds of 64 quads (host-guaranteed)
 
 struct BoxGeom {
   long long H, W;
@@ -50,10 +53,16 @@ struct BoxGeom {
 // applied to every vector's tile; each segment's 4-lane group accumulates all
 // K vectors in registers.  Per vector the products and their summation order
 // are those of K = 1 (bitwise).
+//
+// Segment s's partial of vector b goes to part[seg_slot[s] * pk + b] (pk =
+// vectors of the call): one contiguous store per segment for all vectors, and
+// the reduce reads each line's slots contiguously.  The bounds and slots of
+// all of a thread's segments (LOS_SEG_ROUNDS rounds of 64) are loaded before
+// the barrier, off the critical path of the segment loop.
 template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __restrict__ x,
                                                      const T* __restrict__ cs, double* __restrict__ part,
-                                                     long long xs, long long ps) {
+                                                     long long xs, int pk) {
   // every product is rounded before it is summed, in all K variants alike
   // (no FMA contraction): batched results are bitwise the K = 1 results
 #pragma clang fp contract(off)
@@ -91,14 +100,17 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
     }
     u[b][t] = v;
   }
-  // four lanes per segment; the first segment's bounds are loaded early too
+  // four lanes per segment: thread t serves segments sq + 64 r
+  constexpr int RND = LOS_SEG_ROUNDS;
   const int sub = t & 3;
-  int s = s0 + (t >> 2);
-  int sa = 0, sb = 0, slot = 0;
-  if (s < s1) {
-    sa = p.seg_ent[s] - e0;
-    sb = p.seg_ent[s + 1] - e0;
-    slot = p.seg_slot[s];
+  const int sq = s0 + (t >> 2);
+  int sa[RND], sb[RND], so[RND];
+#pragma unroll
+  for (int r = 0; r < RND; ++r) {
+    const int s = sq + 64 * r;
+    sa[r] = s < s1 ? p.seg_ent[s] - e0 : 0;
+    sb[r] = s < s1 ? p.seg_ent[s + 1] - e0 : 0;
+    so[r] = s < s1 ? p.seg_slot[s] : 0;
   }
   if (K > 1 && staged) {
 #pragma unroll
@@ -122,31 +134,29 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       }
     }
     __syncthreads();
-    while (s < s1) {
+    auto seg1 = [&](int slot, int a, int e) {
       double a0 = 0.0;
       if (staged) {
-        for (int k = sa + sub; k < sb; k += 4) a0 += prod[k];
+        for (int k = a + sub; k < e; k += 4) a0 += prod[k];
       } else {
-        for (int k = sa + sub; k < sb; k += 4)
+        for (int k = a + sub; k < e; k += 4)
           a0 = a0 + (double)p.ent_wf[e0 + k] * u[0][p.ent_loc[e0 + k]];
       }
       a0 += __shfl_xor(a0, 1, 64);
       a0 += __shfl_xor(a0, 2, 64);
-      if (sub == 0) part[slot] = a0;
-      s += 64;
-      if (s < s1) {
-        sa = p.seg_ent[s] - e0;
-        sb = p.seg_ent[s + 1] - e0;
-        slot = p.seg_slot[s];
-      }
-    }
+      if (sub == 0) part[(long long)slot * pk] = a0;
+    };
+#pragma unroll
+    for (int r = 0; r < RND; ++r)
+      if (sq + 64 * r < s1) seg1(so[r], sa[r], sb[r]);
+    for (int s = sq + 64 * RND; s < s1; s += 64) seg1(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
     return;
   }
-  while (s < s1) {
+  auto segk = [&](int slot, int a, int e) {
     double acc[K];
 #pragma unroll
     for (int b = 0; b < K; ++b) acc[b] = 0.0;
-    for (int k = sa + sub; k < sb; k += 4) {
+    for (int k = a + sub; k < e; k += 4) {
       const double w = staged ? (double)ew[k] : (double)p.ent_wf[e0 + k];
       const int l = staged ? el[k] : p.ent_loc[e0 + k];
 #pragma unroll
@@ -154,38 +164,51 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
     }
 #pragma unroll
     for (int b = 0; b < K; ++b) {
-      double a = acc[b];
-      a += __shfl_xor(a, 1, 64);
-      a += __shfl_xor(a, 2, 64);
-      if (sub == 0) part[b * ps + slot] = a;
+      double v = acc[b];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      // every lane of the quad holds the sum: lane sub stores vectors sub, sub + 4
+      if ((b & 3) == sub) part[(long long)slot * pk + b] = v;
     }
-    s += 64;
-    if (s < s1) {
-      sa = p.seg_ent[s] - e0;
-      sb = p.seg_ent[s + 1] - e0;
-      slot = p.seg_slot[s];
-    }
-  }
+  };
+#pragma unroll
+  for (int r = 0; r < RND; ++r)
+    if (sq + 64 * r < s1) segk(so[r], sa[r], sb[r]);
+  for (int s = sq + 64 * RND; s < s1; s += 64) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
 }
 
+// one wave per line of sight, all K vectors: the line's slots (boxes
+// ascending) hold K adjacent partials each; per vector a fixed-order sum
+// (lane strides, then a shuffle tree)
 template <typename T>
 __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const double* __restrict__ part,
                                                       const T* __restrict__ rs, T* __restrict__ y, double scale,
-                                                      long long ps, long long ys) {
+                                                      int K, long long ys) {
   const int lane = threadIdx.x & 63;
   const long long l = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= p.nlos) return;
-  part += blockIdx.y * ps;
-  y += blockIdx.y * ys;
   const int a = p.los_ptr[l], b = p.los_ptr[l + 1];
-  double acc = 0.0;
-  for (int k = a + lane; k < b; k += 64) acc += part[k];
+  double acc[LOS_KMAX];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-  if (lane == 0) {
-    acc *= scale;
-    if (rs) acc *= (double)rs[l];
-    y[l] = (T)acc;
+  for (int v = 0; v < LOS_KMAX; ++v) acc[v] = 0.0;
+  for (int k = a + lane; k < b; k += 64) {
+    const double* q = part + (long long)k * K;
+#pragma unroll
+    for (int v = 0; v < LOS_KMAX; ++v)
+      if (v < K) acc[v] += q[v];
+  }
+#pragma unroll
+  for (int v = 0; v < LOS_KMAX; ++v) {
+    if (v < K) {
+      double s = acc[v];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+      if (lane == 0) {
+        s *= scale;
+        if (rs) s *= (double)rs[l];
+        y[v * ys + l] = (T)s;
+      }
+    }
   }
 }
 
@@ -200,11 +223,14 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
                                                      long long ys, long long os) {
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CH_A / 256;
-  constexpr int YL = LOS_YL;
+  // line table: 256 lines per vector cover every box of an 8-bit-index plan
+  // (boxes with more lines read y from global memory); sized per K so that
+  // K = 4 fits 8 workgroups per CU (18 KB of LDS instead of 28 KB)
+  constexpr int YL = 256 * K < LOS_YL ? 256 * K : LOS_YL;
   __shared__ double yl[YL];
   // K == 1 uses ew as a double product buffer (LOS_CH_A doubles)
   __shared__ __align__(16) float ew[K == 1 ? 2 * LOS_CH_A : LOS_CH_A];
-  __shared__ unsigned short el[K == 1 ? 1 : LOS_CH_A];
+  __shared__ IDX el[K == 1 ? 1 : LOS_CH_A];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int box = blockIdx.x, t = threadIdx.x;
   const int l0 = p.box_lptr[box], nl = p.box_lptr[box + 1] - l0;
@@ -277,7 +303,7 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
       const int k = t + i * 256;
       if (k < cn) {
         ew[k] = wv[i];
-        el[k] = (unsigned short)lv[i];
+        el[k] = (IDX)lv[i];
       }
     }
     __syncthreads();
@@ -313,9 +339,9 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
 }
 
 template <typename T, int K>
-static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* part, long long xs, long long ps,
+static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* part, long long xs, int pk,
                         hipStream_t s) {
-  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, ps);
+  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, pk);
 }
 
 template <typename T, typename IDX, int K>
@@ -331,26 +357,25 @@ static int kgroup(int k) { return k >= 8 ? 8 : (k >= 4 ? 4 : (k >= 2 ? 2 : 1)); 
 template <typename T>
 static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, const void* rs, void* y, double* part,
                          double scale, int K, long long xs, long long ys, hipStream_t s) {
-  const long long ps = p->nseg;
   prof_mark(s, "los_fwd_items");
   if (p->nitems > 0) {
     for (int v = 0; v < K;) {
       const int g = kgroup(K - v);
       const T* xv = (const T*)x + v * xs;
-      double* pv = part + v * ps;
+      double* pv = part + v;  // slot-major partials, K per slot
       switch (g) {
-        case 8: fwd_items_k<T, 8>(p, xv, (const T*)cs, pv, xs, ps, s); break;
-        case 4: fwd_items_k<T, 4>(p, xv, (const T*)cs, pv, xs, ps, s); break;
-        case 2: fwd_items_k<T, 2>(p, xv, (const T*)cs, pv, xs, ps, s); break;
-        default: fwd_items_k<T, 1>(p, xv, (const T*)cs, pv, xs, ps, s); break;
+        case 8: fwd_items_k<T, 8>(p, xv, (const T*)cs, pv, xs, K, s); break;
+        case 4: fwd_items_k<T, 4>(p, xv, (const T*)cs, pv, xs, K, s); break;
+        case 2: fwd_items_k<T, 2>(p, xv, (const T*)cs, pv, xs, K, s); break;
+        default: fwd_items_k<T, 1>(p, xv, (const T*)cs, pv, xs, K, s); break;
       }
       v += g;
     }
   }
   prof_mark(s, "los_fwd_reduce");
   if (p->nlos > 0)
-    hipLaunchKernelGGL(los_fwd_reduce<T>, dim3((unsigned)((p->nlos + 3) / 4), (unsigned)K), dim3(256), 0, s, *p,
-                       part, (const T*)rs, (T*)y, scale, ps, ys);
+    hipLaunchKernelGGL(los_fwd_reduce<T>, dim3((unsigned)((p->nlos + 3) / 4)), dim3(256), 0, s, *p, part,
+                       (const T*)rs, (T*)y, scale, K, ys);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

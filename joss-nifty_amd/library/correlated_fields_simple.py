@@ -365,7 +365,7 @@ class CFJacobian(LinearOperator):
         _native.hartley_fused(oxi, range(w.ndim), m.c_h, x=g.contiguous(), epi=epi,
                               convention=hartley_convention_code())
         ga = torch.empty(m.amp.B, dtype=w.dtype, device=w.device)
-        _native.bin_scatter(w, b.perm, b.offsets, ga, 1, b.npix, b.nbin, 1, order=b.gather_order)
+        m.jbins.scatter(w, ga, 1)
         if out is None:
             if _AMP_TORCH:
                 res = m.amp.vjp(self._c, ga)
@@ -438,8 +438,7 @@ class CFJacobian(LinearOperator):
             bt["d"] = size
         _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt)
         ga = torch.empty((k, B), dtype=w.dtype, device=self.device)
-        b = m.bins
-        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1, order=b.gather_order)
+        m.jbins.scatter(w, ga, k)
         amp.native_vjp_batched(const, ga, Q, off, D, shift)
         return Q
 
@@ -495,8 +494,7 @@ class CFJacobian(LinearOperator):
             bt["d"] = size
         _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt)
         ga = torch.empty((k, B), dtype=torch.float32, device=self.device)
-        b = m.bins
-        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1, order=b.gather_order)
+        m.jbins.scatter(w, ga, k)
         Q64 = torch.zeros((k, size), dtype=torch.float64, device=D.device)
         amp.native_vjp_batched(const, ga.double(), Q64, off, D64, shift)
         for o, n in segs:
@@ -525,6 +523,9 @@ class _CorrelatedFieldModel(Operator):
         self.c_h = float(harmonic_partner.scalar_dvol)
         self.offset_mean = None if offset_mean is None else float(offset_mean)
         self.bins = BinIndex.get(self.amp.pspace.pindex, self.amp.B, config.device())
+        # bin sums of the Jacobian adjoint: mirror-folded where the grid allows
+        # (rounding-level parity); the value path keeps the bincount order
+        self.jbins = BinIndex.get(self.amp.pspace.pindex, self.amp.B, config.device(), fold=True)
         self._layout = None
         self.amplitude = _AmplitudeOperator(self.amp)
         self.power_spectrum = _AmplitudeOperator(self.amp, power=2)

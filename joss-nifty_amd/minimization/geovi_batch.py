@@ -167,8 +167,7 @@ class _CFStage:
         _native.hartley_fused(Q[0, self.xo:], self.axes, m.c_h, x=G.contiguous(), epi=epi,
                               convention=hartley_convention_code(), shape=(k,) + self.grid, batch=batch)
         ga = torch.empty((k, m.amp.B), dtype=G.dtype, device=G.device)
-        b = m.bins
-        _native.bin_scatter(w, b.perm, b.offsets, ga, k, b.npix, b.nbin, 1, order=b.gather_order)
+        m.jbins.scatter(w, ga, k)
         m.amp.native_vjp_batched(st["consts"][0], ga, Q, self.off,
                                  item_consts=None if shared else st["dconst"].data_ptr())
         return Q

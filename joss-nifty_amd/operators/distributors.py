@@ -2,6 +2,8 @@
 
 Forward (gather) and adjoint (deterministic segmented scatter, bit-identical
 to np.bincount) run as native kernels (csrc/nft_cf.hip)."""
+import os
+
 import numpy as np
 import torch
 
@@ -13,26 +15,77 @@ from ..utilities import infer_space
 from .linear_operator import LinearOperator
 
 
+def _chunk_bins(offs, nbin, npix):
+    """First bin owned by each chunk of nft_bin_chunk() sorted positions (the
+    first bin whose offset is >= c * chunk), last entry nbin (int32)."""
+    ch = int(_native.load().nft_bin_chunk())
+    nch = (npix + ch - 1) // ch
+    cb = np.searchsorted(offs[:-1], np.arange(nch + 1, dtype=np.int64) * ch, side="left")
+    cb[-1] = nbin
+    return cb.astype(np.int32)
+
+
 class BinIndex:
     """Device-resident bin index: pindex (int32) plus the stable bin->pixel
     permutation and CSR offsets for the adjoint.  Built once on the host."""
     _cache = {}
 
-    def __init__(self, dofdex, nbin, device):
-        dofdex = np.asarray(dofdex).ravel()
+    def __init__(self, dofdex, nbin, device, fold=False):
+        grid = np.asarray(dofdex)
+        dofdex = grid.ravel()
         self.npix = dofdex.size
         self.nbin = int(nbin)
+        if self.npix >= 2 ** 31:
+            raise ValueError("grids with >= 2^31 pixels are not supported")
+        self._order = None
+        self.fold = self._make_fold(grid, device) if fold and self.FOLD else None
+        if self.fold is not None:
+            # a folded index serves scatter() only: no full-grid permutation
+            self.pindex = self.perm = self.offsets = None
+            return
         perm = np.argsort(dofdex, kind="stable")
         cnt = np.bincount(dofdex, minlength=self.nbin)
         offs = np.zeros(self.nbin + 1, dtype=np.int64)
         np.cumsum(cnt, out=offs[1:])
-        if self.npix >= 2 ** 31:
-            raise ValueError("grids with >= 2^31 pixels are not supported")
         self.pindex = torch.from_numpy(dofdex.astype(np.int32)).to(device)
         self.perm = torch.from_numpy(perm.astype(np.int32)).to(device)
         self.offsets = torch.from_numpy(offs.astype(np.int32)).to(device)
-        self.counts = cnt
-        self._order = None
+
+    # Mirror-folded adjoint (nft_bin_fold + scatter over the fundamental cell,
+    # 2^d fewer scattered gathers) for harmonic grids whose bins are invariant
+    # under k_a -> -k_a on every axis.  Sums agree with np.bincount to rounding
+    # (not bitwise), so only the fused CF Jacobian paths ask for it; the
+    # PowerDistributor operator keeps the bit-exact scatter.
+    FOLD = os.environ.get("NFT_BIN_FOLD", "1") != "0"
+
+    def _make_fold(self, grid, device):
+        shp = grid.shape
+        if not (1 <= len(shp) <= 3) or self.npix < 4096:
+            return None
+        for ax in range(len(shp)):
+            if not np.array_equal(grid, np.roll(np.flip(grid, ax), 1, ax)):
+                return None
+        f = np.ascontiguousarray(grid[tuple(slice(0, n // 2 + 1) for n in shp)]).ravel()
+        perm = np.argsort(f, kind="stable")
+        offs = np.zeros(self.nbin + 1, dtype=np.int64)
+        np.cumsum(np.bincount(f, minlength=self.nbin), out=offs[1:])
+        cb = _chunk_bins(offs, self.nbin, f.size)
+        return dict(shape=tuple(int(n) for n in shp), nf=int(f.size),
+                    perm=torch.from_numpy(perm.astype(np.int32)).to(device),
+                    offsets=torch.from_numpy(offs.astype(np.int32)).to(device),
+                    order=(None, None, torch.from_numpy(cb).to(device)))
+
+    def scatter(self, w, out, pre):
+        """out[p, b] = sum over the pixels of bin b of w[p, :] (w: pre grids,
+        contiguous).  Folded when available, else the bit-exact scatter."""
+        f = self.fold
+        if f is None:
+            return _native.bin_scatter(w, self.perm, self.offsets, out, pre, self.npix, self.nbin, 1,
+                                       order=self.gather_order)
+        wf = torch.empty((pre, f["nf"]), dtype=w.dtype, device=w.device)
+        _native.bin_fold(w, wf, pre, f["shape"])
+        return _native.bin_scatter(wf, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
+                                   order=f["order"])
 
     # pixel-ordered chunk gathers: measured no faster than the sorted ones at
     # 2048^2 (the chunk kernel is bound by its per-bin phase, not by gather
@@ -52,9 +105,7 @@ class BinIndex:
             dev = self.perm.device
             nch = (perm.size + ch - 1) // ch
             offs = self.offsets.cpu().numpy().astype(np.int64)
-            cb = np.searchsorted(offs[:-1], np.arange(nch + 1, dtype=np.int64) * ch, side="left")
-            cb[-1] = self.nbin
-            cbt = torch.from_numpy(cb.astype(np.int32)).to(dev)
+            cbt = torch.from_numpy(_chunk_bins(offs, self.nbin, perm.size)).to(dev)
             if self.PIXEL_ORDER:
                 cid = np.arange(perm.size, dtype=np.int64) // ch
                 order = np.lexsort((perm, cid))
@@ -66,11 +117,12 @@ class BinIndex:
         return self._order
 
     @classmethod
-    def get(cls, dofdex, nbin, device):
-        key = (id(dofdex), int(nbin), str(device))
+    def get(cls, dofdex, nbin, device, fold=False):
+        fold = bool(fold) and cls.FOLD
+        key = (id(dofdex), int(nbin), str(device), fold)
         obj = cls._cache.get(key)
         if obj is None or obj._ref is not dofdex:
-            obj = cls(dofdex, nbin, device)
+            obj = cls(dofdex, nbin, device, fold)
             obj._ref = dofdex
             cls._cache[key] = obj
         return obj

@@ -67,6 +67,35 @@ def test_bin_index_matches_bincount_order():
         assert np.all(p.ravel()[members] == bin_)
 
 
+def test_bin_fold_layout_host():
+    """Host half of the mirror-folded Jacobian bin sums: BinIndex(fold=True)
+    indexes the fundamental cell; summing each cell point's mirror images
+    (numpy restatement of nft_bin_fold) and then the cell's bins reproduces
+    np.bincount on the full grid to rounding.  Asymmetric grids do not fold."""
+    import nifty_amd as ift
+    from nifty_amd.operators.distributors import BinIndex
+    rng = np.random.default_rng(2)
+    for shape in [(64, 64), (63, 67), (16, 18, 20), (4097,)]:
+        grid = np.asarray(ift.PowerSpace(ift.RGSpace(shape, harmonic=True)).pindex)
+        nb = int(grid.max()) + 1
+        f = BinIndex(grid, nb, "cpu", fold=True).fold
+        assert f is not None and f["nf"] == int(np.prod([n // 2 + 1 for n in shape]))
+        x = rng.standard_normal(shape)
+        xf = x
+        for ax, n in enumerate(shape):
+            q = np.arange(n // 2 + 1)
+            two = ((q != 0) & (2 * q != n)).reshape([-1 if a == ax else 1 for a in range(len(shape))])
+            xf = np.take(xf, q, axis=ax) + np.where(two, np.take(xf, (n - q) % n, axis=ax), 0.)
+        xf = xf.ravel()
+        perm, offs = f["perm"].numpy(), f["offsets"].numpy()
+        got = np.array([xf[perm[offs[i]:offs[i + 1]]].sum() for i in range(nb)])
+        g = grid.ravel()
+        ref = np.bincount(g, weights=x.ravel(), minlength=nb)
+        bound = 1e-15 * np.bincount(g, minlength=nb) * np.bincount(g, weights=np.abs(x).ravel(), minlength=nb)
+        assert np.all(np.abs(got - ref) <= bound), shape
+    assert BinIndex(rng.integers(0, 50, (64, 64)), 50, "cpu", fold=True).fold is None
+
+
 def test_random_streams_match_reference():
     import nifty_amd as ift
     G = golden("random.npz")

@@ -45,6 +45,8 @@ def main(n=2048):
                     lambda: nat.bin_scatter(w, b.perm, b.offsets, ga, k, N, B, 1, order=b.gather_order))
                 run(f"{lab:6s} no-order         k={k}",
                     lambda: nat.bin_scatter(w, b.perm, b.offsets, ga, k, N, B, 1))
+                bf = BinIndex(pi.reshape(n, n), B, "cuda", fold=True)
+                run(f"{lab:6s} mirror-folded    k={k}", lambda: bf.scatter(w, ga, k))
 
 
 if __name__ == "__main__":
