@@ -663,10 +663,13 @@ __global__ void fuse_epi_kernel(fast::FuseArgs f, const T* __restrict__ h, T* __
 template <typename T>
 __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __restrict__ u, long long P,
                                                         int nb) {
-  const T* px = (const T*)f.px;
-  const T* pa = (const T*)f.pa;
-  const T* pb = (const T*)f.pb;
-  const T* pc = (const T*)f.pc;
+  // restrict-qualified: the loads of the next element may be issued before
+  // the stores of this one
+  const T* __restrict__ px = (const T*)f.px;
+  const T* __restrict__ pa = (const T*)f.pa;
+  const T* __restrict__ pb = (const T*)f.pb;
+  const T* __restrict__ pc = (const T*)f.pc;
+  const int* __restrict__ pidx = f.pidx;
   using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   // interleaved dA (ce == nb, sc == 1): each pixel's gather is one contiguous
   // run; read it with 2-wide vector loads (half the divergent load
@@ -675,7 +678,7 @@ __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __r
   for (long long j = (long long)blockIdx.x * 256 + threadIdx.x; j < P; j += (long long)gridDim.x * 256) {
     const T a = pa ? pa[j] : (T)1;
     const T bj = pb ? pb[j] : (T)0;
-    const int ix = pb ? f.pidx[j] : 0;
+    const int ix = pb ? pidx[j] : 0;
     if (vec) {
       const V2* q = (const V2*)(pc + (long long)ix * nb);
 #pragma unroll 2
@@ -714,7 +717,9 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
       (long long)f.nb * f.P == ntot &&
       ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
     T* u = (T*)((char*)ws + align256(hws));
-    const unsigned nblk = (unsigned)std::min<long long>((f.P + 255) / 256, 8192);
+    // one element per thread (no grid-stride chain of dependent gathers)
+    static const long long cap = getenv("NFT_PRO_NBLK") ? atoll(getenv("NFT_PRO_NBLK")) : (1LL << 30);
+    const unsigned nblk = (unsigned)std::min<long long>((f.P + 255) / 256, cap);
     prof_mark(s, "pro_batch");
     hipLaunchKernelGGL(pro_batch_kernel<T>, dim3(nblk), dim3(256), 0, s, f, u, f.P, f.nb);
     NFT_HIP_CHECK(hipGetLastError());
