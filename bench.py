@@ -165,7 +165,9 @@ def byte_model(cf, R, k, n_lat):
         "bin_scatter": 4 * Nf + 8 * k * Nf + 4 * B + 8 * k * B,
         "cg_dir_kernel": 3 * 8 * k * n_lat,
         "curv_partial": 2 * 8 * k * n_lat,
-        "cg_update_kernel": 7 * 8 * k * n_lat,
+        # x, r, d, q in; x, r out (b is not streamed: the probe passes none,
+        # and the sampling CG's value-blind controllers skip it too)
+        "cg_update_kernel": 6 * 8 * k * n_lat,
     }
 
 

@@ -61,9 +61,16 @@ class _State:
     """Energy-like view of the fused iterate for IterationControllers."""
 
     def __init__(self, value, gnorm, lazy):
-        self.value = value
+        self._value = value
         self.gradient_norm = gnorm
         self._lazy = lazy
+
+    @property
+    def value(self):
+        """the energy value (a callable is evaluated on first access)"""
+        if callable(self._value):
+            self._value = self._value()
+        return self._value
 
     @property
     def position(self):
@@ -95,6 +102,14 @@ def _capture(fn):
             g.capture_end()
     cur.wait_stream(_CAPTURE_STREAM)
     return g
+
+
+def _reads_value(ctl):
+    """False for controllers that never look at the energy value
+    (GradientNormController.check without a name,
+    iteration_controllers.py:188-221)."""
+    from .iteration_controllers import GradientNormController
+    return not (type(ctl) is GradientNormController and getattr(ctl, "_name", None) is None)
 
 
 def _worth_capturing(ctl, niter, min_left=4):
@@ -388,13 +403,18 @@ class FusedCGBatch(FusedCG):
         if not active:
             return X, results
 
+        # The update kernel's x.b partial only feeds the energy value; when no
+        # controller reads the value (GradientNormController without a name),
+        # b is not streamed and the value is computed on demand.
+        Bu = Bv if any(_reads_value(c) for c in self.controllers) else None
+
         def body(with_dir):
             s_ = _native.stream_ptr()
             if with_dir:
                 chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), s_))
             core.metric_flat_batch(D, Q, self.W, 0.0)
             chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), s_))
-            chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bv), n, n, k, dt, sh, P(SC), P(ws), s_))
+            chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws), s_))
 
         graph = None
         ii = 0
@@ -423,7 +443,7 @@ class FusedCGBatch(FusedCG):
                 core.metric_flat_batch(D, Q, self.W, 0.0)
                 chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), sp))
                 gp = SC[:, _native.CG_GAMMA].clone()
-                chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bv), n, n, k, dt, sh, P(SC), P(ws), sp))
+                chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws), sp))
                 if AX is None:
                     AX = torch.zeros_like(X)
                 core.metric_flat_batch(X, AX, self.W, 0.0)
@@ -466,7 +486,14 @@ class FusedCGBatch(FusedCG):
                             if "v" not in cache:
                                 cache["v"] = (lay.unpack(X[j].double()), lay.unpack(Rr[j].double()))
                             return cache["v"]
-                        value = 0.5 * (float(hj[_native.CG_XR]) - float(hj[_native.CG_XB]))
+                        xr, xb = float(hj[_native.CG_XR]), float(hj[_native.CG_XB])
+                        if Bu is None and Bv is not None and ii != 0:
+                            # x.b was not accumulated by the update kernel
+                            def value(j=j, xr=xr):
+                                xbj = float(torch.dot(X[j].double(), Bv[j].double()))
+                                return 0.5 * (xr - xbj)
+                        else:
+                            value = 0.5 * (xr - xb)
                         st = ctl.check(_State(value, math.sqrt(gamma), lazy))
                         if st != ctl.CONTINUE:
                             status = st
