@@ -186,34 +186,42 @@ struct FoldShape {
   long long nin, nout;  // elements per pre item
 };
 
-template <typename T>
+// I: index type -- 32-bit when pre * nin < 2^31 (the usual case: cheaper
+// div/mod per element), 64-bit otherwise
+template <typename T, typename I>
 __global__ __launch_bounds__(256) void bin_fold_kernel(const T* __restrict__ in, T* __restrict__ out, FoldShape fs,
                                                        long long pre) {
-  const long long tot = pre * fs.nout;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += stride) {
-    long long r = e % fs.nout;
-    const long long p = e / fs.nout;
-    long long q[FOLD_MAXD], m[FOLD_MAXD];
+  const I tot = (I)(pre * fs.nout), nout = (I)fs.nout, nin = (I)fs.nin;
+  I n[FOLD_MAXD], h[FOLD_MAXD];
+#pragma unroll
+  for (int a = 0; a < FOLD_MAXD; ++a) {
+    n[a] = (I)fs.n[a];
+    h[a] = (I)fs.h[a];
+  }
+  const I stride = (I)gridDim.x * blockDim.x;
+  for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += stride) {
+    I r = e % nout;
+    const I p = e / nout;
+    I q[FOLD_MAXD], m[FOLD_MAXD];
     bool two[FOLD_MAXD];
 #pragma unroll
     for (int a = FOLD_MAXD - 1; a >= 0; --a) {
       if (a < fs.d) {
-        q[a] = r % fs.h[a];
-        r /= fs.h[a];
-        m[a] = fs.n[a] - q[a];
+        q[a] = r % h[a];
+        r /= h[a];
+        m[a] = n[a] - q[a];
         two[a] = q[a] != 0 && m[a] != q[a];
       } else {
         q[a] = m[a] = 0;
         two[a] = false;
       }
     }
-    const T* src = in + p * fs.nin;
+    const T* src = in + p * nin;
     T acc = (T)0;
 #pragma unroll
     for (int s = 0; s < (1 << FOLD_MAXD); ++s) {
       bool ok = true;
-      long long idx = 0;
+      I idx = 0;
 #pragma unroll
       for (int a = 0; a < FOLD_MAXD; ++a) {
         if (a >= fs.d) {
@@ -222,7 +230,7 @@ __global__ __launch_bounds__(256) void bin_fold_kernel(const T* __restrict__ in,
         }
         const bool hi = (s >> (FOLD_MAXD - 1 - a)) & 1;
         ok = ok && (!hi || two[a]);
-        idx = idx * fs.n[a] + (hi ? m[a] : q[a]);
+        idx = idx * n[a] + (hi ? m[a] : q[a]);
       }
       if (ok) acc += src[idx];
     }
@@ -345,16 +353,21 @@ int nft_bin_fold(const void* in, void* out, int64_t pre, int ndim, const int64_t
   const long long tot = pre * fs.nout;
   if (tot <= 0) return NFT_OK;
   prof_mark(stream, "bin_fold");
-  if (dtype == 0)
-    hipLaunchKernelGGL(bin_fold_kernel<double>, dim3(nblocks(tot)), dim3(256), 0, stream, (const double*)in,
-                       (double*)out, fs, (long long)pre);
-  else if (dtype == 1)
-    hipLaunchKernelGGL(bin_fold_kernel<float>, dim3(nblocks(tot)), dim3(256), 0, stream, (const float*)in,
-                       (float*)out, fs, (long long)pre);
-  else {
+  const bool i32 = pre * fs.nin < (1LL << 31) - 65536LL * 256;  // grid-stride increments stay in range
+#define NFT_FOLD(TT, II)                                                                                     \
+  hipLaunchKernelGGL((bin_fold_kernel<TT, II>), dim3(nblocks(tot)), dim3(256), 0, stream, (const TT*)in, \
+                     (TT*)out, fs, (long long)pre)
+  if (dtype == 0) {
+    if (i32) NFT_FOLD(double, unsigned);
+    else NFT_FOLD(double, long long);
+  } else if (dtype == 1) {
+    if (i32) NFT_FOLD(float, unsigned);
+    else NFT_FOLD(float, long long);
+  } else {
     set_last_error("nft_bin_fold: bad dtype");
     return NFT_ERR_ARG;
   }
+#undef NFT_FOLD
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
