@@ -2,6 +2,7 @@
 the geoVI nonlinear sample refinement runs NewtonCG on
 GaussianEnergy(m) @ transformation (kl_energies.py:147-155)."""
 from ..logger import logger
+from . import trace
 from .conjugate_gradient import ConjugateGradient
 from .iteration_controllers import AbsDeltaEnergyController, GradientNormController
 from .line_search import LineSearch
@@ -26,24 +27,31 @@ class DescentMinimizer(Minimizer):
     def serve(self, req):
         """Synchronous evaluation of one request of minimize_gen."""
         if req[0] == "dir":
+            self._trace_sample = req[3]
             return self.get_descent_direction(req[1], req[2])
         return self.line_searcher.serve(req)
 
     def minimize_gen(self, energy):
         """DescentMinimizer.__call__ (descent_minimizers.py:52-108) as a
-        generator of requests: ("dir", energy, f_k_minus_1) -> descent
-        direction, plus the line search's ("dd", ...) / ("at", ...)."""
+        generator of requests: ("dir", energy, f_k_minus_1, sample) -> descent
+        direction, plus the line search's ("dd", ...) / ("at", ...).
+        ``sample`` (energy.sample of the starting energy, if set) only tags
+        the decision trace (minimization/trace.py)."""
         f_k_minus_1 = None
         controller = self._controller
+        stag = getattr(energy, "sample", None)
+        trace.tag(controller, ("newton", stag))
         status = controller.start(energy)
         if status != controller.CONTINUE:
             return energy, status
         while True:
             if energy.gradient_norm == 0:
                 return energy, controller.CONVERGED
-            pk = yield ("dir", energy, f_k_minus_1)
-            new_energy, success = yield from self.line_searcher.perform_line_search_gen(
-                energy=energy, pk=pk, f_k_minus_1=f_k_minus_1)
+            pk = yield ("dir", energy, f_k_minus_1, stag)
+            ls = self.line_searcher.perform_line_search_gen(energy=energy, pk=pk, f_k_minus_1=f_k_minus_1)
+            if trace.active():
+                ls = _traced_trials(ls, stag)
+            new_energy, success = yield from ls
             if not success:
                 self.reset()
             f_k_minus_1 = energy.value
@@ -63,6 +71,30 @@ class DescentMinimizer(Minimizer):
 
     def get_descent_direction(self, energy, old_value=None):
         raise NotImplementedError
+
+
+def _traced_trials(gen, stag):
+    """pass a line-search generator through, recording its trial steps and
+    the energies found there"""
+    trace.emit(("trial", stag), None)
+    trace.emit(("trialE", stag), None)
+    try:
+        req = next(gen)
+        while True:
+            if req[0] == "at":
+                trace.emit(("trial", stag), float(req[2]))
+            try:
+                ans = yield req
+            except Exception as exc:     # noqa: BLE001 -- forwarded to the search
+                req = gen.throw(exc)
+                continue
+            if req[0] == "at":
+                trace.emit(("trialE", stag), float(ans.value))
+            elif req[0] == "dd":
+                trace.emit(("trialD", stag), (float(req[1].value), float(ans)))
+            req = gen.send(ans)
+    except StopIteration as e:
+        return e.value
 
 
 class SteepestDescent(DescentMinimizer):
@@ -90,6 +122,7 @@ class NewtonCG(DescentMinimizer):
         else:
             ediff = self._alpha * (old_value - energy.value)
             ic = AbsDeltaEnergyController(ediff, iteration_limit=self._max_cg_iterations, name=self._name)
+        trace.tag(ic, ("dir", getattr(self, "_trace_sample", None)))
         if self._history is not None:
             ic.enable_logging()
         # CG from x0 = 0: the metric is linear, so A(x0) - b is -b and the

@@ -81,6 +81,11 @@ class _State:
         return self._lazy()[1]
 
 
+def _stale():
+    raise RuntimeError("CG energy value read after its iteration: the fused solve computes it "
+                       "on demand only while the controller checks that iterate")
+
+
 _CAPTURE_STREAM = None
 
 
@@ -106,10 +111,14 @@ def _capture(fn):
 
 def _reads_value(ctl):
     """False for controllers that never look at the energy value
-    (GradientNormController.check without a name,
-    iteration_controllers.py:188-221)."""
+    (GradientNormController.check without a name, without an energy history
+    and with the decision trace off, iteration_controllers.py:188-221).  A
+    subclass may read it in an overridden check, so only the exact class
+    qualifies."""
+    from . import trace
     from .iteration_controllers import GradientNormController
-    return not (type(ctl) is GradientNormController and getattr(ctl, "_name", None) is None)
+    return not (type(ctl) is GradientNormController and getattr(ctl, "_name", None) is None
+                and getattr(ctl, "_history", None) is None and not trace.active())
 
 
 def _worth_capturing(ctl, niter, min_left=4):
@@ -494,7 +503,12 @@ class FusedCGBatch(FusedCG):
                                 return 0.5 * (xr - xbj)
                         else:
                             value = 0.5 * (xr - xb)
-                        st = ctl.check(_State(value, math.sqrt(gamma), lazy))
+                        state = _State(value, math.sqrt(gamma), lazy)
+                        st = ctl.check(state)
+                        if callable(state._value):
+                            # not read during the check: the buffers move on with the
+                            # next iteration, so a later read would see another iterate
+                            state._value = _stale
                         if st != ctl.CONTINUE:
                             status = st
                 if status is not None:

@@ -15,7 +15,7 @@ on its own host floats) -- and their requests are served in batches:
 
   ("at", e, alpha, pk)  value, gradient, |gradient| at e.x + alpha * pk
   ("dd", e, pk)         directional derivative  e.gradient . pk
-  ("dir", e, f_prev)    NewtonCG direction: CG on the sample's metric
+  ("dir", e, f_prev, s) NewtonCG direction: CG on the sample's metric
 
 Energy of a batch X (k, latent) of positions, everything on the device:
 
@@ -490,14 +490,16 @@ class GeoVIBatch:
         from .conjugate_gradient import ConjugateGradient  # noqa: F401
         from .fused_cg import FusedCGBatch, _State
         from .iteration_controllers import AbsDeltaEnergyController, GradientNormController
+        from . import trace
         mz = self.minimizer
         ctls = []
-        for _, (_, e, old) in reqs:
+        for _, (_, e, old, stag) in reqs:
             if old is None:
                 ctls.append(GradientNormController(iteration_limit=5))
             else:
                 ediff = mz._alpha * (old - e.value)
                 ctls.append(AbsDeltaEnergyController(ediff, iteration_limit=mz._max_cg_iterations, name=mz._name))
+            trace.tag(ctls[-1], ("dir", stag))
         states = self.pipe.stack([(r[1].states, r[1].row) for _, r in reqs])
         G = torch.stack([r[1].g for _, r in reqs])
         core = _MetricCore(self.metric_batch(states), self.layout)

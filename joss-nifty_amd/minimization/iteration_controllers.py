@@ -7,6 +7,7 @@ import time
 import numpy as np
 
 from ..logger import logger
+from . import trace as _trace
 
 
 class IterationController:
@@ -67,11 +68,16 @@ class EnergyHistory:
 
 
 def append_history(func):
+    traced = func.__name__ == "check"
+
     @functools.wraps(func)
     def wrapper(self, energy):
         if self._history is not None:
             self._history.append((time.time(), energy.value))
-        return func(self, energy)
+        st = func(self, energy)
+        if traced and _trace.TRACE is not None:
+            _trace.emit(getattr(self, "_trace_tag", None), (self._itcount, float(energy.value)))
+        return st
     return wrapper
 
 

@@ -119,6 +119,7 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
                 pos = sam_position - yi if neg else sam_position + yi
                 en = GaussianEnergy(m) @ transformation
                 en = EnergyAdapter(pos, en, nanisinf=True, want_metric=True)
+                en.sample = i - lo      # tags the decision trace (trace.py) only
                 en, _ = minimizer(en)
                 local_samples.append(en.position - sam_position)
                 local_neg.append(False)

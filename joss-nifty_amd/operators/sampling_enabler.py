@@ -1,5 +1,6 @@
 """SamplingEnabler (src/operators/sampling_enabler.py:24-89): draws from the
 inverse of likelihood + prior metric by CG from a prior sample."""
+from ..minimization import trace
 from ..minimization.conjugate_gradient import ConjugateGradient
 from ..minimization.quadratic_energy import QuadraticEnergy
 from .endomorphic_operator import EndomorphicOperator
@@ -54,11 +55,12 @@ class SamplingEnabler(EndomorphicOperator):
         res = None
         if self._approximation is None and len(todo) > 1:
             from ..minimization.fused_cg import fused_cg_batch_or_none
-            ctls = [copy.deepcopy(self._ic) for _ in todo]
+            ctls = [trace.tag(copy.deepcopy(self._ic), ("lin", j)) for j in todo]
             res = fused_cg_batch_or_none(energies, ctls, ConjugateGradient(self._ic)._nreset)
         if res is None:
             res = []
-            for e in energies:
+            for j, e in zip(todo, energies):
+                trace.tag(self._ic, ("lin", j))
                 inverter = ConjugateGradient(self._ic)
                 if self._approximation is not None:
                     res.append(inverter(e, preconditioner=self._approximation.inverse))

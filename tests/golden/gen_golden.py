@@ -438,6 +438,46 @@ def gen_kl_constants():
     _save("kl32_constants.npz", d)
 
 
+def gen_napprox_probe():
+    """The napprox32 geoVI draw's mirrored sample (seed 43, napprox=3): its
+    line search meets inf energies at alpha = 1 and 0.5, then zooms.  At the
+    zoom's first accepted-side point (alpha_lo ~ 0.0334) the reference's
+    directional derivative (LineEnergy.directional_derivative,
+    line_search.py:68-74) is compared with a central finite difference of its
+    own energies along the same line (h = 1e-7): they disagree by 2.4x, which
+    is what sends the reference's zoom to bisection (line_search.py:309-317)
+    where a consistent derivative gives a cubic step."""
+    from nifty8.minimization import line_search
+    LE = line_search.LineEnergy
+    zero = []
+    orig_init = LE.__init__
+
+    def init(self, line_position, energy, line_direction, offset=0.):
+        orig_init(self, line_position, energy, line_direction, offset)
+        if line_position == 0.0 and offset == 0.0:
+            zero.append(self)
+    LE.__init__ = init
+    try:
+        _, lh, data, _, pos = _gaussian_problem(32)
+        H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=6))
+        mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=1))
+        ift.random.push_sseq_from_seed(43)
+        ift.minimization.kl_energies.draw_samples(pos, H, mini, 1, True, napprox=3)
+        ift.random.pop_sseq()
+    finally:
+        LE.__init__ = orig_init
+    le0 = zero[-1]          # the mirrored sample's (last) line search
+    d = {}
+    alphas = np.array([0.0, 0.03336566092948427])
+    h = 1e-7
+    d["alpha"] = alphas
+    d["dd"] = np.array([le0.at(a).directional_derivative if a else le0.directional_derivative for a in alphas])
+    d["fd"] = np.array([(le0.at(a + h).value - le0.at(a - h).value) / (2 * h) for a in alphas])
+    d["value"] = np.array([le0.at(a).value if a else le0.value for a in alphas])
+    print("napprox probe: alpha", alphas, "dd", d["dd"], "fd", d["fd"])
+    _save("napprox32_probe.npz", d)
+
+
 def gen_napprox():
     """draw_samples with the napprox diagonal preconditioner
     (kl_energies.py:127-128, probing.py:142-152): MGVI and geoVI on the 32^2
@@ -472,6 +512,269 @@ def gen_napprox():
     for k, v in _flat(diag).items():
         d["diag_" + k] = v
     _save("napprox32.npz", d)
+
+
+class _Tracer:
+    """Records the decisions of one draw_samples call of the reference by
+    wrapping (in this process only) ConjugateGradient.__call__ (every
+    controller check: iteration number and energy value),
+    DescentMinimizer.__call__ (one NewtonCG refinement per sample) and
+    LineEnergy.at (every trial step of the line search).
+
+    events[s] for refinement sample s (draw order):
+      "lin"   energies of the linear sampling CG that produced its pair
+      "newton" energies at the outer controller checks
+      "dir"   list (per Newton step) of inner-CG energy lists
+      "trial" list (per Newton step) of line-search trial step sizes"""
+
+    def __init__(self, lin_ctl):
+        from nifty8.minimization import conjugate_gradient, descent_minimizers, line_search
+        self.mods = (conjugate_gradient.ConjugateGradient, descent_minimizers.DescentMinimizer,
+                     line_search.LineEnergy)
+        self.lin_ctl = lin_ctl
+        self.lin = []          # one energy list per linear solve
+        self.samples = []      # one dict per refinement
+        self.orig = None
+
+    def __enter__(self):
+        CG, DM, LE = self.mods
+        self.orig = (CG.__call__, DM.__call__, LE.at)
+        cg_call, dm_call, le_at = self.orig
+        tr = self
+
+        def _watch(ctl, sink):
+            chk = ctl.check
+
+            def check(energy):
+                st = chk(energy)
+                sink.append(float(energy.value))
+                return st
+            ctl.check = check
+            return chk
+
+        def cg(self_, energy, preconditioner=None):
+            ctl = self_._controller
+            sink = []
+            if ctl is tr.lin_ctl:
+                tr.lin.append(sink)
+            else:
+                s = tr.samples[-1]
+                s["dir"].append(sink)
+                s["trial"].append([])
+                s["trialE"].append([])
+            chk = _watch(ctl, sink)
+            try:
+                return cg_call(self_, energy, preconditioner)
+            finally:
+                ctl.check = chk
+
+        def dm(self_, energy):
+            s = {"lin": len(tr.lin) - 1, "newton": [], "dir": [], "trial": [], "trialE": []}
+            tr.samples.append(s)
+            chk = _watch(self_._controller, s["newton"])
+            try:
+                return dm_call(self_, energy)
+            finally:
+                self_._controller.check = chk
+
+        def at(self_, line_position):
+            res = le_at(self_, line_position)
+            if tr.samples and tr.samples[-1]["trial"]:
+                tr.samples[-1]["trial"][-1].append(float(line_position))
+                try:
+                    v = float(res.value)
+                except FloatingPointError:
+                    v = np.nan
+                tr.samples[-1]["trialE"][-1].append(v)
+            return res
+
+        CG.__call__, DM.__call__, LE.at = cg, dm, at
+        return self
+
+    def __exit__(self, *a):
+        CG, DM, LE = self.mods
+        CG.__call__, DM.__call__, LE.at = self.orig
+
+
+def _pad(lists, fill=np.nan):
+    """ragged lists -> 2-D array padded with `fill` (nan; inf where the
+    values themselves may be nan)"""
+    n = max([len(x) for x in lists] + [1])
+    out = np.full((len(lists), n), fill)
+    for i, x in enumerate(lists):
+        out[i, :len(x)] = x
+    return out
+
+
+def _los_problem(n=64, nlos=300):
+    pos_space = ift.RGSpace((n, n))
+    cf = ift.SimpleCorrelatedField(pos_space, **CF_ARGS)
+    signal = ift.sigmoid(cf)
+    ift.random.push_sseq_from_seed(27)
+    rng = ift.random.current_rng()
+    starts = rng.random((nlos, 2)).T
+    ends = rng.random((nlos, 2)).T
+    R = ift.LOSResponse(pos_space, starts=list(starts), ends=list(ends))
+    sr = R(signal)
+    N = ift.ScalingOperator(R.target, 1e-3, np.float64)
+    mock = ift.from_random(sr.domain, "normal")
+    data = sr(mock) + N.draw_sample()
+    pos = 0.1 * ift.from_random(sr.domain, "normal")
+    ift.random.pop_sseq()
+    lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ sr
+    return lh, pos, {"starts": starts, "ends": ends, "data": data.val}
+
+
+class _FFTNoise:
+    """Context: every Hartley transform of the reference's operators
+    (harmonic_operators.py:27,211) returns its output times
+    (1 + 2^-52 N(0, 1)) elementwise -- the rounding of another, equally
+    valid FFT implementation (the build's kernels round differently from
+    pocketfft in every matvec, not once at the start)."""
+
+    def __init__(self, seed):
+        self.rng = np.random.default_rng(seed)
+
+    def __enter__(self):
+        from nifty8.operators import harmonic_operators as ho
+        self.ho, self.orig = ho, ho.hartley
+        rng, orig = self.rng, self.orig
+
+        def hartley(a, axes=None):
+            out = orig(a, axes=axes)
+            return out * (1 + 2.0**-52 * rng.standard_normal(out.shape))
+        ho.hartley = hartley
+        return self
+
+    def __exit__(self, *a):
+        self.ho.hartley = self.orig
+
+
+def _perturbed(pos):
+    """three last-bit perturbations of a draw: xi scaled by 1 + 1e-15, and
+    two runs with rounding-level noise on every Hartley transform
+    (_FFTNoise seeds 1, 2).  Returns [(position, context)]."""
+    import contextlib
+    p1 = ift.MultiField.from_dict({k: (v * (1 + 1e-15) if k == "xi" else v) for k, v in pos.items()})
+    return [(p1, contextlib.nullcontext()), (pos, _FFTNoise(1)), (pos, _FFTNoise(2))]
+
+
+def _sens(sl, perturbed, pos):
+    """largest relative change of any residual sample over the perturbed runs"""
+    return max(np.linalg.norm(b[k].val - a[k].val) / max(np.linalg.norm(a[k].val), 1e-300)
+               for slp in perturbed for a, b in zip(sl._r, slp._r) for k in pos.keys())
+
+
+GEOVI_TRACE_CASES = {
+    # geovi32.npz: the demo NewtonCG with the AbsDelta inner-CG branch
+    "g32": dict(problem="gauss32", seed=27, nsamp=1, lin=("absdelta", 0.05, 100),
+                newton=("absdelta", 0.5, 2, 5), max_cg=200),
+    # the bench chain (sigmoid o LOS) with the bench's controllers, 2 pairs
+    "bench64": dict(problem="los64", seed=1000, nsamp=2, lin=("gradnorm", 100),
+                    newton=("gradnorm", 2), max_cg=50),
+    # four Newton steps: three AbsDeltaEnergyController(0.1 dE) inner solves
+    "newton64": dict(problem="los64", seed=1002, nsamp=1, lin=("gradnorm", 100),
+                     newton=("gradnorm", 4), max_cg=50),
+    # napprox32.npz's geoVI draw (napprox=3 preconditioner)
+    "napprox32": dict(problem="gauss32", seed=43, nsamp=1, lin=("gradnorm", 6),
+                      newton=("gradnorm", 1), max_cg=200, napprox=3),
+    # the demo controllers of SURVEY §8(d) on the same chain
+    "demo64": dict(problem="los64", seed=1001, nsamp=2, lin=("absdelta", 0.05, 100),
+                   newton=("absdelta", 0.5, 2, 15), max_cg=200),
+}
+
+
+def _ctl(spec):
+    if spec[0] == "gradnorm":
+        return ift.GradientNormController(iteration_limit=spec[1])
+    if len(spec) == 3:
+        return ift.AbsDeltaEnergyController(deltaE=spec[1], iteration_limit=spec[2])
+    return ift.AbsDeltaEnergyController(deltaE=spec[1], convergence_level=spec[2], iteration_limit=spec[3])
+
+
+def gen_geovi_trace():
+    """Multi-step geoVI draws with every controller decision recorded
+    (descent_minimizers.py:52-108,187-206, iteration_controllers.py:356-423,
+    line_search.py:147-250): per sample the linear CG energies, the Newton
+    outer energies, every inner-CG energy (first step GradientNormController(5),
+    later steps the AbsDeltaEnergyController(0.1 dE) branch) and the line
+    search's trial step sizes.  Each case is also run under three last-bit
+    perturbations (_perturbed): the reference's own sensitivity."""
+    d = {}
+    for name, c in GEOVI_TRACE_CASES.items():
+        if c["problem"] == "gauss32":
+            _, lh, data, _, pos = _gaussian_problem(32)
+            d[name + "_data"] = data.val
+        else:
+            lh, pos, extra = _los_problem()
+            for k, v in extra.items():
+                d[f"{name}_{k}"] = v
+        for k, v in _flat(pos).items():
+            d[f"{name}_pos_{k}"] = v
+        runs = []
+        import contextlib
+        for p, ctx in [(pos, contextlib.nullcontext())] + _perturbed(pos):
+            ic = _ctl(c["lin"])
+            H = ift.StandardHamiltonian(lh, ic)
+            mini = ift.NewtonCG(_ctl(c["newton"]), max_cg_iterations=c["max_cg"])
+            ift.random.push_sseq_from_seed(c["seed"])
+            with _Tracer(ic) as tr, ctx:
+                sl = ift.minimization.kl_energies.draw_samples(p, H, mini, c["nsamp"], True,
+                                                               napprox=c.get("napprox", 0))
+            ift.random.pop_sseq()
+            runs.append((sl, tr))
+        (sl, tr), pruns = runs[0], runs[1:]
+        d[name + "_sens"] = np.array(_sens(sl, [r[0] for r in pruns], pos))
+        d[name + "_nsamples"] = np.array(len(sl._r))
+        for i, r in enumerate(sl._r):
+            for k, v in _flat(r).items():
+                d[f"{name}_r{i}_{k}"] = v
+        # the unperturbed trace ("") and the perturbed ones ("p1_" ...): the
+        # tests hold the build to the reference where the reference agrees
+        # with itself
+        for pre, t_ in [("", tr)] + [(f"p{j + 1}_", r[1]) for j, r in enumerate(pruns)]:
+            d[f"{name}_{pre}lin"] = _pad(t_.lin)
+            for i, s in enumerate(t_.samples):
+                t = f"{name}_{pre}s{i}_"
+                d[t + "lin"] = np.array(s["lin"])
+                d[t + "newton"] = np.array(s["newton"])
+                d[t + "dir"] = _pad(s["dir"])
+                d[t + "trial"] = _pad(s["trial"])
+                d[t + "trialE"] = _pad(s["trialE"], fill=np.inf)
+            print(name, pre or "base", "linear CG checks", [len(x) for x in t_.lin],
+                  "newton checks", [len(s["newton"]) for s in t_.samples],
+                  "inner CG checks", [[len(x) for x in s["dir"]] for s in t_.samples])
+        d[name + "_nperturbed"] = np.array(len(pruns))
+        print(name, "sens", float(d[name + "_sens"]))
+    _save("geovi_trace.npz", d)
+
+
+def gen_mgvi_absdelta_trace():
+    """The mgvi128.npz "absdelta" draw (AbsDeltaEnergyController(0.05,
+    iteration_limit=100), 128^2, seed 27, 2 mirrored pairs) with the energy of
+    every linear-CG check, unperturbed and under three last-bit perturbations
+    (_perturbed): the reference's own spread, which bounds the tests."""
+    cf, lh, data, mock, pos = _gaussian_problem(128)
+    d = {}
+    runs = []
+    import contextlib
+    for p, ctx in [(pos, contextlib.nullcontext())] + _perturbed(pos):
+        ic = ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=100)
+        H = ift.StandardHamiltonian(lh, ic)
+        ift.random.push_sseq_from_seed(27)
+        with _Tracer(ic) as tr, ctx:
+            sl = ift.minimization.kl_energies.draw_samples(p, H, None, 2, True)
+        ift.random.pop_sseq()
+        runs.append((sl, tr))
+    (sl, tr), pruns = runs[0], runs[1:]
+    d["sens"] = np.array(_sens(sl, [r[0] for r in pruns], pos))
+    d["lin"] = _pad(tr.lin)
+    for j, r in enumerate(pruns):
+        d[f"p{j + 1}_lin"] = _pad(r[1].lin)
+    d["nperturbed"] = np.array(len(pruns))
+    print("mgvi absdelta: checks", [len(x) for x in tr.lin], [[len(x) for x in r[1].lin] for r in pruns],
+          "sens", float(d["sens"]))
+    _save("mgvi128_absdelta_trace.npz", d)
 
 
 if __name__ == "__main__":
