@@ -606,6 +606,23 @@ def _pad(lists, fill=np.nan):
     return out
 
 
+def _cube_problem(n=16):
+    pos_space = ift.RGSpace((n, n, n))
+    cf = ift.SimpleCorrelatedField(pos_space, **dict(CF_ARGS, asperity=None))
+    R = ift.GeometryRemover(pos_space)
+    sr = R @ cf
+    # noise variance 1: the 100-step linear solve converges (at 0.01 it is
+    # chaotic from the 16th step on, as the 2-D GeometryRemover cases)
+    N = ift.ScalingOperator(R.target, 1.0, np.float64)
+    ift.random.push_sseq_from_seed(29)
+    mock = ift.from_random(sr.domain, "normal")
+    data = sr(mock) + N.draw_sample()
+    pos = 0.1 * ift.from_random(sr.domain, "normal")
+    ift.random.pop_sseq()
+    lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ sr
+    return lh, pos, data
+
+
 def _los_problem(n=64, nlos=300):
     pos_space = ift.RGSpace((n, n))
     cf = ift.SimpleCorrelatedField(pos_space, **CF_ARGS)
@@ -675,6 +692,10 @@ GEOVI_TRACE_CASES = {
     # four Newton steps: three AbsDeltaEnergyController(0.1 dE) inner solves
     "newton64": dict(problem="los64", seed=1002, nsamp=1, lin=("gradnorm", 100),
                      newton=("gradnorm", 4), max_cg=50),
+    # 3-D: 16^3 CorrelatedField (no asperity), GeometryRemover Gaussian --
+    # the 3-D bin fold and the lowered Newton metric at d = 3
+    "cube16": dict(problem="cube16", seed=1003, nsamp=2, lin=("gradnorm", 100),
+                   newton=("gradnorm", 2), max_cg=50),
     # napprox32.npz's geoVI draw (napprox=3 preconditioner)
     "napprox32": dict(problem="gauss32", seed=43, nsamp=1, lin=("gradnorm", 6),
                       newton=("gradnorm", 1), max_cg=200, napprox=3),
@@ -704,6 +725,9 @@ def gen_geovi_trace():
     for name, c in GEOVI_TRACE_CASES.items():
         if c["problem"] == "gauss32":
             _, lh, data, _, pos = _gaussian_problem(32)
+            d[name + "_data"] = data.val
+        elif c["problem"] == "cube16":
+            lh, pos, data = _cube_problem()
             d[name + "_data"] = data.val
         else:
             lh, pos, extra = _los_problem()

@@ -197,3 +197,75 @@ def test_c5_fp32_mixed_precision_cg(ift, shape):
         err = float(torch.linalg.vector_norm(a - r) / torch.linalg.vector_norm(r))
         assert err < 1e-4, (k, err)
     assert abs(res["fp32"].value - res["fp64"].value) < 1e-4 * abs(res["fp64"].value)
+
+
+def _kl_checks(ift, sl, H, n):
+    assert sl.n_samples == n and len(sl._r) == n
+    for r in sl._r:
+        for k in r.keys():
+            assert bool(torch.all(torch.isfinite(r[k].val))), k
+    kl = ift.SampledKLEnergyClass(sl, H, [], None, True)
+    assert np.isfinite(kl.value)
+    for k in kl.gradient.keys():
+        assert bool(torch.all(torch.isfinite(kl.gradient[k].val))), k
+    return kl
+
+
+def test_c4_geovi_draw_512(ift):
+    """C4's per-GPU share (n_samples=16 mirrored over 8 GPUs: 2 pairs) as a
+    geoVI draw at 512^3: linear CG 10 steps, one Newton step (inner CG 5),
+    batched refinement of the 4 samples; finite samples, the two members of a
+    pair start mirrored about the expansion point, finite KL value and
+    gradient."""
+    cf, lh, pos = _gauss_problem(ift, (512, 512, 512))
+    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=10))
+    mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=1))
+    ift.random.push_sseq_from_seed(12)
+    sl = ift.draw_samples(pos, H, mini, 2, True)
+    ift.random.pop_sseq()
+    _kl_checks(ift, sl, H, 4)
+    # the refinement moves the mirrored starts only a little: the pair stays
+    # roughly antisymmetric about the expansion point
+    for a, b in ((0, 1), (2, 3)):
+        ra, rb = sl._r[a]["xi"].val, sl._r[b]["xi"].val
+        asym = float(torch.linalg.vector_norm(ra + rb) / torch.linalg.vector_norm(ra - rb))
+        assert asym < 0.5, asym
+
+
+def test_c5_geovi_draw_4096_fp32(ift):
+    """C5's per-GPU share (n_samples=32 mirrored over 8 GPUs: 4 pairs) as a
+    geoVI draw at 4096^2 with fp32 CG storage (config.set_cg_precision("fp32"),
+    fp64 reductions): finite samples and KL, and every sample within rtol
+    1e-4 of the same draw in fp64 (BASELINE.json C5)."""
+    from nifty_amd import config
+    cf, lh, pos = _gauss_problem(ift, (4096, 4096))
+    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=8))
+    out = {}
+    for prec in ("fp64", "fp32"):
+        config.set_cg_precision(prec)
+        try:
+            mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=1))
+            ift.random.push_sseq_from_seed(13)
+            sl = ift.draw_samples(pos, H, mini, 4, True)
+            ift.random.pop_sseq()
+        finally:
+            config.set_cg_precision("fp64")
+        out[prec] = _kl_checks(ift, sl, H, 8)
+    from nifty_amd.minimization import geovi_batch
+    p64 = [out["fp64"].samples.local_item(i) for i in range(8)]
+    p32 = [out["fp32"].samples.local_item(i) for i in range(8)]
+    for i, (a, b) in enumerate(zip(p32, p64)):
+        va = torch.cat([a[k].val.reshape(-1) for k in a.keys()])
+        vb = torch.cat([b[k].val.reshape(-1) for k in b.keys()])
+        err = float(torch.linalg.vector_norm(va - vb) / torch.linalg.vector_norm(vb))
+        assert err < 1e-4, (i, err)
+    # the KL value (2.9e8, dominated by the data misfit at noise 0.01) moves
+    # with the samples: its fp32 - fp64 change equals the first-order
+    # prediction mean_i grad H(s_i) . (s32_i - s64_i) up to 5 % + 1e-9 KL
+    v64, g64 = geovi_batch.kl_batch(H, p64)
+    v32, _ = geovi_batch.kl_batch(H, p32)
+    pred = np.mean([sum(float(torch.sum(g[k].val * (a[k].val - b[k].val))) for k in g.keys())
+                    for g, a, b in zip(g64, p32, p64)])
+    d = float(np.mean(v32) - np.mean(v64))
+    assert abs(d - pred) <= 0.05 * abs(pred) + 1e-9 * abs(np.mean(v64)), (d, pred)
+    assert abs(out["fp32"].value - float(np.mean(v32))) <= 1e-12 * abs(out["fp32"].value)

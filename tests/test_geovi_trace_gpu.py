@@ -43,6 +43,8 @@ CASES = {
     # four Newton steps: three AbsDeltaEnergyController(0.1 dE) inner solves
     "newton64": dict(problem="los64", seed=1002, nsamp=1, lin=("gradnorm", 100),
                      newton=("gradnorm", 4), max_cg=50),
+    "cube16": dict(problem="cube16", seed=1003, nsamp=2, lin=("gradnorm", 100),
+                   newton=("gradnorm", 2), max_cg=50),
     # sample 1's zoom step 8 follows the reference's inconsistent directional
     # derivative (napprox32_probe.npz, test_napprox_reference_derivative_defect)
     "napprox32": dict(problem="gauss32", seed=43, nsamp=1, lin=("gradnorm", 6),
@@ -78,6 +80,12 @@ def _problem(ift, G, name):
         cf = ift.SimpleCorrelatedField(sp, **CF_ARGS)
         R = ift.GeometryRemover(sp)
         N = ift.ScalingOperator(R.target, 0.01, np.float64)
+        lh = ift.GaussianEnergy(ift.makeField(R.target, G[name + "_data"]), inverse_covariance=N.inverse) @ (R @ cf)
+    elif c["problem"] == "cube16":
+        sp = ift.RGSpace((16, 16, 16))
+        cf = ift.SimpleCorrelatedField(sp, **dict(CF_ARGS, asperity=None))
+        R = ift.GeometryRemover(sp)
+        N = ift.ScalingOperator(R.target, 1.0, np.float64)
         lh = ift.GaussianEnergy(ift.makeField(R.target, G[name + "_data"]), inverse_covariance=N.inverse) @ (R @ cf)
     else:
         sp = ift.RGSpace((64, 64))
