@@ -13,6 +13,8 @@ import numpy as np
 
 from .. import random, utilities
 from ..linearization import Linearization
+from ..field import Field
+from ..multi_domain import MultiDomain
 from ..multi_field import MultiField
 from ..operators.energy_operators import GaussianEnergy, StandardHamiltonian
 from ..operators.sampling_enabler import SamplingEnabler
@@ -222,10 +224,16 @@ class SampledKLEnergyClass(Energy):
         kb = None
         if isinstance(sample_list._m, MultiField) and len(constants) == 0:
             kb = geovi_batch.kl_batch(hamiltonian, list(sample_list.local_iterator()))
+        dom = self.position.domain
+
+        def template():
+            # a rank without samples joins the one all-reduce with zeros
+            from ..multi_field import MultiField
+            return 0.0, (MultiField.full(dom, 0.) if isinstance(dom, MultiDomain) else Field.full(dom, 0.))
         if kb is not None:
-            self._val, self._grad = sample_list._average_results(list(zip(*kb)))
+            self._val, self._grad = sample_list._average_results(list(zip(*kb)), template)
         else:
-            self._val, self._grad = sample_list._average_tuple(_func)
+            self._val, self._grad = sample_list._average_tuple(_func, template)
         if np.isnan(self._val) and self._nanisinf:
             self._val = np.inf
 

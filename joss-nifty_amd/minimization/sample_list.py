@@ -1,8 +1,10 @@
 """ResidualSampleList: latent mean + (possibly distributed) residual samples
 (src/minimization/sample_list.py:42-531, averaging :285-341).
 
-Averages over samples use the deterministic pairwise sum of
-utilities.allreduce_sum (bit-identical for any number of ranks)."""
+Averages over samples: per rank the reference's pairwise order, across ranks
+ONE all-reduce of a packed buffer (utilities.allreduce_sum), or the
+reference's global pairwise tree over point-to-point messages in
+deterministic mode (bit-identical for any number of ranks)."""
 import numpy as np
 
 from .. import utilities
@@ -20,10 +22,12 @@ class ResidualSampleList:
         ntask, rank, _ = utilities.get_MPI_params_from_comm(comm)
         self._nlocal = len(self._r)
         if comm is None:
+            self._counts = None
             self._ntotal = self._nlocal
             self._lo = 0
         else:
-            counts = comm.allgather(self._nlocal)
+            counts = [int(c) for c in comm.allgather(self._nlocal)]
+            self._counts = counts
             self._ntotal = int(sum(counts))
             self._lo = int(sum(counts[:rank]))
 
@@ -65,23 +69,31 @@ class ResidualSampleList:
         for s in self.local_iterator():
             yield s if op is None else op(s)
 
-    def _average_tuple(self, func):
+    def _average_tuple(self, func, template=None):
         """Average a tuple-valued function over all samples (sample_list.py:312-341)."""
-        return self._average_results([func(s) for s in self.local_iterator()])
+        return self._average_results([func(s) for s in self.local_iterator()], template)
 
-    def _average_results(self, res):
-        """The reduction of _average_tuple on precomputed per-sample tuples."""
+    def _average_results(self, res, template=None):
+        """The reduction of _average_tuple on precomputed per-sample tuples:
+        per rank the pairwise sum of every tuple element, then ONE all-reduce
+        of all elements packed into one buffer (utilities.allreduce_sum).  A
+        rank without samples contributes zeros of ``template()``'s layout
+        (the reference splits off an active communicator instead and
+        broadcasts, sample_list.py:62-70,327-341)."""
         n = self._ntotal
-        out = []
-        for k in range(len(res[0]) if res else 0):
-            vals = [r[k] for r in res]
-            tot = utilities.allreduce_sum(vals, self._comm)
-            out.append(tot / n)
-        return tuple(out)
+        if self._comm is None and not res:
+            return None
+        tot = utilities.allreduce_sum([tuple(r) for r in res], self._comm, counts=self._counts,
+                                      template=template)
+        return tuple(t / n for t in tot)
 
     def average(self, op=None):
         res = [op(s) if op is not None else s for s in self.local_iterator()]
-        return utilities.allreduce_sum(res, self._comm) / self._ntotal
+
+        def template():
+            # a rank without samples: the layout of op's result
+            return 0 * (op(self._m) if op is not None else self._m)
+        return utilities.allreduce_sum(res, self._comm, counts=self._counts, template=template) / self._ntotal
 
     def at(self, mean):
         """sample_list.py:489-507: only the keys present in ``mean`` are

@@ -72,11 +72,28 @@ class TorchComm:
         self._dist.all_reduce(t, group=self._group)
         return t
 
+    def _global(self, r):
+        return r if self._group is None else self._dist.get_global_rank(self._group, r)
+
+    def send_tensor(self, t, dest):
+        self._dist.send(t.contiguous(), self._global(dest), group=self._group)
+
+    def recv_tensor_(self, t, source):
+        self._dist.recv(t, self._global(source), group=self._group)
+        return t
+
+    def broadcast_tensor_(self, t, root):
+        self._dist.broadcast(t, self._global(root), group=self._group)
+        return t
+
 
 def pairwise_sum(vals):
     """The fixed pairwise summation order of allreduce_sum
-    (src/utilities.py:374-387) for a local list."""
+    (src/utilities.py:374-387) for a local list.  Tuples are summed
+    element by element."""
     vals = list(vals)
+    if vals and isinstance(vals[0], tuple):
+        return tuple(pairwise_sum(col) for col in zip(*vals))
     n = len(vals)
     step = 1
     while step < n:
@@ -92,9 +109,21 @@ DETERMINISTIC_ALLREDUCE = False
 
 
 def _flatten(obj):
-    """object -> (list of tensors, rebuild function) for Field/MultiField/scalars"""
+    """object -> (list of tensors, rebuild function) for Field / MultiField /
+    scalars / torch tensors and tuples of them"""
     from .field import Field
     from .multi_field import MultiField
+    if isinstance(obj, tuple):
+        parts = [_flatten(o) for o in obj]
+        sizes = [len(ts) for ts, _ in parts]
+
+        def rebuild(ts):
+            out, off = [], 0
+            for (_, rb), n in zip(parts, sizes):
+                out.append(rb(ts[off:off + n]))
+                off += n
+            return tuple(out)
+        return [t for ts, _ in parts for t in ts], rebuild
     if isinstance(obj, MultiField):
         return [f.val for f in obj.values()], lambda ts: MultiField(
             obj.domain, tuple(Field(d, t) for d, t in zip(obj.domain.values(), ts)))
@@ -107,41 +136,113 @@ def _flatten(obj):
     raise TypeError(f"cannot all-reduce {type(obj)}")
 
 
-def allreduce_sum(obj, comm, deterministic=None):
+class _Packed:
+    """one object (Field / MultiField / scalar / tuple of them) as ONE flat
+    fp64 buffer on the collective's device, and back"""
+
+    def __init__(self, obj, comm):
+        self.ts, self.rebuild = _flatten(obj)
+        self.dev = _comm_device(comm, self.ts[0].device)
+        self.buf = torch.cat([t.reshape(-1).to(self.dev, torch.float64) for t in self.ts])
+
+    def zeros(self):
+        return torch.zeros_like(self.buf)
+
+    def unpack(self, buf):
+        out, off = [], 0
+        for t in self.ts:
+            n = t.numel()
+            out.append(buf[off:off + n].reshape(t.shape).to(t.device, t.dtype))
+            off += n
+        return self.rebuild(out)
+
+
+def _comm_device(comm, dev):
+    """gloo runs its collectives on host tensors, RCCL ("nccl") on the GPU"""
+    backend = getattr(comm, "backend", "gloo")
+    if backend == "nccl":
+        if dev.type != "cuda":
+            from . import config
+            return config.device()
+        return dev
+    return torch.device("cpu")
+
+
+def allreduce_sum(obj, comm, deterministic=None, counts=None, template=None):
     """Sum of a list of per-sample objects held by the ranks
-    (src/utilities.py:331-390).
+    (src/utilities.py:331-390).  Items may be Fields, MultiFields, scalars or
+    tuples of them (summed element by element).
 
     Serial: the reference's pairwise tree.  Distributed, default: each rank
-    sums its samples in pairwise order, then ONE all-reduce over a packed
-    fp64 buffer (RCCL over xGMI on the GPU box).  ``deterministic=True``
-    (or DETERMINISTIC_ALLREDUCE): every rank gathers all per-sample objects
-    and evaluates the reference's global tree, bit-identical for any number
-    of ranks (test_mpi/test_kl.py semantics)."""
+    sums its samples in pairwise order, then ONE all-reduce of a packed fp64
+    buffer (RCCL over xGMI on the GPU box).  ``deterministic=True`` (or
+    DETERMINISTIC_ALLREDUCE): the reference's global pairwise tree over the
+    ranks with point-to-point send/recv of packed buffers and a final
+    broadcast -- bit-identical to the serial sum for any number of ranks
+    (test_mpi/test_kl.py semantics).
+
+    ``counts``: the per-rank item counts if known (else one allgather).
+    A rank holding no items needs ``template()``, a zero object of the
+    result's layout (the reference instead splits off an active
+    communicator, sample_list.py:62-70)."""
     vals = list(obj)
     if comm is None:
         return pairwise_sum(vals)
     if deterministic is None:
         deterministic = DETERMINISTIC_ALLREDUCE
+    if counts is None:
+        counts = comm.allgather(len(vals))
+    counts = [int(c) for c in counts]
+    if sum(counts) == 0:
+        raise ValueError("allreduce_sum over no items at all")
     if deterministic:
-        allvals = comm.allgather(vals)
-        flat = [v for lst in allvals for v in lst]
-        return pairwise_sum(flat)
-    if len(vals) == 0:
-        raise RuntimeError("every rank needs at least one sample for the fast all-reduce")
-    local = pairwise_sum(vals)
-    ts, rebuild = _flatten(local)
-    dev = ts[0].device
-    if getattr(comm, "backend", "gloo") == "nccl" and dev.type != "cuda":
-        from . import config
-        dev = config.device()
-    buf = torch.cat([t.reshape(-1).to(dev, torch.float64) for t in ts])
+        return _tree_sum(vals, comm, counts, template)
+    if vals:
+        pk = _Packed(pairwise_sum(vals), comm)
+        buf = pk.buf
+    else:
+        if template is None:
+            raise RuntimeError("a rank without items needs a template of the result layout")
+        pk = _Packed(template(), comm)
+        buf = pk.zeros()
     comm.allreduce_tensor_(buf)
-    out, off = [], 0
-    for t in ts:
-        n = t.numel()
-        out.append(buf[off:off + n].reshape(t.shape).to(t.device, t.dtype))
-        off += n
-    return rebuild(out)
+    return pk.unpack(buf)
+
+
+def _tree_sum(vals, comm, counts, template):
+    """allreduce_sum's pairwise tree (src/utilities.py:358-390) with the items
+    as packed fp64 buffers: who[j] holds item j; at distance `step` the
+    holder of j + step sends its partial sum to the holder of j (a local add
+    when both are on one rank); the total ends on who[0] and is broadcast."""
+    rank = comm.Get_rank()
+    hi = list(np.cumsum(counts))
+    lo = [0] + hi[:-1]
+    nobj = hi[-1]
+    who = [t for t, (a, b) in enumerate(zip(lo, hi)) for _ in range(b - a)]
+    mine = [_Packed(v, comm) for v in vals]
+    like = mine[0] if mine else _Packed(template(), comm)
+    bufs = [None] * nobj
+    for i, p in enumerate(mine):
+        bufs[lo[rank] + i] = p.buf
+    step = 1
+    while step < nobj:
+        for j in range(0, nobj, 2 * step):
+            if j + step < nobj:
+                if rank == who[j]:
+                    if who[j] == who[j + step]:
+                        bufs[j] = bufs[j] + bufs[j + step]
+                    else:
+                        other = like.zeros()
+                        comm.recv_tensor_(other, who[j + step])
+                        bufs[j] = bufs[j] + other
+                    bufs[j + step] = None
+                elif rank == who[j + step]:
+                    comm.send_tensor(bufs[j + step], who[j])
+                    bufs[j + step] = None
+        step *= 2
+    out = bufs[0] if rank == who[0] else like.zeros()
+    comm.broadcast_tensor_(out, who[0])
+    return like.unpack(out)
 
 
 def check_MPI_equality(obj, comm, hash_=False):

@@ -71,6 +71,33 @@ def _worker(rank, world, port, q):
         val, grad = sl._average_tuple(lambda s: (float(np.asarray(s["b"])), s))
         res["tuple"] = (val, {k: np.asarray(grad[k]) for k in dom.keys()})
         res["bcast"] = comm.bcast(rank * 7 + 3, root=0)
+        # ONE collective per KL value + gradient mean (sample_list._average_results)
+        calls = []
+        orig = comm.allreduce_tensor_
+        comm.allreduce_tensor_ = lambda t: (calls.append(t.numel()), orig(t))[1]
+        sl._average_tuple(lambda s: (float(np.asarray(s["b"])), s))
+        comm.allreduce_tensor_ = orig
+        res["ncoll"] = len(calls)
+        # a rank without samples (reference: the _active_comm split,
+        # sample_list.py:62-70): rank 1 holds none of the 3 samples
+        few = vals[:3] if rank == 0 else []
+        sl0 = ift.ResidualSampleList(mean, few, [False] * len(few), comm)
+        assert sl0.n_samples == 3
+        zero = lambda: (0.0, 0 * mean)  # noqa: E731
+        for det in (False, True):
+            utilities.DETERMINISTIC_ALLREDUCE = det
+            v0, g0 = sl0._average_tuple(lambda s: (float(np.asarray(s["b"])), s), zero)
+            a0 = sl0.average()
+            res[f"empty{int(det)}"] = (v0, {k: np.asarray(g0[k]) for k in dom.keys()},
+                                       {k: np.asarray(a0[k]) for k in dom.keys()})
+        utilities.DETERMINISTIC_ALLREDUCE = False
+        # the deterministic tree with uneven splits: every split of 10 items
+        dets = {}
+        for n0 in (0, 1, 4, 7, 10):
+            mine = vals[:n0] if rank == 0 else vals[n0:]
+            t = utilities.allreduce_sum(mine, comm, deterministic=True, template=lambda: 0 * mean)
+            dets[n0] = {k: np.asarray(t[k]) for k in dom.keys()}
+        res["dets"] = dets
         comm.Barrier()
         dist.destroy_process_group()
         q.put((rank, res))
@@ -134,3 +161,44 @@ def test_sample_list_average_over_ranks(results):
         assert val == pytest.approx(float(np.mean([np.asarray(f["b"]) for f in full])), rel=1e-10)
         np.testing.assert_allclose(grad["xi"], results[r]["avg"]["xi"], rtol=1e-12, atol=1e-300)
     assert results[0]["bcast"] == results[1]["bcast"] == 3
+
+
+def test_one_collective_per_kl_mean(results):
+    """value and gradient travel in ONE packed all-reduce"""
+    for r in results:
+        assert results[r]["ncoll"] == 1
+
+
+def test_rank_without_samples(results):
+    """3 samples on 2 ranks, rank 1 holding none: both ranks get the mean of
+    the 3 (fast and deterministic mode), as the reference's _active_comm +
+    broadcast gives"""
+    sys.path.insert(0, ROOT)
+    from nifty_amd import utilities
+    dom, vals = _values(10)
+    mean = vals[0]
+    full = [mean + v for v in vals[:3]]
+    ref = utilities.pairwise_sum(full)
+    for det in (0, 1):
+        for r in results:
+            v0, g0, a0 = results[r][f"empty{det}"]
+            assert v0 == pytest.approx(float(np.asarray(ref["b"])) / 3, rel=1e-14)
+            for k in dom.keys():
+                np.testing.assert_allclose(g0[k], np.asarray(ref[k]) / 3, rtol=1e-13, atol=1e-300)
+                np.testing.assert_allclose(a0[k], np.asarray(ref[k]) / 3, rtol=1e-13, atol=1e-300)
+            if det:
+                for k in dom.keys():
+                    np.testing.assert_array_equal(g0[k], np.asarray(ref[k]) / 3)
+
+
+def test_deterministic_tree_any_split(results):
+    """the point-to-point pairwise tree equals the serial pairwise sum bit for
+    bit for every split of the items over the ranks (src/utilities.py:331-390)"""
+    sys.path.insert(0, ROOT)
+    from nifty_amd import utilities
+    dom, vals = _values(10)
+    serial = utilities.pairwise_sum(vals)
+    for r in results:
+        for n0, d in results[r]["dets"].items():
+            for k in dom.keys():
+                np.testing.assert_array_equal(d[k], np.asarray(serial[k]), err_msg=f"split {n0}")
