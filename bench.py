@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--newton-iters", type=int, default=2)
     p.add_argument("--newton-cg-max", type=int, default=50)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-iters", type=int, default=20)
+    p.add_argument("--cpu-pairs", type=int, default=1, help="mirrored pairs in the timed CPU oracle draw")
+    p.add_argument("--no-demo", action="store_true", help="skip the demo-controller line")
     p.add_argument("--deterministic-allreduce", action="store_true")
     return p.parse_args()
 
@@ -236,37 +237,81 @@ def load_pmc(label):
     return None if e is None else e.get("traffic_bytes")
 
 
-def roofline_of(kp):
-    """roofline object for the kernel with the largest time per CG iteration"""
-    lab = max(kp, key=lambda k: kp[k]["avg_us"] * kp[k]["launches"])
-    k = kp[lab]
-    if k["bytes"] is None:
-        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernel": lab, "avg_launch_us": k["avg_us"]}
-    return {"bound": "hbm", "achieved": k["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(k["gbs"] / HBM_PEAK_GBS, 4), "traffic": load_pmc(lab), "kernel": lab,
-            "avg_launch_us": k["avg_us"], "algorithmic_bytes_per_launch": k["bytes"]}
+def survey_bytes_per_iteration(cf, R):
+    """SURVEY.md §8(d)'s algorithmic bytes of one linear-CG iteration of one
+    right-hand side: N [(4d + 13) s + 8] for the CF metric + CG update, plus
+    2 s N + 16 nnz for the LOS pair (s = 8, d = 2)."""
+    N = int(np.prod(cf.target.shape))
+    d = len(cf.target.shape)
+    nnz = int(R._plan_np["box_ent"][-1])
+    return N * ((4 * d + 13) * 8 + 8) + 2 * 8 * N + 16 * nnz
 
 
-def cpu_baseline(cf_np_args, lat0, R, n, iters):
-    """Oracle (numpy + scipy.fft on all host cores) sampling-metric CG on the
-    same problem, bounded to `iters` CG iterations."""
+def roofline_of(kp, cgit, cf, R):
+    """roofline of the FFT+CG matvec the north star targets: one batched CG
+    iteration (k right-hand sides) as a unit -- §8(d) bytes x k over the
+    measured iteration time (the sum of its launches' HIP-event durations).
+    traffic: PMC HBM bytes of the same launches (profiles/pmc_traffic.json),
+    when every kernel of the iteration has an entry."""
+    k = cgit["rhs"]
+    by = survey_bytes_per_iteration(cf, R) * k
+    us = cgit["us_per_iteration"]
+    ach = by / (us * 1e-6) / 1e9
+    traffic = 0
+    for lab, e in kp.items():
+        t = load_pmc(lab)
+        if t is None:
+            traffic = None
+            break
+        traffic += t * e["launches"]
+    dom = max(kp, key=lambda lab: kp[lab]["avg_us"] * kp[lab]["launches"])
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "cg_iteration",
+            "rhs": k, "avg_launch_us": us, "algorithmic_bytes_per_launch": by,
+            "bytes_model": "SURVEY §8(d): k x (N[(4d+13)s+8] + 2sN + 16 nnz)",
+            "largest_kernel": {"label": dom, "avg_us": kp[dom]["avg_us"], "launches": kp[dom]["launches"],
+                               "gbs": kp[dom]["gbs"]}}
+
+
+def cpu_baseline(args, lat0, R, n, pairs):
+    """The oracle's geoVI draw (oracle/geovi.py: numpy + scipy.fft on all host
+    cores, scipy.sparse LOS) of `pairs` mirrored pair(s) with the bench's
+    controllers, timed from the seed spawn to the last residual."""
     import scipy.fft
     from oracle.cf import CFOracle
-    from oracle.sampling import LOSLikelihood, SamplingMetric, GradNormCtl, conjugate_gradient
-    # the box's CPU share for one GPU (OMP_NUM_THREADS=16 there), not os.cpu_count()
-    ncores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    o = CFOracle((n, n), **cf_np_args)
+    from oracle.geovi import LOSWhitened, draw_geovi
+    from oracle.sampling import GradNormCtl
+    ncores = os.cpu_count() or 1
+    o = CFOracle((n, n), **CF_ARGS)
     rows, cols, w = R.coo
-    lh = LOSLikelihood(o, rows, cols, w, R.target.shape[0], 1e-3)
+    lh = LOSWhitened(o, rows, cols, w, R.target.shape[0], 1e-3)
     with scipy.fft.set_workers(ncores):
-        M = SamplingMetric(o, lat0, lh.middle(lat0))
-        rng = np.random.default_rng(0)
-        b = {k: rng.standard_normal(np.shape(v)) for k, v in lat0.items()}
         t = time.perf_counter()
-        conjugate_gradient(M, {k: 0 * v for k, v in b.items()}, b, GradNormCtl(iteration_limit=iters))
+        res, iters = draw_geovi(lh, lat0, pairs, True, np.random.SeedSequence(1000),
+                                lambda: GradNormCtl(iteration_limit=args.lin_iters), args.newton_iters,
+                                max_cg=args.newton_cg_max)
         el = time.perf_counter() - t
-    return iters / el, ncores, el
+    return 2 * pairs / el, iters / el, ncores, el, iters
+
+
+def demo_step(ift, lh, pos, nsamp, comm):
+    """One step with SURVEY §8(d)'s demo controllers: sampling
+    AbsDeltaEnergyController(0.05, iteration_limit=100), NewtonCG(
+    AbsDeltaEnergyController(0.5, convergence_level=2, iteration_limit=15))."""
+    H = ift.StandardHamiltonian(lh, ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=100))
+    mini = ift.NewtonCG(ift.AbsDeltaEnergyController(deltaE=0.5, convergence_level=2, iteration_limit=15))
+    ift.random.push_sseq_from_seed(2000)
+    barrier_sync(1)
+    it0 = ift.ConjugateGradient.iterations_total
+    t = time.perf_counter()
+    sl = ift.draw_samples(pos, H, mini, nsamp, True, comm=comm)
+    ift.SampledKLEnergyClass(sl, H, [], None, True)
+    barrier_sync(1)
+    el = time.perf_counter() - t
+    ift.random.pop_sseq()
+    return {"samples_per_s": round(2 * nsamp / el, 4), "ms_per_step": round(el * 1e3, 1),
+            "cg_iters": int(ift.ConjugateGradient.iterations_total - it0),
+            "controllers": "sampling AbsDelta(0.05, 100); NewtonCG(AbsDelta(0.5, convergence_level=2, 15))"}
 
 
 def main():
@@ -315,16 +360,20 @@ def main():
     cgps = iters / el
     kp, cgit = kernel_probe(ift, cf, R, lh, pos, args.samples_per_gpu) if torch.cuda.is_available() \
         else (None, None)
-    roof = roofline_of(kp) if kp else None
+    roof = roofline_of(kp, cgit, cf, R) if kp else None
+    demo = None
+    if not args.no_demo and torch.cuda.is_available():
+        demo = demo_step(ift, lh, pos, nsamp, comm)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        lat0 = {k: np.asarray(pos[k]) for k in cf.domain.keys()}
-        cgi, ncores, cel = cpu_baseline(CF_ARGS, lat0, R, n, args.cpu_iters)
-        cpu = {"value": round(cgi * sps / cgps, 6), "unit": "samples/s", "cores": ncores, "kind": "port",
-               "cg_iter_per_s": round(cgi, 4),
-               "sample": (f"oracle (numpy + scipy.fft workers={ncores}) sampling-metric CG on the same "
-                          f"{n}^2 LOS problem, {args.cpu_iters} iterations in {cel:.1f}s; samples/s = "
-                          f"cpu_cg_iter_per_s x (GPU samples per CG iteration)")}
+        lat0 = {k: pos[k].val.cpu().numpy() for k in cf.domain.keys()}
+        sps_c, cgps_c, ncores, cel, citers = cpu_baseline(args, lat0, R, n, args.cpu_pairs)
+        cpu = {"value": round(sps_c, 6), "unit": "samples/s", "cores": ncores, "kind": "port",
+               "cg_iter_per_s": round(cgps_c, 4),
+               "sample": (f"oracle geoVI draw (oracle/geovi.py: numpy, scipy.fft workers={ncores}, "
+                          f"scipy.sparse LOS) of {args.cpu_pairs} mirrored pair(s) on the same {n}^2 LOS "
+                          f"problem with the bench's controllers: {2 * args.cpu_pairs} samples, {citers} CG "
+                          f"iterations in {cel:.1f} s")}
     if rank == 0:
         line = {"metric": "geoVI samples-drawn/sec (+ CG-iter/sec), 2048^2 CorrelatedField",
                 "value": round(sps, 6), "unit": "samples/s", "n_gpus": ws, "steps": args.steps,
@@ -337,7 +386,8 @@ def main():
                                        f"(inner CG <= {args.newton_cg_max})",
                            "global_batch": samples // args.steps, "parallelism": f"sample-dp{ws}"},
                 "cg_iter_per_s": round(cgps, 3), "cg_iters": int(iters),
-                "roofline": roof, "cpu_baseline": cpu, "cg_iteration": cgit, "kernels": kp}
+                "roofline": roof, "cpu_baseline": cpu, "demo_controllers": demo,
+                "cg_iteration": cgit, "kernels": kp}
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist
