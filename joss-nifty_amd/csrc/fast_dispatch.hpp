@@ -21,6 +21,12 @@ inline bool is_pow2(long long n) { return n > 0 && (n & (n - 1)) == 0; }
 
 inline bool rows_supported(int N) { return is_pow2(N) && N >= 8 && N <= 8192; }
 inline bool strided_supported(int N) { return is_pow2(N) && N >= 8 && N <= 512; }
+// single-pass strided transform of a long axis (1024 / 2048: L = 8 / 4
+// adjacent columns, 135-139 KB LDS, one 1024-thread workgroup per CU)
+inline bool longcol_supported(int N) {
+  static const int on = getenv("NFT_COL1P") ? atoi(getenv("NFT_COL1P")) : 0;
+  return on && (N == 1024 || N == 2048);
+}
 // lengths handled as a four-step pair of strided passes
 inline bool fourstep_supported(int N) { return is_pow2(N) && N >= 1024 && N <= 16384; }
 inline void fourstep_split(int N, int& N1, int& N2) {
@@ -109,6 +115,7 @@ static int launch_n(int N, const FastArgs<T>& a, hipStream_t s) {
   } else {
     switch (N) {
       NFT_CASE(8) NFT_CASE(16) NFT_CASE(32) NFT_CASE(64) NFT_CASE(128) NFT_CASE(256) NFT_CASE(512)
+      NFT_CASE(1024) NFT_CASE(2048)
     }
   }
 #undef NFT_CASE

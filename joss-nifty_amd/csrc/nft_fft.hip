@@ -564,7 +564,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
     const long long O = prod(cs, 0, axis);
     const long long rrs = prod(g.shape, axis + 1, g.nd);
     LineDesc desc = make_desc(g, cs, ax, axis, h);
-    if (strided_supported(N)) {
+    if (strided_supported(N) || longcol_supported(N)) {
       FastArgs<T> a;
       memset(&a, 0, sizeof(a));
       a.in = ws;
