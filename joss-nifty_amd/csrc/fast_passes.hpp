@@ -117,12 +117,31 @@ constexpr bool persist_ok() {
   return N <= 2048 && NT <= 256 && KIND == K_R2C;
 }
 
+// in-line LDS padding of a pass (fft_fast.hpp padx): every 8 elements for
+// the strided passes; NFT_PAD_ROWS / NFT_PAD_COLS override at build time
+#ifndef NFT_PAD_ROWS
+#define NFT_PAD_ROWS -1
+#endif
+#ifndef NFT_PAD_COLS
+#define NFT_PAD_COLS 3
+#endif
+template <int N, bool ROWS>
+constexpr int pass_pad() {
+  return ROWS ? NFT_PAD_ROWS : NFT_PAD_COLS;
+}
+// line pitch in LDS: the (padded) length, +1 for strided passes so the L
+// lines' element x fall in different banks
+template <int N, bool ROWS>
+constexpr int pass_pitch() {
+  return padded_len<N, pass_pad<N, ROWS>()>() + (ROWS ? 0 : 1);
+}
+
 // dynamic LDS of a pass: L lines (+ the unpack line table), then the
 // quarter twiddle table (N/4 entries) at a 16-byte aligned offset
 template <typename T, int N, int NT, int KIND, bool ROWS>
 constexpr size_t tw_lds_offset() {
   constexpr int L = NT * VPT / N;
-  constexpr int PITCH = ROWS ? N : N + 1;
+  constexpr int PITCH = pass_pitch<N, ROWS>();
   return ((size_t)L * PITCH * sizeof(cplx_t<T>) + (KIND == K_UNPACK ? (size_t)L * sizeof(UnpackLine) : 0) + 15) &
          ~(size_t)15;
 }
@@ -142,7 +161,8 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   using C = cplx_t<T>;
   constexpr int L = NT * VPT / N;
   static_assert(L >= 1, "NT*VPT must cover one line");
-  constexpr int PITCH = ROWS ? N : N + 1;
+  constexpr int PITCH = pass_pitch<N, ROWS>();
+  constexpr int PS = pass_pad<N, ROWS>();
   constexpr int SHN = ilog2(N), SHL = ilog2(L);
   extern __shared__ __align__(16) unsigned char smem[];
   C* lds = (C*)smem;
@@ -228,12 +248,12 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
     for (int r = 0; r < VPT; ++r) {
       int l, x;
       lx_of(r, l, x);
-      lds[l * PITCH + x] = rv[r];
+      lds[l * PITCH + padx<PS>(x)] = rv[r];
     }
     __syncthreads();
     const long long tn = PERSIST ? t + gridDim.x : ntiles;
     if (prefetch && tn < ntiles) load(tn, rv);  // in flight during the FFT and the stores
-    fft<T, N, NT, L, PITCH>(lds, twq, tid);
+    fft<T, N, NT, L, PITCH, PS>(lds, twq, tid);
     long long o, m, i0;
     tile_of(t, o, m, i0);
 
@@ -245,7 +265,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       for (int r = 0; r < VPT; ++r) {
         int l, x;
         lx_of(r, l, x);
-        C v = lds[l * PITCH + x];
+        C v = lds[l * PITCH + padx<PS>(x)];
         if (tw2) v = cmul(v, tw2[(m * x) & (a.Nfull - 1)]);
         if (a.conj_out) v.y = -v.y;
         v.x *= a.scale;
@@ -268,8 +288,8 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           const int k = e - l * NH;
           const long long row0 = 2 * (o + l);
           if (row0 >= a.Ireal) continue;
-          const C zk = lds[l * PITCH + k];
-          const C zm = lds[l * PITCH + ((N - k) & (N - 1))];
+          const C zk = lds[l * PITCH + padx<PS>(k)];
+          const C zm = lds[l * PITCH + padx<PS>((N - k) & (N - 1))];
           const C xa = C{h * (zk.x + zm.x), h * (zk.y - zm.y)};
           const C xb = C{h * (zk.y + zm.y), -h * (zk.x - zm.x)};
           const long long ko = (long long)k * g.out_sn;
@@ -286,8 +306,8 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           const int k = e & (N - 1);
           const long long row0 = 2 * (o + l);
           if (row0 >= a.Ireal) continue;
-          const C zk = lds[l * PITCH + k];
-          const C zm = lds[l * PITCH + ((N - k) & (N - 1))];
+          const C zk = lds[l * PITCH + padx<PS>(k)];
+          const C zm = lds[l * PITCH + padx<PS>((N - k) & (N - 1))];
           const long long ko = (long long)k * g.out_sn;
           fuse_store<T>(a.f, out, row0 * g.out_so + ko, hs * ((zk.x + zm.x) + sg * (zk.y - zm.y)));
           if (row0 + 1 < a.Ireal)
@@ -323,7 +343,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         lx_of(r, l, x);
         const UnpackLine u = lines[l];
         if (!u.valid) continue;
-        const C f = lds[l * PITCH + x];
+        const C f = lds[l * PITCH + padx<PS>(x)];
         const int k = (int)m * a.km + x * a.kx;
         fuse_store<T>(a.f, out, u.base + (long long)k * a.rs, sc * (f.x + sg * f.y));
         if (u.mirror) {

@@ -51,8 +51,23 @@ __device__ __forceinline__ cplx_t<T> tw_at(const cplx_t<T>* twq, int m) {
   return w;
 }
 
+// LDS position of element x of a line: PS >= 0 inserts one pad slot every
+// 2^PS elements, so the stride-R butterfly writes of the first stages (and
+// the strided passes' column-interleaved fills) spread over all banks
+// (MI355X_MICROARCH.md LDS table: ds_write_b128 serves 8 lanes per cycle,
+// 16-byte lanes at a 128-byte stride all hit one bank group).
+template <int PS>
+__device__ __forceinline__ constexpr int padx(int x) {
+  if constexpr (PS >= 0) return x + (x >> PS);
+  else return x;
+}
+template <int N, int PS>
+constexpr int padded_len() {
+  return PS >= 0 ? N + (N >> PS) : N;
+}
+
 // -------------------------------------------------------------- one stage
-template <typename T, int N, int NT, int L, int PITCH, int R, int NS>
+template <typename T, int N, int NT, int L, int PITCH, int R, int NS, int PS>
 __device__ __forceinline__ void stage(cplx_t<T>* lds, const cplx_t<T>* __restrict__ tw, int tid) {
   using C = cplx_t<T>;
   constexpr int NBL = N / R;
@@ -67,9 +82,9 @@ __device__ __forceinline__ void stage(cplx_t<T>* lds, const cplx_t<T>* __restric
     if (NBF % NT == 0 || b < NBF) {
       const int line = b >> SH_NBL;
       const int j = b & (NBL - 1);
-      const C* src = lds + line * PITCH + j;
+      const C* src = lds + line * PITCH;
 #pragma unroll
-      for (int t = 0; t < R; ++t) v[i][t] = src[t * NBL];
+      for (int t = 0; t < R; ++t) v[i][t] = src[padx<PS>(j + t * NBL)];
     }
   }
   __syncthreads();
@@ -86,28 +101,29 @@ __device__ __forceinline__ void stage(cplx_t<T>* lds, const cplx_t<T>* __restric
         for (int t = 1; t < R; ++t) v[i][t] = cmul(v[i][t], tw_at<T, N>(tw, t * step));
       }
       dftR<T, R>(v[i]);
-      C* dst = lds + line * PITCH + (j - k) * R + k;
+      C* dst = lds + line * PITCH;
+      const int d0 = (j - k) * R + k;
 #pragma unroll
-      for (int t = 0; t < R; ++t) dst[t * NS] = v[i][t];
+      for (int t = 0; t < R; ++t) dst[padx<PS>(d0 + t * NS)] = v[i][t];
     }
   }
   __syncthreads();
 }
 
-template <typename T, int N, int NT, int L, int PITCH, int NS>
+template <typename T, int N, int NT, int L, int PITCH, int NS, int PS>
 __device__ __forceinline__ void stages(cplx_t<T>* lds, const cplx_t<T>* __restrict__ tw, int tid) {
   if constexpr (NS < N) {
     constexpr int R = radix_at(N, NS);
-    stage<T, N, NT, L, PITCH, R, NS>(lds, tw, tid);
-    stages<T, N, NT, L, PITCH, NS * R>(lds, tw, tid);
+    stage<T, N, NT, L, PITCH, R, NS, PS>(lds, tw, tid);
+    stages<T, N, NT, L, PITCH, NS * R, PS>(lds, tw, tid);
   }
 }
 
 // forward FFT of the L lines in LDS (caller synced after filling); tw is the
 // LDS quarter twiddle table (tw_at)
-template <typename T, int N, int NT, int L, int PITCH>
+template <typename T, int N, int NT, int L, int PITCH, int PS = -1>
 __device__ __forceinline__ void fft(cplx_t<T>* lds, const cplx_t<T>* __restrict__ tw, int tid) {
-  stages<T, N, NT, L, PITCH, 1>(lds, tw, tid);
+  stages<T, N, NT, L, PITCH, 1, PS>(lds, tw, tid);
 }
 
 // -------------------------------------------------------------- tiles

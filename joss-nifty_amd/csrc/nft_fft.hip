@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "fast_dispatch.hpp"
+#include "fast_pro.hpp"
 #include "fft_passes.hpp"
 #include <type_traits>
 
@@ -481,10 +482,24 @@ static LineDesc make_desc(const Geo& g, const long long* cs, const std::vector<i
   return d;
 }
 
+// geometry covered by hartley_v2's multi-axis path
+static bool v2_multi_ok(const Geo& g, const std::vector<int>& ax) {
+  using namespace fast;
+  const int m = (int)ax.size();
+  if (m < 2) return false;
+  const int h = ax[m - 1];
+  if (h != g.nd - 1 || !rows_supported((int)g.shape[h])) return false;
+  for (int k = 1; k < m - 1; ++k)
+    if (!strided_supported((int)g.shape[ax[k]])) return false;
+  const int N0 = (int)g.shape[ax[0]];
+  return strided_supported(N0) || fourstep_supported(N0);
+}
+
+// r2c_done: the R2C row pass has already written the half spectra to ws
 template <typename T>
 static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector<int>& ax, int sigma,
                       double scale, void* ws, size_t ws_bytes, hipStream_t s,
-                      const fast::FuseArgs* fz = nullptr) {
+                      const fast::FuseArgs* fz = nullptr, bool r2c_done = false) {
   using namespace fast;
   const int m = (int)ax.size();
   const int last = g.nd - 1;
@@ -520,7 +535,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
     return NFT_ERR_ARG;
   }
   int st;
-  {  // R2C rows along the last axis
+  if (!r2c_done) {  // R2C rows along the last axis
     const int N = (int)g.shape[h];
     FastArgs<T> a;
     memset(&a, 0, sizeof(a));
@@ -713,6 +728,32 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
   static const bool v1_only = getenv("NFT_ENGINE_V1") != nullptr;
   static const bool no_split = getenv("NFT_NO_PRO_SPLIT") != nullptr;
   const long long ntot = prod(g.shape, 0, g.nd);
+  // R2C+prologue in one pass (fast_pro.hpp): bitwise equal to the split
+  // path, but measured slower at 4 x 2048^2 (209 vs 128 + 73 us: the dA
+  // gathers, 32 B per pixel from a 10 MB table, stay latency-bound inside
+  // the FFT workgroup) -- opt-in, NFT_PRO_PAIRS=1
+  static const bool pairs = getenv("NFT_PRO_PAIRS") != nullptr;
+  if (!v1_only && pairs && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && f.nb >= 1 &&
+      (long long)f.nb * f.P == ntot && v2_multi_ok(g, ax)) {
+    // R2C row pass with the prologue, the items' rows paired as in the plain pass
+    const int N = (int)g.shape[g.nd - 1];
+    const long long rows = f.P / N;
+    const int L = fast::pro_pairs_group(N, f.nb);
+    if (N >= 512 && N <= 4096 && f.P % N == 0 && rows % 2 == 0 && L > 0) {
+      long long cs[MAXD];
+      half_shape(g, g.nd - 1, cs);
+      const long long ostride = rows * cs[g.nd - 1];
+      int st = fast::launch_pro_pairs<T>(N, f, ws, rows, f.nb, ostride, cs[g.nd - 1], s);
+      if (st == NFT_OK) {
+        fast::FuseArgs f2 = f;
+        f2.pro = 0;
+        f2.px = f2.pa = f2.pb = f2.pc = nullptr;
+        f2.pidx = nullptr;
+        return hartley_v2<T>(nullptr, out, g, ax, sigma, scale, ws, hws, s, &f2, true);
+      }
+      if (st != 1) return st;
+    }
+  }
   if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && f.nb > 1 &&
       (long long)f.nb * f.P == ntot &&
       ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
