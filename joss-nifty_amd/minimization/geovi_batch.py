@@ -554,16 +554,11 @@ def plan(minimizer, f_lh, _unused, position):
 
 
 # ------------------------------------------------------------------ KL terms
-def kl_batch(hamiltonian, positions):
-    """Hamiltonian values and gradients at a list of latent MultiFields in one
-    batched pass (SampledKLEnergyClass, kl_energies.py:295-356: its per
-    sample H(Linearization.make_var(s)) evaluations), or None if the
-    likelihood is not a GaussianEnergy(data, scaling / diagonal inverse
-    covariance) or PoissonianEnergy applied to a supported model chain.
-
-    Returns ([value_i], [gradient_i MultiField])."""
-    if not ENABLED or len(positions) < 2:
-        return None
+def _likelihood(hamiltonian, positions):
+    """(kind, E, icov value, scale, pipeline) of a StandardHamiltonian whose
+    likelihood is GaussianEnergy(data, scaling / diagonal inverse covariance)
+    or PoissonianEnergy (optionally scaled) on a supported model chain, else
+    None."""
     from ..operators.diagonal_operator import DiagonalOperator
     from ..operators.energy_operators import GaussianEnergy, PoissonianEnergy, _LikelihoodChain
     from ..operators.scaling_operator import ScalingOperator
@@ -576,6 +571,7 @@ def kl_batch(hamiltonian, positions):
         scale = float(np.real(ops[0]._factor))
         ops = ops[1:]
     E = ops[0]
+    icv = None
     if isinstance(E, GaussianEnergy):
         if E._data is None:
             return None
@@ -594,6 +590,23 @@ def kl_batch(hamiltonian, positions):
     pipe = Pipeline.parse(ops[1:])
     if pipe is None or pipe.layout.device.type != "cuda" or pipe.layout.domain != positions[0].domain:
         return None
+    return kind, E, icv, scale, pipe
+
+
+def kl_batch(hamiltonian, positions):
+    """Hamiltonian values and gradients at a list of latent MultiFields in one
+    batched pass (SampledKLEnergyClass, kl_energies.py:295-356: its per
+    sample H(Linearization.make_var(s)) evaluations), or None if the
+    likelihood is not a GaussianEnergy(data, scaling / diagonal inverse
+    covariance) or PoissonianEnergy applied to a supported model chain.
+
+    Returns ([value_i], [gradient_i MultiField])."""
+    if not ENABLED or len(positions) < 2:
+        return None
+    parsed = _likelihood(hamiltonian, positions)
+    if parsed is None:
+        return None
+    kind, E, icv, scale, pipe = parsed
     lay = pipe.layout
     X = torch.stack([lay.pack(p) for p in positions])
     k = X.shape[0]
@@ -627,3 +640,51 @@ def kl_batch(hamiltonian, positions):
     G.add_(X)                                      # prior: 0.5 x.x
     vals = [float(lval[i]) + 0.5 * float(h[1, i]) for i in range(k)]
     return vals, [lay.unpack(G[i]) for i in range(k)]
+
+
+def kl_metric_batch(hamiltonian, positions):
+    """The per-sample Hamiltonian metrics of SampledKLEnergyClass.apply_metric
+    (kl_energies.py:340-350: per sample and per application a full
+    H(Linearization.make_var(s, want_metric=True)) rebuild) linearised ONCE
+    at the k local sample positions and applied to all of them in one batched
+    pass: M_s x = J_s^T W_s J_s x + x with W_s the likelihood's Fisher metric
+    at s (Gaussian: the inverse covariance; Poissonian: 1 / lambda_s; times
+    the likelihood scale) and the identity of the standard prior.
+
+    Returns a callable x -> [M_s x for every local sample] (MultiFields, in
+    sample order, for the caller's sample average), or None when the
+    Hamiltonian is not covered (then the caller keeps the reference's
+    per-sample path)."""
+    if not ENABLED or not positions:
+        return None
+    parsed = _likelihood(hamiltonian, positions)
+    if parsed is None:
+        return None
+    kind, E, icv, scale, pipe = parsed
+    lay = pipe.layout
+    X = torch.stack([lay.pack(p) for p in positions])
+    k = X.shape[0]
+    Sf, states = pipe.fwd(X)
+    if kind == "gauss":
+        W = icv if isinstance(icv, float) else icv.reshape((1,) + tuple(Sf.shape[1:]))
+    else:
+        W = 1. / Sf
+    if scale != 1.0:
+        W = W * scale
+    del X
+
+    def apply(x):
+        v = lay.pack(x)
+        V = v.reshape(1, -1).expand(k, -1).contiguous()
+        U = pipe.jvp(states, V)
+        U = (U * W).contiguous()
+        Q = torch.empty((k, lay.size), dtype=torch.float64, device=V.device)
+        ends = [o + n for o, n in zip(lay.offsets, lay.sizes)]
+        starts = list(lay.offsets[1:]) + [lay.size]
+        for a, b in zip(ends, starts):
+            if b > a:
+                Q[:, a:b] = 0.0
+        pipe.vjp(states, U, Q)
+        Q.add_(V)
+        return [lay.unpack(Q[i]) for i in range(k)]
+    return apply

@@ -250,6 +250,23 @@ class SampledKLEnergyClass(Energy):
                                     self._invariants, self._nanisinf)
 
     def apply_metric(self, x):
+        """Sample average of the Hamiltonian metric (kl_energies.py:340-350).
+        Covered likelihoods: the local samples' metrics are linearised once per
+        KL position and applied batched (geovi_batch.kl_metric_batch), the
+        per-sample results summed in the reference's pairwise order and
+        reduced across ranks with ONE all-reduce per application; otherwise
+        the reference's per-sample Linearization path."""
+        sl = self._sample_list
+        if not hasattr(self, "_mbatch"):
+            self._mbatch = None
+            if isinstance(sl._m, MultiField) and len(self._constants) == 0 and sl.n_local_samples > 0:
+                from . import geovi_batch
+                self._mbatch = geovi_batch.kl_metric_batch(self._hamiltonian, list(sl.local_iterator()))
+        if self._mbatch is not None:
+            res = self._mbatch(x)
+            return utilities.allreduce_sum(res, sl.comm, counts=sl._counts,
+                                           template=lambda: 0 * x) / sl.n_samples
+
         def _func(inp):
             inp, tmp = _reduce_by_keys(inp, self._hamiltonian, self._constants)
             tmp = tmp(Linearization.make_var(inp, want_metric=True))

@@ -801,6 +801,57 @@ def gen_mgvi_absdelta_trace():
     _save("mgvi128_absdelta_trace.npz", d)
 
 
+def gen_kl_metric():
+    """SampledKLEnergyClass.apply_metric (kl_energies.py:340-350 ->
+    sample_list.py:285-310): the sample average of the Hamiltonian's metric
+    (likelihood Fisher metric + identity) at every sample position, for a
+    fixed ResidualSampleList (two mirrored pairs of seeded residuals at a
+    seeded mean) -- no CG inside, so the fixture pins the averaging alone.
+    Gaussian (32^2, GeometryRemover) and Poissonian (32^2, exp) likelihoods;
+    the KL value / gradient at the same samples alongside."""
+    d = {}
+    for tag in ("g", "p"):
+        pos_space = ift.RGSpace((32, 32))
+        cf = ift.SimpleCorrelatedField(pos_space, **CF_ARGS)
+        ift.random.push_sseq_from_seed(51)
+        if tag == "g":
+            R = ift.GeometryRemover(pos_space)
+            sr = R @ cf
+            N = ift.ScalingOperator(R.target, 0.01, np.float64)
+            mock = ift.from_random(sr.domain, "normal")
+            data = sr(mock) + N.draw_sample()
+            lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ sr
+            d[tag + "_data"] = data.val
+        else:
+            sig = cf.exp()
+            mock = ift.from_random(sig.domain, "normal")
+            counts = ift.random.current_rng().poisson(sig(mock).val).astype(np.int64)
+            lh = ift.PoissonianEnergy(ift.makeField(pos_space, counts)) @ sig
+            d[tag + "_counts"] = counts
+        mean = 0.1 * ift.from_random(lh.domain, "normal")
+        res = [0.3 * ift.from_random(lh.domain, "normal") for _ in range(2)]
+        v = ift.from_random(lh.domain, "normal")
+        ift.random.pop_sseq()
+        H = ift.StandardHamiltonian(lh)
+        sl = ift.ResidualSampleList(mean, [res[0], res[0], res[1], res[1]], [False, True, False, True])
+        kl = ift.minimization.kl_energies.SampledKLEnergyClass(sl, H, [], None, True)
+        for k, val in _flat(mean).items():
+            d[f"{tag}_mean_" + k] = val
+        for i, r in enumerate(res):
+            for k, val in _flat(r).items():
+                d[f"{tag}_r{i}_" + k] = val
+        for k, val in _flat(v).items():
+            d[f"{tag}_v_" + k] = val
+        for k, val in _flat(kl.apply_metric(v)).items():
+            d[f"{tag}_mv_" + k] = val
+        for k, val in _flat(kl.metric(v)).items():
+            d[f"{tag}_mop_" + k] = val
+        d[tag + "_value"] = np.array(kl.value)
+        for k, val in _flat(kl.gradient).items():
+            d[f"{tag}_grad_" + k] = val
+    _save("klmetric32.npz", d)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:

@@ -56,11 +56,17 @@ def _run(comm):
             ift.random.push_sseq_from_seed(51)
             kl = ift.SampledKLEnergy(pos, H, 2, mini, True, comm=comm)
             ift.random.pop_sseq()
+            # the KL metric (kl_energies.py:340-350): batched per-sample
+            # metrics, one reduction per application
+            with ift.random.Context(7):
+                v = ift.from_random(cf.domain, "normal")
+            mvf = kl.apply_metric(v)
+            mv = {k: mvf[k].val.cpu().numpy() for k in mvf.keys()}
             utilities.DETERMINISTIC_ALLREDUCE = False
             grad = {k: kl.gradient[k].val.cpu().numpy() for k in kl.gradient.keys()}
             sl = kl.samples
             loc = [{k: sl._r[i][k].val.cpu().numpy() for k in cf.domain.keys()} for i in range(len(sl._r))]
-            out[(geo, det)] = (kl.value, grad, loc, list(sl._n), sl.n_samples)
+            out[(geo, det)] = (kl.value, grad, loc, list(sl._n), sl.n_samples, mv)
     return out
 
 
@@ -115,9 +121,9 @@ def single(dev):
 
 @pytest.mark.parametrize("geo", [False, True])
 def test_sharded_kl_bitwise_deterministic(sharded, single, geo):
-    v1, g1, loc1, neg1, n1 = single[(geo, True)]
+    v1, g1, loc1, neg1, n1 = single[(geo, True)][:5]
     for r in sharded:
-        v, g, loc, neg, n = sharded[r][(geo, True)]
+        v, g, loc, neg, n = sharded[r][(geo, True)][:5]
         assert n == n1 == 4
         assert v == v1, (r, v, v1)
         for k in g1:
@@ -132,9 +138,9 @@ def test_sharded_kl_bitwise_deterministic(sharded, single, geo):
 
 @pytest.mark.parametrize("geo", [False, True])
 def test_sharded_kl_fast_mode(sharded, single, geo):
-    v1, g1, _, _, _ = single[(geo, False)]
+    v1, g1 = single[(geo, False)][:2]
     for r in sharded:
-        v, g, _, _, _ = sharded[r][(geo, False)]
+        v, g = sharded[r][(geo, False)][:2]
         assert abs(v - v1) <= 1e-13 * abs(v1)
         for k in g1:
             np.testing.assert_allclose(g[k], g1[k], rtol=1e-12, atol=1e-14 * np.abs(g1[k]).max())
@@ -145,7 +151,23 @@ def test_sharded_mgvi_mirrored(sharded):
     """MGVI residuals of a pair are one residual with neg flags (False, True),
     the pair held by one rank (test_mpi/test_kl.py:117-133)"""
     for r in sharded:
-        _, _, loc, neg, _ = sharded[r][(False, True)]
+        _, _, loc, neg = sharded[r][(False, True)][:4]
         assert neg == [False, True]
         for k in loc[0]:
             np.testing.assert_array_equal(loc[0][k], loc[1][k])
+
+
+@pytest.mark.parametrize("geo", [False, True])
+def test_sharded_kl_metric(sharded, single, geo):
+    """KL metric application on 2 ranks: bit-identical to 1 rank in
+    deterministic mode, to rounding with the one all-reduce"""
+    m1 = single[(geo, True)][5]
+    for r in sharded:
+        m = sharded[r][(geo, True)][5]
+        for k in m1:
+            np.testing.assert_array_equal(m[k], m1[k], err_msg=f"rank {r} key {k}")
+    m1 = single[(geo, False)][5]
+    for r in sharded:
+        m = sharded[r][(geo, False)][5]
+        for k in m1:
+            np.testing.assert_allclose(m[k], m1[k], rtol=1e-12, atol=1e-14 * np.abs(m1[k]).max())
