@@ -29,7 +29,8 @@ from .minimization.iteration_controllers import (AbsDeltaEnergyController, Delta
 from .minimization.kl_energies import SampledKLEnergy, SampledKLEnergyClass, draw_samples
 from .minimization.line_search import LineSearch
 from .minimization.quadratic_energy import QuadraticEnergy
-from .minimization.sample_list import ResidualSampleList
+from .minimization.optimize_kl import optimize_kl
+from .minimization.sample_list import ResidualSampleList, SampleList
 from .probing import StatCalculator, approximation2endo, probe_diagonal
 from .multi_domain import MultiDomain
 from .multi_field import MultiField

@@ -5,6 +5,9 @@ Averages over samples: per rank the reference's pairwise order, across ranks
 ONE all-reduce of a packed buffer (utilities.allreduce_sum), or the
 reference's global pairwise tree over point-to-point messages in
 deterministic mode (bit-identical for any number of ranks)."""
+import glob
+import os
+
 import numpy as np
 
 from .. import utilities
@@ -106,3 +109,120 @@ class ResidualSampleList:
         mean = self.average(op)
         sq = self.average(lambda s: (op(s) if op is not None else s) ** 2)
         return mean, sq - mean ** 2
+
+    @property
+    def local_indices(self):
+        return range(self._lo, self._lo + self._nlocal)
+
+    # ------------------------------------------------------------ disk
+    # sample_list.py:510-531: one file per sample (global index) written by
+    # its rank, the mean by the MPI master; data-only files (checkpoint.py)
+    def save(self, file_name_base, overwrite=False):
+        from .checkpoint import save_field
+        for i, isample in enumerate(self.local_indices):
+            save_field(f"{file_name_base}.{isample}.npz", self._r[i], {"neg": bool(self._n[i])}, overwrite)
+        if utilities.get_MPI_params_from_comm(self._comm)[2]:
+            save_field(f"{file_name_base}.mean.npz", self._m, None, overwrite)
+        _barrier(self._comm)
+
+    @classmethod
+    def load(cls, file_name_base, comm=None, domain=None):
+        """``domain``: the latent MultiDomain the fields belong to (else the
+        domains are rebuilt from the files' descriptors)"""
+        from .checkpoint import load_field
+        _barrier(comm)
+        mean, _ = load_field(f"{file_name_base}.mean.npz", domain)
+        res, neg = [], []
+        for f in _local_sample_files(file_name_base, comm):
+            r, ex = load_field(f, domain)
+            res.append(r)
+            neg.append(bool(ex["neg"]))
+        return cls(mean, res, neg, comm=comm)
+
+    @classmethod
+    def load_mean(cls, file_name_base, domain=None):
+        from .checkpoint import load_field
+        return load_field(f"{file_name_base}.mean.npz", domain)[0]
+
+
+class SampleList:
+    """Plain list of (possibly distributed) samples (sample_list.py:533-653);
+    optimize_kl's result for maximum-a-posteriori iterations."""
+
+    def __init__(self, samples, comm=None, domain=None):
+        self._s = list(samples)
+        self._comm = comm
+        if domain is None:
+            if not self._s:
+                raise ValueError("SampleList without samples needs a domain")
+            domain = self._s[0].domain
+        self._domain = domain
+        ntask, rank, _ = utilities.get_MPI_params_from_comm(comm)
+        counts = [len(self._s)] if comm is None else [int(c) for c in comm.allgather(len(self._s))]
+        self._counts = None if comm is None else counts
+        self._lo = int(sum(counts[:rank]))
+
+    @property
+    def comm(self):
+        return self._comm
+
+    @property
+    def domain(self):
+        return self._domain
+
+    @property
+    def n_samples(self):
+        return len(self._s) if self._counts is None else int(sum(self._counts))
+
+    @property
+    def n_local_samples(self):
+        return len(self._s)
+
+    @property
+    def local_indices(self):
+        return range(self._lo, self._lo + len(self._s))
+
+    def local_item(self, i):
+        return self._s[i]
+
+    def local_iterator(self):
+        return iter(self._s)
+
+    def average(self, op=None):
+        res = [op(s) if op is not None else s for s in self._s]
+        return utilities.allreduce_sum(res, self._comm, counts=self._counts) / self.n_samples
+
+    def sample_stat(self, op=None):
+        mean = self.average(op)
+        sq = self.average(lambda s: (op(s) if op is not None else s) ** 2)
+        return mean, sq - mean ** 2
+
+    def save(self, file_name_base, overwrite=False):
+        from .checkpoint import save_field
+        for s, isample in zip(self._s, self.local_indices):
+            save_field(f"{file_name_base}.{isample}.npz", s, None, overwrite)
+        _barrier(self._comm)
+
+    @classmethod
+    def load(cls, file_name_base, comm=None, domain=None):
+        from .checkpoint import load_field
+        _barrier(comm)
+        return cls([load_field(f, domain)[0] for f in _local_sample_files(file_name_base, comm)], comm=comm)
+
+
+def _barrier(comm):
+    if comm is not None:
+        comm.Barrier()
+
+
+def _local_sample_files(file_name_base, comm):
+    """this rank's share (shareRange) of the sample files, in index order
+    (sample_list.py:626-653)"""
+    files = glob.glob(f"{file_name_base}.*.npz")
+    idx = sorted(int(f[len(file_name_base) + 1:-4]) for f in files
+                 if f[len(file_name_base) + 1:-4].isdigit())
+    if idx != list(range(len(idx))):
+        raise RuntimeError(f"sample files of {file_name_base} are not numbered 0..n-1")
+    ntask, rank, _ = utilities.get_MPI_params_from_comm(comm)
+    lo, hi = utilities.shareRange(len(idx), ntask, rank)
+    return [f"{file_name_base}.{i}.npz" for i in range(lo, hi)]

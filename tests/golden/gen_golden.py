@@ -852,6 +852,46 @@ def gen_kl_metric():
     _save("klmetric32.npz", d)
 
 
+def gen_optimize_kl():
+    """optimize_kl (optimize_kl.py:51-412) end to end on the 32^2 Gaussian
+    problem: 3 global iterations (MGVI, one mirrored pair; then one MAP
+    iteration with n_samples = 0; then geoVI, one pair), NewtonCG(2) on the
+    KL, no output directory.  Records the mean after every iteration and the
+    KL energy history; the reference's own sensitivity to a 1e-15 relative
+    perturbation of the initial xi bounds the comparison tolerance."""
+    cf, lh, data, mock, pos = _gaussian_problem(32)
+    d = {"data": data.val}
+    for k, v in _flat(pos).items():
+        d["pos_" + k] = v
+    pos_p = ift.MultiField.from_dict({k: (v * (1 + 1e-15) if k == "xi" else v) for k, v in pos.items()})
+    runs = []
+    for p0 in (pos, pos_p):
+        means = []
+        ift.random.push_sseq_from_seed(61)
+        sl, mean = ift.optimize_kl(
+            lh, 3, lambda i: 0 if i == 1 else 1,
+            ift.NewtonCG(ift.GradientNormController(iteration_limit=2)),
+            ift.GradientNormController(iteration_limit=8),
+            lambda i: ift.NewtonCG(ift.GradientNormController(iteration_limit=1)) if i == 2 else None,
+            initial_position=p0, plot_energy_history=False, plot_minisanity_history=False,
+            return_final_position=True, inspect_callback=lambda sl, i: means.append(
+                {k: np.asarray(v.val) for k, v in (sl._m if hasattr(sl, "_m") else sl.local_item(0)).items()}))
+        ift.random.pop_sseq()
+        runs.append((means, sl, mean))
+    (means, sl, mean), (means_p, _, _) = runs
+    for i, m in enumerate(means):
+        for k, v in m.items():
+            d[f"it{i}_mean_" + k] = v
+        d[f"it{i}_sens"] = np.array(max(np.linalg.norm(means_p[i][k] - v) / max(np.linalg.norm(v), 1e-300)
+                                        for k, v in m.items()))
+    for k, v in _flat(mean).items():
+        d["final_" + k] = v
+    for i in range(sl.n_samples):
+        for k, v in _flat(sl.local_item(i)).items():
+            d[f"s{i}_" + k] = v
+    _save("optkl32.npz", d)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
