@@ -151,6 +151,8 @@ def byte_model(cf, R, k, n_lat):
         "fft_r2c+pro": 8 * k * N + 8 * N + 8 * N + 4 * N + 8 * k * B + 16 * k * Hh,
         # batched prologue as its own pass: x (k), A, xi0, pindex, dA (k) -> u (k)
         "pro_batch": 8 * k * N + 8 * N + 8 * N + 4 * N + 8 * k * B + 8 * k * N,
+        # folded: the cell's bin (N_f), dA gathered per mirror class; no pindex
+        "pro_fold": 8 * k * N + 8 * N + 8 * N + 4 * Nf + 8 * k * B + 8 * k * N,
         "fft_r2c": 8 * k * N + 16 * k * Hh,
         "fft_c2c": 2 * 16 * k * Hh,
         "fft_unpack": 16 * k * Hh + 8 * k * N,

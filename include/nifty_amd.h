@@ -203,6 +203,15 @@ typedef struct nft_hartley_fuse {
   /* per-item strides of pro_a, pro_b, epi_a, epi_b (0: shared by the batch,
    * the default) -- a batch of different linearisation points */
   int64_t a_bstride, b_bstride, ea_bstride, eb_bstride;
+  /* 1: pro_index holds one bin per cell of the FUNDAMENTAL CELL of the
+   * harmonic grid (n_a / 2 + 1 per transform axis, C order) instead of one
+   * per element: element j reads pro_c[pro_index[cell(j)] * c_estride +
+   * item * c_bstride], cell(j) = (min(k_a, n_a - k_a))_a -- the |k| mirror
+   * image, which has j's bin.  The batched prologue then gathers dA once per
+   * mirror class and writes all 2^d images (4x fewer scattered gathers at
+   * d = 2, no per-element index read).  Requires the transform axes to be
+   * all of an item's axes. */
+  int64_t pro_folded;
 } nft_hartley_fuse;
 
 int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes,

@@ -68,7 +68,7 @@ class HartleyFuse(ctypes.Structure):
                                   "epi_out2")] + [("epi_shift", _d)] + \
                [(n, _i64) for n in ("batch_period", "x_bstride", "c_bstride", "out_bstride", "d_bstride",
                                     "out2_bstride", "c_estride", "a_bstride", "b_bstride", "ea_bstride",
-                                    "eb_bstride")]
+                                    "eb_bstride", "pro_folded")]
 
 
 class LosPlan(ctypes.Structure):
@@ -301,7 +301,9 @@ def spmv_scaled(indptr, indices, weights, rowblocks, x, y, colscale=None, rowsca
 
 def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None):
     """out = epilogue(scale * Hartley(prologue)) with
-    pro = dict(a=, x=, b=, c=, index=) and epi = dict(a=, d=, shift=, b=, out2=)
+    pro = dict(a=, x=, b=, c=, index=) (or fold=True and c per fundamental
+    cell instead of index, nft_hartley_fuse.pro_folded) and
+    epi = dict(a=, d=, shift=, b=, out2=)
     (nft_hartley_fused); `x` is the plain input when no prologue is given.
     Batched transforms: `shape` = (k, *grid), axes over the grid, and
     batch = dict(period=, x=, c=, out=, d=, out2=) with the per-item strides
@@ -320,6 +322,7 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
             v = pro.get(k)
             tens.append(v)
             setattr(f, fld, v.data_ptr() if v is not None else None)
+        f.pro_folded = 1 if pro.get("fold") else 0
     if epi:
         for k, fld in (("a", "epi_a"), ("d", "epi_d"), ("b", "epi_b"), ("out2", "epi_out2")):
             v = epi.get(k)

@@ -36,7 +36,27 @@ struct FuseArgs {
   long long sx, sc, so, sd, s2;
   long long ce;  // element stride of pc (>= 1)
   long long sa, sb, sea, seb;  // per-item strides of pa, pb, ea, eb (0: shared)
+  // folded bin gather (nft_hartley_fuse.pro_folded): item grid n[0..fnd)
+  // (all transform axes), fundamental-cell strides fs[] (C order over n/2+1)
+  int fnd;
+  long long fn[3], fs[3];
 };
+
+// element index into pc of item-element j: its bin (pidx[j]) or, folded, the
+// bin of its fundamental cell (pidx[cell(j)]), times the element stride
+// (an item has < 2^31 elements: 32-bit index arithmetic)
+__device__ __forceinline__ long long pro_cidx(const FuseArgs& f, long long j) {
+  if (f.fnd == 0) return (long long)f.pidx[j] * f.ce;
+  unsigned c = 0, r = (unsigned)j;
+  for (int a = f.fnd - 1; a >= 0; --a) {
+    const unsigned n = (unsigned)f.fn[a];
+    const unsigned q = r / n;
+    const unsigned k = r - q * n;
+    r = q;
+    c += (k <= n - k ? k : n - k) * (unsigned)f.fs[a];
+  }
+  return (long long)f.pidx[c] * f.ce;
+}
 
 __device__ __forceinline__ void fuse_split(const FuseArgs& f, long long i, long long& b, long long& j) {
   if (f.P == 0) {
@@ -57,7 +77,7 @@ __device__ __forceinline__ T fuse_pro(const FuseArgs& f, long long i) {
   fuse_split(f, i, b, j);
   T v = ((const T*)f.px)[b * f.sx + j];
   if (f.pa) v *= ((const T*)f.pa)[b * f.sa + j];
-  if (f.pb) v += ((const T*)f.pb)[b * f.sb + j] * ((const T*)f.pc)[b * f.sc + f.pidx[j] * f.ce];
+  if (f.pb) v += ((const T*)f.pb)[b * f.sb + j] * ((const T*)f.pc)[b * f.sc + pro_cidx(f, j)];
   return v;
 }
 
@@ -208,7 +228,8 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         const long long row0 = 2 * (o + l);
         if (row0 < a.Ireal) {
           const long long e0 = row0 * g.in_so + (long long)x * g.in_sn;
-          if (a.f.pro) {
+          // the persistent variant never runs a prologue (launch_one)
+          if (!PF && a.f.pro) {
             v.x = fuse_pro<T>(a.f, e0);
             if (row0 + 1 < a.Ireal) v.y = fuse_pro<T>(a.f, e0 + g.in_so);
           } else {

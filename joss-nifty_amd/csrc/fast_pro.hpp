@@ -46,7 +46,6 @@ __global__ __launch_bounds__(L* N / VPT) void r2c_pro_pairs(FuseArgs f, cplx_t<T
   const T* __restrict__ pa = (const T*)f.pa;
   const T* __restrict__ pb = (const T*)f.pb;
   const T* __restrict__ pc = (const T*)f.pc;
-  const int* __restrict__ pidx = f.pidx;
   const bool has1 = row0 + 1 < nrows;
   // every load of the tile is issued before the first use (the x values and
   // the dA gathers of all L items), so one workgroup keeps ~40 loads per
@@ -61,7 +60,7 @@ __global__ __launch_bounds__(L* N / VPT) void r2c_pro_pairs(FuseArgs f, cplx_t<T
       const bool ok = h == 0 || has1;
       a[h][m] = (pa && ok) ? pa[j] : (T)1;
       c[h][m] = (pb && ok) ? pb[j] : (T)0;
-      g[h][m] = (pb && ok) ? (long long)pidx[j] * f.ce : 0;
+      g[h][m] = (pb && ok) ? pro_cidx(f, j) : 0;
     }
   T xv[L][2][PX], cv[L][2][PX];
 #pragma unroll

@@ -684,7 +684,6 @@ __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __r
   const T* __restrict__ pa = (const T*)f.pa;
   const T* __restrict__ pb = (const T*)f.pb;
   const T* __restrict__ pc = (const T*)f.pc;
-  const int* __restrict__ pidx = f.pidx;
   using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   // interleaved dA (ce == nb, sc == 1): each pixel's gather is one contiguous
   // run; read it with 2-wide vector loads (half the divergent load
@@ -693,9 +692,9 @@ __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __r
   for (long long j = (long long)blockIdx.x * 256 + threadIdx.x; j < P; j += (long long)gridDim.x * 256) {
     const T a = pa ? pa[j] : (T)1;
     const T bj = pb ? pb[j] : (T)0;
-    const int ix = pb ? pidx[j] : 0;
+    const long long ix = pb ? pro_cidx(f, j) : 0;  // element index (pindex or folded cell) x ce
     if (vec) {
-      const V2* q = (const V2*)(pc + (long long)ix * nb);
+      const V2* q = (const V2*)(pc + ix);
 #pragma unroll 2
       for (int bp = 0; bp < nb / 2; ++bp) {
         const V2 c2 = q[bp];
@@ -715,8 +714,80 @@ __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __r
     for (int b = 0; b < nb; ++b) {
       T v = px[b * f.sx + j];
       if (pa) v *= a;
-      if (pb) v += bj * pc[b * f.sc + ix * f.ce];
+      if (pb) v += bj * pc[b * f.sc + ix];
       u[b * P + j] = v;
+    }
+  }
+}
+
+// Folded prologue of a batch (nft_hartley_fuse.pro_folded): one thread per
+// fundamental cell c reads the cell's bin (coalesced), gathers the dA run of
+// that bin for all items once, and forms u at every distinct mirror image
+// of c (2^d pixels, fewer on self-mirror axes) -- each image's x, A, xi0 and
+// u accesses are contiguous across the wave (forward or reversed).  Same
+// arithmetic per element as pro_batch_kernel (bitwise).
+template <typename T>
+__global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __restrict__ u, long long P, int nb,
+                                                       long long ncell) {
+  const T* __restrict__ px = (const T*)f.px;
+  const T* __restrict__ pa = (const T*)f.pa;
+  const T* __restrict__ pb = (const T*)f.pb;
+  const T* __restrict__ pc = (const T*)f.pc;
+  using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
+  const bool vec = f.ce == nb && f.sc == 1 && (nb & 1) == 0 && nb <= 8;
+  const int D = f.fnd;
+  for (long long c = (long long)blockIdx.x * 256 + threadIdx.x; c < ncell; c += (long long)gridDim.x * 256) {
+    unsigned cc[3], nn[3], rest = (unsigned)c;
+    for (int a = D - 1; a >= 0; --a) {
+      nn[a] = (unsigned)f.fn[a];
+      const unsigned h = nn[a] / 2 + 1;
+      const unsigned q = rest / h;
+      cc[a] = rest - q * h;
+      rest = q;
+    }
+    const long long ix = (long long)f.pidx[c] * f.ce;
+    T cv[8];
+    if (vec) {
+      const V2* q = (const V2*)(pc + ix);
+#pragma unroll
+      for (int bp = 0; bp < 4; ++bp)
+        if (2 * bp < nb) {
+          const V2 c2 = q[bp];
+          cv[2 * bp] = c2.x;
+          cv[2 * bp + 1] = c2.y;
+        }
+    }
+    // images: bit a of m flips axis a (skipped when that axis is self-mirror)
+    for (int m = 0; m < (1 << D); ++m) {
+      unsigned j = 0;
+      bool dup = false;
+      for (int a = 0; a < D; ++a) {
+        unsigned k = cc[a];
+        if ((m >> a) & 1) {
+          const unsigned km = (nn[a] - k) % nn[a];
+          if (km == k) dup = true;
+          k = km;
+        }
+        j = j * nn[a] + k;
+      }
+      if (dup) continue;
+      const T a = pa ? pa[j] : (T)1;
+      const T bj = pb[j];
+      if (vec) {
+        for (int b = 0; b < nb; ++b) {
+          T v = px[b * f.sx + j];
+          if (pa) v *= a;
+          v += bj * cv[b];
+          u[b * P + j] = v;
+        }
+      } else {
+        for (int b = 0; b < nb; ++b) {
+          T v = px[b * f.sx + j];
+          if (pa) v *= a;
+          v += bj * pc[b * f.sc + ix];
+          u[b * P + j] = v;
+        }
+      }
     }
   }
 }
@@ -761,8 +832,16 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     // one element per thread (no grid-stride chain of dependent gathers)
     static const long long cap = getenv("NFT_PRO_NBLK") ? atoll(getenv("NFT_PRO_NBLK")) : (1LL << 30);
     const unsigned nblk = (unsigned)std::min<long long>((f.P + 255) / 256, cap);
-    prof_mark(s, "pro_batch");
-    hipLaunchKernelGGL(pro_batch_kernel<T>, dim3(nblk), dim3(256), 0, s, f, u, f.P, f.nb);
+    if (f.fnd > 0 && f.pb) {
+      long long ncell = 1;
+      for (int a = 0; a < f.fnd; ++a) ncell *= f.fn[a] / 2 + 1;
+      prof_mark(s, "pro_fold");
+      hipLaunchKernelGGL(pro_fold_kernel<T>, dim3((unsigned)((ncell + 255) / 256)), dim3(256), 0, s, f, u, f.P, f.nb,
+                         ncell);
+    } else {
+      prof_mark(s, "pro_batch");
+      hipLaunchKernelGGL(pro_batch_kernel<T>, dim3(nblk), dim3(256), 0, s, f, u, f.P, f.nb);
+    }
     NFT_HIP_CHECK(hipGetLastError());
     fast::FuseArgs f2 = f;
     f2.pro = 0;
@@ -942,6 +1021,24 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     if (f.P < 0 || (f.P > 0 && f.pb && f.sc == 0)) {
       set_last_error("nft_hartley_fused: batch needs c_bstride");
       return NFT_ERR_ARG;
+    }
+    f.fnd = 0;
+    if (fz->pro_folded && f.pb) {
+      // item grid = the transform axes (in order); fold strides over n/2+1
+      long long per = 1;
+      for (int a : ax) per *= shape[a];
+      if ((int)ax.size() > 3 || per != (f.P > 0 ? f.P : per) ||
+          (f.P > 0 && ax.size() + 1 != (size_t)ndim) || (f.P == 0 && ax.size() != (size_t)ndim)) {
+        set_last_error("nft_hartley_fused: pro_folded needs the transform axes to span each item");
+        return NFT_ERR_ARG;
+      }
+      f.fnd = (int)ax.size();
+      long long st = 1;
+      for (int a = f.fnd - 1; a >= 0; --a) {
+        f.fn[a] = shape[ax[a]];
+        f.fs[a] = st;
+        st *= shape[ax[a]] / 2 + 1;
+      }
     }
     if ((f.pb && (!f.pc || !f.pidx)) || (f.out2 && !f.eb)) {
       set_last_error("nft_hartley_fused: incomplete fusion spec");

@@ -51,6 +51,9 @@ def _t(a):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=config.device())
 
 
+# folded prologue gather (NFT_PRO_FOLD=0 restores the per-pixel pindex gather)
+_PRO_FOLD = os.environ.get("NFT_PRO_FOLD", "1") != "0"
+
 class _AmplitudeModel:
     """Amplitude A(theta) on the PowerSpace, its JVP and VJP (B-sized math)."""
 
@@ -348,8 +351,19 @@ class CFJacobian(LinearOperator):
             da = torch.empty(m.amp.B, dtype=torch.float64, device=self.device)
             m.amp.native_jvp(self._const(), {k: v.contiguous() for k, v in t.items()}, da)
         out = torch.empty(self._afull.shape, dtype=self._afull.dtype, device=self.device)
-        pro = dict(a=self._afull, x=t[m.k_xi].contiguous(), b=self._xi0, c=da.contiguous(), index=m.bins.pindex)
+        pro = dict(a=self._afull, x=t[m.k_xi].contiguous(), b=self._xi0, **self._pro_bins(da.contiguous(), 1))
         return _native.hartley_fused(out, range(out.ndim), m.c_h, pro=pro, convention=hartley_convention_code())
+
+    def _pro_bins(self, da, k):
+        """bin operand of the forward prologue: with mirror-symmetric bins the
+        per-cell bin index of the fundamental cell (nft_hartley_fuse.pro_folded:
+        dA gathered once per mirror class, 2^d fewer scattered gathers, no
+        per-pixel index read), else the per-pixel pindex.  The values read
+        are the same either way."""
+        jb = self._m.jbins
+        if _PRO_FOLD and jb.fold is not None:
+            return dict(c=da, index=jb.fold["pindex"], fold=True)
+        return dict(c=da, index=self._m.bins.pindex)
 
     def _adjoint_t(self, g, out=None, d=None, shift=0.0):
         """g: grid tensor.  Returns dict key->tensor, or fills the `out` views
@@ -425,7 +439,7 @@ class CFJacobian(LinearOperator):
         da = torch.empty((B, k), dtype=torch.float64, device=self.device)
         amp.native_jvp_batched(const, D, off, da, interleave=True)
         s = torch.empty((k,) + grid, dtype=self._afull.dtype, device=self.device)
-        pro = dict(a=self._afull, x=D[0, xo:], b=self._xi0, c=da, index=m.bins.pindex)
+        pro = dict(a=self._afull, x=D[0, xo:], b=self._xi0, **self._pro_bins(da, k))
         _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
                               batch=dict(period=N, x=size, c=1, c_elem=k))
         g = W(s) if callable(W) else s * W
@@ -472,7 +486,7 @@ class CFJacobian(LinearOperator):
         amp.native_jvp_batched(const, D64, off, da, interleave=True)
         da32 = da.float()
         s = torch.empty((k,) + grid, dtype=torch.float32, device=self.device)
-        pro = dict(a=c32["afull"], x=D[0, xo:], b=c32["xi0"], c=da32, index=m.bins.pindex)
+        pro = dict(a=c32["afull"], x=D[0, xo:], b=c32["xi0"], **self._pro_bins(da32, k))
         _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
                               batch=dict(period=N, x=size, c=1, c_elem=k))
         if callable(W):

@@ -72,6 +72,9 @@ def _rowdots(pairs):
 
 
 # ------------------------------------------------------------------ stages
+from ..library.correlated_fields_simple import _PRO_FOLD  # noqa: E402
+
+
 class _CFStage:
     """The fused correlated-field model (library/correlated_fields_simple.py)
     evaluated on a batch of packed latent rows."""
@@ -146,6 +149,10 @@ class _CFStage:
             m.amp.native_jvp_batched(st["consts"][0], V, self.off, da, item_consts=st["dconst"].data_ptr())
             batch = dict(period=N, x=size, c=B, a=N, b=Xs.shape[1])
         pro = dict(a=st["afull"], x=V[0, self.xo:], b=Xs[0, self.xo:], c=da, index=m.bins.pindex)
+        jb = m.jbins
+        if _PRO_FOLD and jb.fold is not None:
+            # dA once per mirror class (correlated_fields_simple._pro_bins)
+            pro.update(index=jb.fold["pindex"], fold=True)
         _native.hartley_fused(out, self.axes, m.c_h, pro=pro, convention=hartley_convention_code(),
                               shape=out.shape, batch=batch)
         return out

@@ -71,9 +71,22 @@ class BinIndex:
         np.cumsum(np.bincount(f, minlength=self.nbin), out=offs[1:])
         cb = _chunk_bins(offs, self.nbin, f.size)
         return dict(shape=tuple(int(n) for n in shp), nf=int(f.size),
+                    pindex=torch.from_numpy(f.astype(np.int32)).to(device),   # cell -> bin
                     perm=torch.from_numpy(perm.astype(np.int32)).to(device),
                     offsets=torch.from_numpy(offs.astype(np.int32)).to(device),
                     order=(None, None, torch.from_numpy(cb).to(device)))
+
+    def gather_folded(self, src, k, interleaved=True):
+        """per-cell values of src on the fundamental cell: (nf, k) from the
+        (B, k) bin-major src, or (k, nf) from a (k, B) src -- the forward
+        Jacobian's bin gather done once per mirror class
+        (nft_hartley_fuse.pro_folded reads it by the cell of each pixel)"""
+        f = self.fold
+        if interleaved:
+            out = torch.empty((f["nf"], k), dtype=src.dtype, device=src.device)
+            return _native.bin_gather(src, f["pindex"], out, 1, f["nf"], self.nbin, k)
+        out = torch.empty((k, f["nf"]), dtype=src.dtype, device=src.device)
+        return _native.bin_gather(src, f["pindex"], out, k, f["nf"], self.nbin, 1)
 
     def scatter(self, w, out, pre):
         """out[p, b] = sum over the pixels of bin b of w[p, :] (w: pre grids,

@@ -892,6 +892,38 @@ def gen_optimize_kl():
     _save("optkl32.npz", d)
 
 
+FFTOP_CASES = [((16,), 0.1, None), ((12, 9), (0.4, 2.7), None), ((6, 8, 10), (1., 0.5, 3.), None),
+               ((10, 14), (0.7, 1.3), "batched")]
+
+
+def gen_fftop():
+    """FFTOperator volume factors and modes (harmonic_operators.py:34-123):
+    times / adjoint_times / inverse_times / adjoint_inverse_times from the
+    position and from the harmonic side, on RGSpaces with non-unit distances
+    and as one space of a product domain."""
+    rng = np.random.default_rng(77)
+    d = {}
+    for i, (shape, dist, kind) in enumerate(FFTOP_CASES):
+        sp = ift.RGSpace(shape, distances=dist)
+        if kind == "batched":
+            dom = ift.DomainTuple.make((ift.UnstructuredDomain(3), sp))
+            op = ift.FFTOperator(dom, space=1)
+        else:
+            dom = ift.DomainTuple.make(sp)
+            op = ift.FFTOperator(dom)
+        for side, D in (("pos", op.domain), ("harm", op.target)):
+            x = rng.standard_normal(D.shape) + 1j * rng.standard_normal(D.shape)
+            d[f"c{i}_{side}_x"] = x
+            f = ift.makeField(D, x)
+            if side == "pos":
+                d[f"c{i}_times"] = op.times(f).val
+                d[f"c{i}_adjinv"] = op.adjoint_inverse_times(f).val
+            else:
+                d[f"c{i}_adj"] = op.adjoint_times(f).val
+                d[f"c{i}_inv"] = op.inverse_times(f).val
+    _save("fftop.npz", d)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:

@@ -22,6 +22,10 @@ kk = torch.sqrt(kx[:, None] ** 2 + kx[None, :] ** 2)
 uq, idx = torch.unique(kk, return_inverse=True)
 idx = idx.to(torch.int32).contiguous()
 nbins = uq.numel()
+if len(sys.argv) > 2 and sys.argv[2] == "seq":   # coalesced stand-in: the gather cost alone
+    idx = (torch.arange(n * n, device=dev, dtype=torch.int64) * nbins // (n * n)).to(torch.int32).view(n, n)
+if len(sys.argv) > 2 and sys.argv[2] == "zero":
+    idx = torch.zeros((n, n), device=dev, dtype=torch.int32)
 c = torch.randn((nbins, k), generator=g, dtype=torch.float64).to(dev)
 size = P + 2 * nbins + 64
 X = torch.randn((k, size), generator=g, dtype=torch.float64).to(dev)
