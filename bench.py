@@ -118,15 +118,26 @@ def probe_setup(ift, lh, pos, k):
 
 def cg_iteration(lib, core, W, shift, bufs, k):
     """One batched CG iteration as FusedCGBatch.body runs it inside the timed
-    loop: direction, batched matvec, curvature, update (+ their folds)."""
+    loop: direction, batched matvec, curvature, update (+ their folds); the
+    curvature from the data space when the metric supports it (fused_cg)."""
     from nifty_amd import _native
+    from nifty_amd.minimization.fused_cg import _quad_blocks
     X, R, D, Q, SC, ws = bufs
     n = X.shape[1]
     P = _native.ptr
     s_ = _native.stream_ptr()
-    _native._check(lib.nft_cg_direction_batched(P(D), P(R), n, n, k, 0, P(SC), s_))
-    core.metric_flat_batch(D, Q, W, 0.0)
-    _native._check(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, 0, shift, P(SC), P(ws), s_))
+    nq = _quad_blocks(core, W, X.dtype)
+    if nq:
+        nbd = int(lib.nft_cg_dd_blocks(n))
+        PQ = torch.empty((k, nbd + nq), dtype=torch.float64, device=X.device)
+        _native._check(lib.nft_cg_direction_dd_batched(P(D), P(R), n, n, k, 0, P(SC), shift, P(PQ), nbd + nq, s_))
+        core.metric_flat_batch(D, Q, W, 0.0, qpart=PQ[:, nbd:])
+        _native._check(lib.nft_fold_partials(P(PQ), nbd + nq, k, P(SC[:, _native.CG_CURV:]), _native.CG_NSCALARS,
+                                             s_))
+    else:
+        _native._check(lib.nft_cg_direction_batched(P(D), P(R), n, n, k, 0, P(SC), s_))
+        core.metric_flat_batch(D, Q, W, 0.0)
+        _native._check(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, 0, shift, P(SC), P(ws), s_))
     _native._check(lib.nft_cg_update_batched(P(X), P(R), P(D), P(Q), 0, n, n, k, 0, shift, P(SC), P(ws), s_))
 
 
@@ -167,6 +178,7 @@ def byte_model(cf, R, k, n_lat):
         # perm over the cell, cell values (k), bin offsets, sums (k)
         "bin_scatter": 4 * Nf + 8 * k * Nf + 4 * B + 8 * k * B,
         "cg_dir_kernel": 3 * 8 * k * n_lat,
+        "cg_dir_dd": 3 * 8 * k * n_lat,
         "curv_partial": 2 * 8 * k * n_lat,
         # x, r, d, q in; x, r out (b is not streamed: the probe passes none,
         # and the sampling CG's value-blind controllers skip it too)

@@ -269,9 +269,36 @@ int nft_los_adjoint(const nft_los_plan* plan, const void* y, const void* colscal
 int nft_los_forward_batched(const nft_los_plan* plan, const void* x, const void* colscale,
                             const void* rowscale, void* y, void* ws, int dtype, double scale,
                             int nvec, int64_t x_stride, int64_t y_stride, hipStream_t stream);
+int nft_los_quad_blocks(const nft_los_plan* plan);
+int nft_los_forward_quad_batched(const nft_los_plan* plan, const void* x, const void* colscale,
+                                 const void* rowscale, void* y, void* ws, int dtype, double scale,
+                                 int nvec, int64_t x_stride, int64_t y_stride, double* qpart,
+                                 int64_t qstride, hipStream_t stream);
 int nft_los_adjoint_batched(const nft_los_plan* plan, const void* y, const void* colscale,
                             const void* rowscale, void* out, int dtype, double scale, int nvec,
                             int64_t y_stride, int64_t out_stride, hipStream_t stream);
+
+/* ---- curvature from the data space ------------------------------------ */
+/* For a CG metric shift * 1 + J^T R^T C R J (the LOS sampling metric) the
+ * curvature d.(shift d + q) equals shift * d.d + (R J d).C (R J d): the first
+ * term is summed while the direction is formed, the second while the LOS
+ * forward reduces each line, and nft_fold_partials adds the two partial
+ * vectors in a fixed order -- no separate pass over q and d.
+ *   nft_cg_direction_dd_batched: d = max(0, gamma/gprev) d + r (as
+ *     nft_cg_direction_batched) and part[rhs * pstride + b] = shift * (block b's
+ *     sum of d_i^2), b < nft_cg_dd_blocks(n).
+ *   nft_los_forward_quad_batched: nft_los_forward_batched plus
+ *     qpart[v * qstride + b] = sum over the lines of block b of t_l * y_l
+ *     (t = R (colscale x) before scale * rowscale, y the output), b <
+ *     nft_los_quad_blocks(plan).
+ *   nft_fold_partials: out[rhs * out_stride] = fixed-order sum of part[rhs * nb
+ *     .. rhs * nb + nb). */
+int nft_cg_dd_blocks(int64_t n);
+int nft_cg_direction_dd_batched(void* d, const void* r, int64_t n, int64_t vstride, int nrhs, int dtype,
+                                const double* sc, double shift, double* part, int64_t pstride,
+                                hipStream_t stream);
+int nft_fold_partials(const double* part, int nb, int nrhs, double* out, int64_t out_stride,
+                      hipStream_t stream);
 
 /* ---- correlated-field amplitude Jacobian ------------------------------ */
 /* Constants of the amplitude linearisation at one expansion point (all device

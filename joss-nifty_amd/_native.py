@@ -51,6 +51,11 @@ SIGNATURES = {
     "nft_los_adjoint": (_i, [_p, _p, _p, _p, _p, _i, _d, _p]),
     "nft_los_forward_batched": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p]),
     "nft_los_adjoint_batched": (_i, [_p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p]),
+    "nft_los_quad_blocks": (_i, [_p]),
+    "nft_los_forward_quad_batched": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p, _i64, _p]),
+    "nft_cg_dd_blocks": (_i, [_i64]),
+    "nft_cg_direction_dd_batched": (_i, [_p, _p, _i64, _i64, _i, _i, _p, _d, _p, _i64, _p]),
+    "nft_fold_partials": (_i, [_p, _i, _i, _p, _i64, _p]),
     "nft_prof_begin": (_i, [_i]),
     "nft_prof_end": (_i, [_p, _p, _i, ctypes.POINTER(_i)]),
     "nft_prof_label": (ctypes.c_char_p, [_i]),
@@ -376,6 +381,21 @@ def los_forward_batched(plan, x, y, colscale=None, rowscale=None, scale=1.0):
     _check(lib.nft_los_forward_batched(ctypes.byref(plan), ptr(x), ptr(colscale), ptr(rowscale), ptr(y), ptr(ws),
                                        dtype_code(x.dtype), float(scale), k, x[0].numel(), y[0].numel(),
                                        stream_ptr()))
+    return y
+
+
+def los_forward_quad_batched(plan, x, y, qpart, colscale=None, rowscale=None, scale=1.0):
+    """los_forward_batched plus the per-block partials of sum_l t_l y_l
+    (qpart: (k, >= nft_los_quad_blocks) fp64 rows, see nifty_amd.h)."""
+    lib = load()
+    require_device(x, y, colscale, rowscale)
+    if not (qpart.is_cuda and qpart.dtype == torch.float64 and qpart.stride(1) == 1 and qpart.shape[0] >= x.shape[0]):
+        raise NativeError("qpart: (k, >= nft_los_quad_blocks) fp64 device rows with unit element stride")
+    k = x.shape[0]
+    ws = workspace(k * lib.nft_los_workspace(ctypes.byref(plan)), x.device, "los")
+    _check(lib.nft_los_forward_quad_batched(ctypes.byref(plan), ptr(x), ptr(colscale), ptr(rowscale), ptr(y),
+                                            ptr(ws), dtype_code(x.dtype), float(scale), k, x[0].numel(),
+                                            y[0].numel(), ptr(qpart), qpart.stride(0), stream_ptr()))
     return y
 
 

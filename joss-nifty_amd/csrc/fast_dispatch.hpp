@@ -45,7 +45,12 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     long long nl = (KIND == K_R2C || KIND == K_H1D) ? (a.Ireal + 1) / 2 : a.g.O;
     ntiles = (nl + L - 1) / L;
   } else {
-    ntiles = a.g.O * a.g.M * ((a.g.I + L - 1) / L);
+    const long long LC = L >> a.los;
+    if (LC < 1 || (a.g.O & ((1LL << a.los) - 1)) != 0) {
+      set_last_error("strided pass: %d items per tile do not divide O = %lld", 1 << a.los, a.g.O);
+      return NFT_ERR_ARG;
+    }
+    ntiles = (a.g.O >> a.los) * a.g.M * ((a.g.I + LC - 1) / LC);
   }
   if (ntiles <= 0) return NFT_OK;
   if (ntiles > 0x7fffffffLL) {

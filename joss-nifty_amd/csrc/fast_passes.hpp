@@ -110,6 +110,7 @@ template <typename T> struct FastArgs {
   FuseArgs f;         // R2C/H1D: prologue; UNPACK/H1D: epilogue
   long long ntiles;   // tiles of the pass (set by the launcher)
   int bgroup;         // > 1: batch-aware XCD tile remap over this many items (set by the launcher)
+  int los;            // strided: log2 of the items (o) sharing one tile (their lines side by side)
 };
 
 // Batch-aware XCD remap.  Tiles are numbered batch-major (t = b * TR + r) and
@@ -198,11 +199,17 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       m = 0;
       i0 = 0;
     } else {
-      Tile tl = strided_tile<L>(g, t);
+      Tile tl = strided_tile<L>(g, t, a.los);
       o = tl.o;
       m = tl.m;
       i0 = tl.i0;
     }
+  };
+  // strided line l of the tile at (o, i0): its o and i (several items per tile: los > 0)
+  const int lcs = SHL - a.los;
+  auto line_oi = [&](long long o, long long i0, int l, long long& lo_, long long& li) {
+    lo_ = o + (l >> lcs);
+    li = i0 + (l & ((1 << lcs) - 1));
   };
   auto lx_of = [&](int r, int& l, int& x) {
     const int e = tid + r * NT;
@@ -245,8 +252,10 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           valid = (o + l) < g.O;
           off = (o + l) * g.in_so + (long long)x * g.in_sn;
         } else {
-          valid = (i0 + l) < g.I;
-          off = o * g.in_so + m * g.in_sm + (i0 + l) * g.in_si + (long long)x * g.in_sn;
+          long long lo_, li;
+          line_oi(o, i0, l, lo_, li);
+          valid = li < g.I && lo_ < g.O;
+          off = lo_ * g.in_so + m * g.in_sm + li * g.in_si + (long long)x * g.in_sn;
         }
         if (valid) v = in[off];
         if (a.conj_in) v.y = -v.y;
@@ -294,8 +303,10 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         if constexpr (ROWS) {
           if ((o + l) < g.O) out[(o + l) * g.out_so + (long long)x * g.out_sn] = v;
         } else {
-          if ((i0 + l) < g.I)
-            out[o * g.out_so + m * g.out_sm + (i0 + l) * g.out_si + (long long)x * g.out_sn] = v;
+          long long lo_, li;
+          line_oi(o, i0, l, lo_, li);
+          if (li < g.I && lo_ < g.O)
+            out[lo_ * g.out_so + m * g.out_sm + li * g.out_si + (long long)x * g.out_sn] = v;
         }
       }
     } else if constexpr (KIND == K_R2C || KIND == K_H1D) {
@@ -345,8 +356,10 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           valid = (o + l) < g.O;
           if (valid) u = unpack_line(a.desc, o + l, 0);
         } else {
-          valid = (i0 + l) < g.I;
-          if (valid) u = unpack_line(a.desc, o, i0 + l);
+          long long lo_, li;
+          line_oi(o, i0, l, lo_, li);
+          valid = li < g.I && lo_ < g.O;
+          if (valid) u = unpack_line(a.desc, lo_, li);
         }
         if (!valid) {
           u.valid = 0;

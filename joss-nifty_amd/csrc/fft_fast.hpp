@@ -134,13 +134,17 @@ struct Tile {
 };
 
 template <int L>
-__device__ __forceinline__ Tile strided_tile(const Lines& g, long long t) {
-  const long long tilesI = (g.I + L - 1) / L;
+__device__ __forceinline__ Tile strided_tile(const Lines& g, long long t, int los = 0) {
+  // los = log2 of the items (o) per tile: lines l -> (o + (l >> (log2 L - los)),
+  // i0 + (l mod (L >> los))); los = 0: all L lines in one o
+  const long long LC = L >> los;
+  const long long tilesI = (g.I + LC - 1) / LC;
   Tile r;
   long long om = t / tilesI;
-  r.i0 = (t - om * tilesI) * L;
-  r.o = om / g.M;
-  r.m = om - r.o * g.M;
+  r.i0 = (t - om * tilesI) * LC;
+  const long long og = om / g.M;
+  r.m = om - og * g.M;
+  r.o = og << los;
   return r;
 }
 

@@ -235,6 +235,39 @@ __global__ void cg_dir_kernel(T* __restrict__ d, const T* __restrict__ r, long l
     d[i] = bt * d[i] + r[i];
 }
 
+// d = max(0, gamma/gprev) d + r, and per-block partials of shift * d.d: the
+// identity part of the curvature d.(shift d + J^T W J d) when the J side
+// comes from the data space (nft_los_forward_quad_batched), so no pass over
+// q and d is needed for the curvature (nft_fold_partials sums both)
+template <typename T>
+__global__ __launch_bounds__(RED_NT) void cg_dir_dd_kernel(T* __restrict__ d, const T* __restrict__ r, long long n,
+                                                           long long vs, const double* __restrict__ sc,
+                                                           double shift, double* __restrict__ part,
+                                                           long long pstride) {
+  __shared__ double sh[RED_NT / 64];
+  sc += blockIdx.y * NFT_CG_NSCALARS;
+  part += (long long)blockIdx.y * pstride;
+  if (sc[NFT_CG_DONE] != 0.0) {
+    if (threadIdx.x == 0) part[blockIdx.x] = 0.0;
+    return;
+  }
+  d += (long long)blockIdx.y * vs;
+  r += (long long)blockIdx.y * vs;
+  double beta = sc[NFT_CG_GAMMA] / sc[NFT_CG_GPREV];
+  if (!(beta > 0.0)) beta = 0.0;
+  const T bt = (T)beta;
+  double v[1] = {0.0};
+  const long long stride = (long long)gridDim.x * RED_NT;
+#pragma unroll 4
+  for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
+    const T di = bt * d[i] + r[i];
+    d[i] = di;
+    v[0] += (double)di * (double)di;
+  }
+  block_sum<1>(v, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = shift * v[0];
+}
+
 // r = (ax + shift x) - b (exact residual refresh, conjugate_gradient.py:103-105
 // via QuadraticEnergy.__init__) and partial dots r.r, x.r, x.b
 template <typename T>
@@ -412,6 +445,60 @@ int nft_cg_direction_batched(void* d, const void* r, int64_t n, int64_t vstride,
     set_last_error("nft_cg_direction: bad dtype %d", dtype);
     return NFT_ERR_ARG;
   }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_dd_blocks(int64_t n) { return red_blocks(n); }
+
+int nft_cg_direction_dd_batched(void* d, const void* r, int64_t n, int64_t vstride, int nrhs, int dtype,
+                                const double* sc, double shift, double* part, int64_t pstride, hipStream_t stream) {
+  const int nb = red_blocks(n);
+  if (!part || pstride < nb || nrhs < 1) {
+    set_last_error("nft_cg_direction_dd: partials need pstride >= nft_cg_dd_blocks(n)");
+    return NFT_ERR_ARG;
+  }
+  const dim3 grid(nb, nrhs);
+  prof_mark(stream, "cg_dir_dd");
+  if (dtype == 0)
+    hipLaunchKernelGGL(cg_dir_dd_kernel<double>, grid, dim3(RED_NT), 0, stream, (double*)d, (const double*)r,
+                       (long long)n, (long long)vstride, sc, shift, part, (long long)pstride);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(cg_dir_dd_kernel<float>, grid, dim3(RED_NT), 0, stream, (float*)d, (const float*)r,
+                       (long long)n, (long long)vstride, sc, shift, part, (long long)pstride);
+  else {
+    set_last_error("nft_cg_direction_dd: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+// fixed-order sum of nb partials per RHS with one 1024-thread workgroup per
+// RHS (thread-strided sums, then the wave / LDS tree)
+__global__ __launch_bounds__(1024) void fold_wide(const double* __restrict__ part, int nb, double* __restrict__ out,
+                                                  long long ostride) {
+  __shared__ double sh[16];
+  part += (long long)blockIdx.x * nb;
+  double v = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 1024) v += part[b];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += sh[w];
+    out[(long long)blockIdx.x * ostride] = t;
+  }
+}
+
+int nft_fold_partials(const double* part, int nb, int nrhs, double* out, int64_t out_stride, hipStream_t stream) {
+  if (!part || !out || nb < 1 || nrhs < 1) {
+    set_last_error("nft_fold_partials: bad arguments");
+    return NFT_ERR_ARG;
+  }
+  prof_mark(stream, "fold_partials");
+  hipLaunchKernelGGL(fold_wide, dim3(nrhs), dim3(1024), 0, stream, part, nb, out, (long long)out_stride);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

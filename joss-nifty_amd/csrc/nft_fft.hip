@@ -495,6 +495,21 @@ static bool v2_multi_ok(const Geo& g, const std::vector<int>& ax) {
   return strided_supported(N0) || fourstep_supported(N0);
 }
 
+// Last (unpack) pass with an epilogue whose operands (A, xi0) are shared by
+// the batch: the lines of 2^los items sit side by side in one tile, so the
+// items' reads of the shared operands hit the same CU's cache instead of
+// going to HBM once per item (NFT_EPI_LO = los).  Measured slower at 4 x
+// 2048^2 (140 / 152 / 163 us for los = 0 / 1 / 2: the narrower column runs
+// of each item cost more than the re-reads save), so off by default
+static int epi_los(const fast::FuseArgs* fz, long long O) {
+  static const int want = getenv("NFT_EPI_LO") ? atoi(getenv("NFT_EPI_LO")) : 0;
+  if (!fz || !fz->epi || fz->P <= 0 || fz->nb < 2) return 0;
+  if ((fz->ea && fz->sea) || (fz->eb && fz->seb)) return 0;
+  int los = want;
+  while (los > 0 && (O % (1LL << los)) != 0) --los;
+  return los;
+}
+
 // r2c_done: the R2C row pass has already written the half spectra to ws
 template <typename T>
 static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector<int>& ax, int sigma,
@@ -601,6 +616,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
         a.f = *fz;
         a.f.pro = 0;
       }
+      a.los = epi_los(fz, O);
       return launch<T>(K_UNPACK, false, N, a, s);
     }
     int N1, N2;
@@ -647,6 +663,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
         a.f = *fz;
         a.f.pro = 0;
       }
+      a.los = epi_los(fz, O);
       return launch<T>(K_UNPACK, false, N2, a, s);
     }
   }

@@ -179,23 +179,30 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 
 // one wave per line of sight, all K vectors: the line's slots (boxes
 // ascending) hold K adjacent partials each; per vector a fixed-order sum
-// (lane strides, then a shuffle tree)
+// (lane strides, then a shuffle tree).  qpart (optional): per workgroup and
+// vector the sum over its 4 lines of t_l * y_l, t_l = (R (cs x))_l before
+// the row scale -- the data-space quadratic form x . (cs R^T (rs' R cs x))
+// of the sampling-metric middle (nft_los_forward_quad_batched)
 template <typename T>
 __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const double* __restrict__ part,
                                                       const T* __restrict__ rs, T* __restrict__ y, double scale,
-                                                      int K, long long ys) {
-  const int lane = threadIdx.x & 63;
-  const long long l = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (l >= p.nlos) return;
-  const int a = p.los_ptr[l], b = p.los_ptr[l + 1];
+                                                      int K, long long ys, double* __restrict__ qpart,
+                                                      long long qstride) {
+  __shared__ double qs[4][LOS_KMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long l = (long long)blockIdx.x * 4 + w;
+  const bool valid = l < p.nlos;
   double acc[LOS_KMAX];
 #pragma unroll
   for (int v = 0; v < LOS_KMAX; ++v) acc[v] = 0.0;
-  for (int k = a + lane; k < b; k += 64) {
-    const double* q = part + (long long)k * K;
+  if (valid) {
+    const int a = p.los_ptr[l], b = p.los_ptr[l + 1];
+    for (int k = a + lane; k < b; k += 64) {
+      const double* q = part + (long long)k * K;
 #pragma unroll
-    for (int v = 0; v < LOS_KMAX; ++v)
-      if (v < K) acc[v] += q[v];
+      for (int v = 0; v < LOS_KMAX; ++v)
+        if (v < K) acc[v] += q[v];
+    }
   }
 #pragma unroll
   for (int v = 0; v < LOS_KMAX; ++v) {
@@ -204,10 +211,21 @@ __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const doub
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
       if (lane == 0) {
-        s *= scale;
-        if (rs) s *= (double)rs[l];
-        y[v * ys + l] = (T)s;
+        double yy = 0.0;
+        if (valid) {
+          yy = s * scale;
+          if (rs) yy *= (double)rs[l];
+          y[v * ys + l] = (T)yy;
+        }
+        if (qpart) qs[w][v] = valid ? s * (double)(T)yy : 0.0;
       }
+    }
+  }
+  if (qpart) {
+    __syncthreads();
+    if (threadIdx.x < K) {
+      const int v = threadIdx.x;
+      qpart[v * qstride + blockIdx.x] = ((qs[0][v] + qs[1][v]) + qs[2][v]) + qs[3][v];
     }
   }
 }
@@ -356,7 +374,8 @@ static int kgroup(int k) { return k >= 8 ? 8 : (k >= 4 ? 4 : (k >= 2 ? 2 : 1)); 
 
 template <typename T>
 static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, const void* rs, void* y, double* part,
-                         double scale, int K, long long xs, long long ys, hipStream_t s) {
+                         double scale, int K, long long xs, long long ys, hipStream_t s, double* qpart = nullptr,
+                         long long qstride = 0) {
   prof_mark(s, "los_fwd_items");
   if (p->nitems > 0) {
     for (int v = 0; v < K;) {
@@ -375,7 +394,7 @@ static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, c
   prof_mark(s, "los_fwd_reduce");
   if (p->nlos > 0)
     hipLaunchKernelGGL(los_fwd_reduce<T>, dim3((unsigned)((p->nlos + 3) / 4)), dim3(256), 0, s, *p, part,
-                       (const T*)rs, (T*)y, scale, K, ys);
+                       (const T*)rs, (T*)y, scale, K, ys, qpart, qstride);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
@@ -440,6 +459,27 @@ int nft_los_forward_batched(const nft_los_plan* p, const void* x, const void* co
   if (dtype == 1)
     return los_forward_t<float>(p, x, colscale, rowscale, y, (double*)ws, scale, nvec, x_stride, y_stride, stream);
   set_last_error("nft_los_forward: bad dtype %d", dtype);
+  return NFT_ERR_ARG;
+}
+
+int nft_los_quad_blocks(const nft_los_plan* p) { return p ? (int)((p->nlos + 3) / 4) : 0; }
+
+int nft_los_forward_quad_batched(const nft_los_plan* p, const void* x, const void* colscale, const void* rowscale,
+                                 void* y, void* ws, int dtype, double scale, int nvec, int64_t x_stride,
+                                 int64_t y_stride, double* qpart, int64_t qstride, hipStream_t stream) {
+  int st = check_plan(p);
+  if (st != NFT_OK) return st;
+  if (nvec < 1 || nvec > LOS_KMAX || !qpart || qstride < nft_los_quad_blocks(p)) {
+    set_last_error("nft_los_forward_quad: 1 <= nvec <= %d, qpart with qstride >= nft_los_quad_blocks", LOS_KMAX);
+    return NFT_ERR_ARG;
+  }
+  if (dtype == 0)
+    return los_forward_t<double>(p, x, colscale, rowscale, y, (double*)ws, scale, nvec, x_stride, y_stride, stream,
+                                 qpart, qstride);
+  if (dtype == 1)
+    return los_forward_t<float>(p, x, colscale, rowscale, y, (double*)ws, scale, nvec, x_stride, y_stride, stream,
+                                qpart, qstride);
+  set_last_error("nft_los_forward_quad: bad dtype %d", dtype);
   return NFT_ERR_ARG;
 }
 

@@ -415,12 +415,14 @@ class CFJacobian(LinearOperator):
         return MultiField(self._domain, tuple(Field(self._domain[k], res[k].reshape(self._domain[k].shape))
                                               for k in self._domain.keys()))
 
-    def metric_flat_batch(self, D, Q, W, shift):
+    def metric_flat_batch(self, D, Q, W, shift, qpart=None):
         """Q[b] = shift * D[b] + J^T W J D[b] for the k rows of D (k, size),
         every stage launched once for the whole batch (nft_*_batched; the LOS
         matrix is streamed once for all rows).  Per row bitwise equal to
         metric_flat."""
         if D.dtype == torch.float32:
+            if qpart is not None:
+                raise NotImplementedError("data-space curvature partials: fp64 only")
             return self._metric_flat_batch32(D, Q, W, shift)
         m = self._m
         lay = self.layout
@@ -442,7 +444,7 @@ class CFJacobian(LinearOperator):
         pro = dict(a=self._afull, x=D[0, xo:], b=self._xi0, **self._pro_bins(da, k))
         _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
                               batch=dict(period=N, x=size, c=1, c_elem=k))
-        g = W(s) if callable(W) else s * W
+        g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
         g = g.contiguous()
         w = torch.empty((k,) + grid, dtype=self._afull.dtype, device=self.device)
         epi = dict(a=self._afull, b=self._xi0, out2=w)
@@ -515,12 +517,18 @@ class CFJacobian(LinearOperator):
             Q[:, o:o + n] = Q64[:, o:o + n]
         return Q
 
-    def metric_flat(self, d, q, W, shift):
-        """q = shift * d + J^T W J d on packed latent buffers (fused CG)."""
+    # metric_flat(_batch) take qpart (data-space curvature partials, fused_cg)
+    supports_quad = True
+
+    def metric_flat(self, d, q, W, shift, qpart=None):
+        """q = shift * d + J^T W J d on packed latent buffers (fused CG).
+        qpart: partials of the quadratic form (J d).W(J d), from a middle W
+        that supports it (W.quad_blocks)."""
         lay = self.layout
         dv = lay.views(d)
         s = self._times_t(dv)
-        self._adjoint_t(W(s) if callable(W) else s * W, lay.views(q), dv, shift)
+        g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
+        self._adjoint_t(g, lay.views(q), dv, shift)
 
 
 class _CorrelatedFieldModel(Operator):

@@ -8,6 +8,8 @@ The triplets are then regrouped into the box-blocked layout of
 csrc/nft_los.hip (box_plan): per 256-pixel box, the runs of each line (for
 R x) and the runs of each pixel (for R^T y), float32 weights as in the
 reference, fp64 accumulation in fixed order."""
+import ctypes
+
 import numpy as np
 import torch
 from scipy.special import erfc
@@ -336,8 +338,21 @@ class LOSResponse(LinearOperator):
                 cast[dt] = (None if drf is None else drf.to(dt), None if cv is None else cv.to(dt))
             return cast[dt]
 
-        def middle(s):
+        def middle(s, qpart=None):
+            """qpart (optional, (k, >= quad_blocks) fp64): per-block partials of
+            the quadratic form s . middle(s), from the data space"""
             drf, cv = scales(s.dtype)
+            if qpart is not None:
+                k = s.shape[0] if s.dim() > len(shape) else 1
+                v = s.reshape(k, npix).contiguous()
+                y = torch.empty((k, nlos), dtype=v.dtype, device=v.device)
+                out = torch.empty((k,) + tuple(shape), dtype=v.dtype, device=v.device)
+                for a in range(0, k, LOS_KMAX):
+                    b = min(k, a + LOS_KMAX)
+                    _native.los_forward_quad_batched(plan, v[a:b], y[a:b], qpart[a:b], colscale=drf, rowscale=cv,
+                                                     scale=scale)
+                    _native.los_adjoint_batched(plan, y[a:b], out[a:b].view(b - a, npix), rowscale=drf)
+                return out if s.dim() > len(shape) else out[0]
             if s.dim() > len(shape):
                 # batch of right-hand sides along a leading axis (batched CG):
                 # the matrix is streamed once per launch for all of them
@@ -358,6 +373,7 @@ class LOSResponse(LinearOperator):
             return out
         middle.supports_batch = True
         middle.supports_fp32 = True
+        middle.quad_blocks = int(_native.load().nft_los_quad_blocks(ctypes.byref(plan)))
         return middle
 
     @property

@@ -121,6 +121,36 @@ def _reads_value(ctl):
                 and getattr(ctl, "_history", None) is None and not trace.active())
 
 
+# data-space curvature (nifty_amd.h "curvature from the data space"):
+# shift * d.d summed while d is formed, (J d).W(J d) while the LOS forward
+# reduces its lines -- no curvature pass over q and d (NFT_CURV_DATA=0: off)
+CURV_DATA = os.environ.get("NFT_CURV_DATA", "1") != "0"
+
+
+def _count_only(ctl):
+    """True for a controller whose decisions depend on the iteration count
+    alone (GradientNormController without tolerances): then the curvature may
+    be formed from the data space.  Equal in exact arithmetic, its rounding
+    differs from the reference's d.(A d), and long CG trajectories are
+    chaotic in the last bits, so value-driven controllers (energy deltas,
+    gradient-norm tolerances) keep the reference's formula and with it the
+    reference's decisions (tests/test_geovi_trace_gpu.py)."""
+    from .iteration_controllers import GradientNormController
+    return (type(ctl) is GradientNormController and ctl._tol_abs_gradnorm is None
+            and ctl._tol_rel_gradnorm is None)
+
+
+def _quad_blocks(core, W, dtype, controllers=()):
+    """partials per RHS of the metric's data-space quadratic form, or 0"""
+    if not CURV_DATA or dtype != torch.float64 or not callable(W):
+        return 0
+    if not all(_count_only(c) for c in controllers):
+        return 0
+    if not getattr(core, "supports_quad", False):
+        return 0
+    return int(getattr(W, "quad_blocks", 0) or 0)
+
+
 def _worth_capturing(ctl, niter, min_left=4):
     """Capture only if the controller's iteration limit leaves at least
     `min_left` more iterations to replay (short solves, e.g. NewtonCG's first
@@ -205,12 +235,23 @@ class FusedCG:
         if gamma == 0:
             return energy, ctl.CONVERGED
 
+        nq = _quad_blocks(core, self.W, x.dtype, (ctl,))
+        if nq:
+            nbd = int(lib.nft_cg_dd_blocks(n))
+            pq = torch.empty((1, nbd + nq), dtype=torch.float64, device=x.device)
+
         def body(with_dir):
             s_ = _native.stream_ptr()
-            if with_dir:
-                chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), s_))
-            core.metric_flat(d, q, self.W, 0.0)
-            chk(lib.nft_cg_curv(P(d), P(q), n, dt, sh, P(sc), P(ws), s_))
+            if with_dir and nq:
+                # the same kernels and partial layout as FusedCGBatch with k = 1
+                chk(lib.nft_cg_direction_dd_batched(P(d), P(r), n, n, 1, dt, P(sc), sh, P(pq), nbd + nq, s_))
+                core.metric_flat(d, q, self.W, 0.0, qpart=pq[:, nbd:])
+                chk(lib.nft_fold_partials(P(pq), nbd + nq, 1, P(sc[_native.CG_CURV:]), _native.CG_NSCALARS, s_))
+            else:
+                if with_dir:
+                    chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), s_))
+                core.metric_flat(d, q, self.W, 0.0)
+                chk(lib.nft_cg_curv(P(d), P(q), n, dt, sh, P(sc), P(ws), s_))
             chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, sh, P(sc), P(ws), s_))
 
         graph = None
@@ -417,12 +458,24 @@ class FusedCGBatch(FusedCG):
         # b is not streamed and the value is computed on demand.
         Bu = Bv if any(_reads_value(c) for c in self.controllers) else None
 
+        nq = _quad_blocks(core, self.W, X.dtype, self.controllers)
+        if nq:
+            nbd = int(lib.nft_cg_dd_blocks(n))
+            PQ = torch.empty((k, nbd + nq), dtype=torch.float64, device=dev)
+
         def body(with_dir):
             s_ = _native.stream_ptr()
-            if with_dir:
-                chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), s_))
-            core.metric_flat_batch(D, Q, self.W, 0.0)
-            chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), s_))
+            if with_dir and nq:
+                # curvature from the data space: shift * d.d partials while d is
+                # formed, (J d).W(J d) partials in the LOS forward reduce
+                chk(lib.nft_cg_direction_dd_batched(P(D), P(Rr), n, n, k, dt, P(SC), sh, P(PQ), nbd + nq, s_))
+                core.metric_flat_batch(D, Q, self.W, 0.0, qpart=PQ[:, nbd:])
+                chk(lib.nft_fold_partials(P(PQ), nbd + nq, k, P(SC[:, _native.CG_CURV:]), NS, s_))
+            else:
+                if with_dir:
+                    chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), s_))
+                core.metric_flat_batch(D, Q, self.W, 0.0)
+                chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), s_))
             chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws), s_))
 
         graph = None
