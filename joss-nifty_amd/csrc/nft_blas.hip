@@ -330,6 +330,24 @@ __global__ void cg_residual_finalize(const double* __restrict__ part, int nb, do
   }
 }
 
+// fixed-order sum of nb partials per RHS with one 1024-thread workgroup per
+// RHS (thread-strided sums, then the wave / LDS tree)
+__global__ __launch_bounds__(1024) void fold_wide(const double* __restrict__ part, int nb, double* __restrict__ out,
+                                                  long long ostride) {
+  __shared__ double sh[16];
+  part += (long long)blockIdx.x * nb;
+  double v = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 1024) v += part[b];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += sh[w];
+    out[(long long)blockIdx.x * ostride] = t;
+  }
+}
+
 }  // namespace nft
 
 using namespace nft;
@@ -472,24 +490,6 @@ int nft_cg_direction_dd_batched(void* d, const void* r, int64_t n, int64_t vstri
   }
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
-}
-
-// fixed-order sum of nb partials per RHS with one 1024-thread workgroup per
-// RHS (thread-strided sums, then the wave / LDS tree)
-__global__ __launch_bounds__(1024) void fold_wide(const double* __restrict__ part, int nb, double* __restrict__ out,
-                                                  long long ostride) {
-  __shared__ double sh[16];
-  part += (long long)blockIdx.x * nb;
-  double v = 0.0;
-  for (int b = threadIdx.x; b < nb; b += 1024) v += part[b];
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < 16; ++w) t += sh[w];
-    out[(long long)blockIdx.x * ostride] = t;
-  }
 }
 
 int nft_fold_partials(const double* part, int nb, int nrhs, double* out, int64_t out_stride, hipStream_t stream) {
