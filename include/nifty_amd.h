@@ -277,6 +277,23 @@ int nft_los_forward_quad_batched(const nft_los_plan* plan, const void* x, const 
 int nft_los_adjoint_batched(const nft_los_plan* plan, const void* y, const void* colscale,
                             const void* rowscale, void* out, int dtype, double scale, int nvec,
                             int64_t y_stride, int64_t out_stride, hipStream_t stream);
+/* Pixel-side scales per vector: the pixel-side factor of vector v is
+ * colscale + v * colscale_stride (forward) / rowscale + v * rowscale_stride
+ * (adjoint); stride 0 shares one factor as in the _batched forms.  This is the
+ * chain rule of a pointwise nonlinearity in front of the response
+ * (R diag(f'(s_v)) in the forward, diag(f'(s_v)) R^T in the adjoint,
+ * src/operators/operator.py:_OpChain jacobians), applied while the pixels are
+ * loaded / stored instead of as a separate pass over every vector.
+ * nft_los_forward_ex takes the optional curvature partials of
+ * nft_los_forward_quad_batched (qpart = NULL: none). */
+int nft_los_forward_ex(const nft_los_plan* plan, const void* x, const void* colscale,
+                       int64_t colscale_stride, const void* rowscale, void* y, void* ws, int dtype,
+                       double scale, int nvec, int64_t x_stride, int64_t y_stride, double* qpart,
+                       int64_t qstride, hipStream_t stream);
+int nft_los_adjoint_ex(const nft_los_plan* plan, const void* y, const void* colscale,
+                       const void* rowscale, int64_t rowscale_stride, void* out, int dtype,
+                       double scale, int nvec, int64_t y_stride, int64_t out_stride,
+                       hipStream_t stream);
 
 /* ---- curvature from the data space ------------------------------------ */
 /* For a CG metric shift * 1 + J^T R^T C R J (the LOS sampling metric) the

@@ -53,6 +53,8 @@ SIGNATURES = {
     "nft_los_adjoint_batched": (_i, [_p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p]),
     "nft_los_quad_blocks": (_i, [_p]),
     "nft_los_forward_quad_batched": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p, _i64, _p]),
+    "nft_los_forward_ex": (_i, [_p, _p, _p, _i64, _p, _p, _p, _i, _d, _i, _i64, _i64, _p, _i64, _p]),
+    "nft_los_adjoint_ex": (_i, [_p, _p, _p, _p, _i64, _p, _i, _d, _i, _i64, _i64, _p]),
     "nft_cg_dd_blocks": (_i, [_i64]),
     "nft_cg_direction_dd_batched": (_i, [_p, _p, _i64, _i64, _i, _i, _p, _d, _p, _i64, _p]),
     "nft_fold_partials": (_i, [_p, _i, _i, _p, _i64, _p]),
@@ -407,6 +409,57 @@ def los_adjoint_batched(plan, y, out, colscale=None, rowscale=None, scale=1.0):
     _check(lib.nft_los_adjoint_batched(ctypes.byref(plan), ptr(y), ptr(colscale), ptr(rowscale), ptr(out),
                                        dtype_code(y.dtype), float(scale), k, y[0].numel(), out[0].numel(),
                                        stream_ptr()))
+    return out
+
+
+def _pixel_scale_stride(sc, k, npix):
+    """Per-vector pixel-side scale: (k, npix) rows -> stride npix, one shared
+    (npix,) / (1, npix) vector -> 0."""
+    if sc is None:
+        return 0
+    if not sc.is_contiguous():
+        raise NativeError("pixel scale: contiguous tensor required")
+    if sc.numel() == npix:
+        return 0
+    if sc.numel() == k * npix:
+        return npix
+    raise NativeError(f"pixel scale: {sc.numel()} elements for {k} vectors of {npix} pixels")
+
+
+def los_forward_ex(plan, x, y, colscale=None, rowscale=None, scale=1.0, qpart=None):
+    """y[b] = scale * rowscale * R (colscale[b] * x[b]): colscale one shared
+    pixel vector or one per vector (nft_los_forward_ex); qpart as in
+    los_forward_quad_batched or None."""
+    lib = load()
+    require_device(x, y, colscale, rowscale)
+    k = x.shape[0]
+    if not (x.is_contiguous() and y.is_contiguous()):
+        raise NativeError("los_forward_ex: contiguous x and y required")
+    css = _pixel_scale_stride(colscale, k, x[0].numel())
+    qs = 0
+    if qpart is not None:
+        if not (qpart.is_cuda and qpart.dtype == torch.float64 and qpart.stride(1) == 1
+                and qpart.shape[0] >= k):
+            raise NativeError("qpart: (k, >= nft_los_quad_blocks) fp64 device rows with unit element stride")
+        qs = qpart.stride(0)
+    ws = workspace(k * lib.nft_los_workspace(ctypes.byref(plan)), x.device, "los")
+    _check(lib.nft_los_forward_ex(ctypes.byref(plan), ptr(x), ptr(colscale), css, ptr(rowscale), ptr(y), ptr(ws),
+                                  dtype_code(x.dtype), float(scale), k, x[0].numel(), y[0].numel(), ptr(qpart), qs,
+                                  stream_ptr()))
+    return y
+
+
+def los_adjoint_ex(plan, y, out, colscale=None, rowscale=None, scale=1.0):
+    """out[b] = scale * rowscale[b] * R^T (colscale * y[b]): the pixel-side
+    rowscale one shared vector or one per vector (nft_los_adjoint_ex)."""
+    lib = load()
+    require_device(y, out, colscale, rowscale)
+    k = y.shape[0]
+    if not (y.is_contiguous() and out.is_contiguous()):
+        raise NativeError("los_adjoint_ex: contiguous y and out required")
+    rss = _pixel_scale_stride(rowscale, k, out[0].numel())
+    _check(lib.nft_los_adjoint_ex(ctypes.byref(plan), ptr(y), ptr(colscale), ptr(rowscale), rss, ptr(out),
+                                  dtype_code(y.dtype), float(scale), k, y[0].numel(), out[0].numel(), stream_ptr()))
     return out
 
 

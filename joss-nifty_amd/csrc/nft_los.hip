@@ -62,7 +62,7 @@ struct BoxGeom {
 template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __restrict__ x,
                                                      const T* __restrict__ cs, double* __restrict__ part,
-                                                     long long xs, int pk) {
+                                                     long long xs, int pk, long long css) {
   // every product is rounded before it is summed, in all K variants alike
   // (no FMA contraction): batched results are bitwise the K = 1 results
 #pragma clang fp contract(off)
@@ -90,13 +90,13 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       lv[i] = k < n ? p.ent_loc[e0 + k] : 0;
     }
   }
-  const double c = (ok && cs) ? (double)cs[px] : 1.0;
+  // column (pixel-side) scale: shared by the vectors (css = 0) or one per vector
 #pragma unroll
   for (int b = 0; b < K; ++b) {
     double v = 0.0;
     if (ok) {
       v = (double)x[b * xs + px];
-      if (cs) v *= c;
+      if (cs) v *= (double)cs[b * css + px];
     }
     u[b][t] = v;
   }
@@ -238,7 +238,7 @@ template <typename T, typename IDX, int K>
 __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* __restrict__ lidx,
                                                      const T* __restrict__ yv, const T* __restrict__ cs,
                                                      const T* __restrict__ rs, T* __restrict__ out, double scale,
-                                                     long long ys, long long os) {
+                                                     long long ys, long long os, long long rss) {
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CH_A / 256;
   // line table: 256 lines per vector cover every box of an 8-bit-index plan
@@ -346,11 +346,11 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   bool ok;
   const long long px = g.pixel(box, t, ok);
   if (ok) {
-    const double r = rs ? (double)rs[px] : 1.0;
+    // pixel-side scale: shared by the vectors (rss = 0) or one per vector
 #pragma unroll
     for (int v = 0; v < K; ++v) {
       double o = acc[v] * scale;
-      if (rs) o *= r;
+      if (rs) o *= (double)rs[v * rss + px];
       out[v * os + px] = (T)o;
     }
   }
@@ -358,15 +358,16 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
 
 template <typename T, int K>
 static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* part, long long xs, int pk,
-                        hipStream_t s) {
-  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, pk);
+                        long long css, hipStream_t s) {
+  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, pk,
+                     css);
 }
 
 template <typename T, typename IDX, int K>
 static void adj_boxes_k(const nft_los_plan* p, const IDX* li, const T* y, const T* cs, const T* rs, T* out,
-                        double scale, long long ys, long long os, hipStream_t s) {
+                        double scale, long long ys, long long os, long long rss, hipStream_t s) {
   hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), dim3((unsigned)p->nbox), dim3(256), 0, s, *p, li, y, cs, rs, out,
-                     scale, ys, os);
+                     scale, ys, os, rss);
 }
 
 // vectors are processed in groups of 8 / 4 / 2 / 1 (template sizes)
@@ -375,18 +376,19 @@ static int kgroup(int k) { return k >= 8 ? 8 : (k >= 4 ? 4 : (k >= 2 ? 2 : 1)); 
 template <typename T>
 static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, const void* rs, void* y, double* part,
                          double scale, int K, long long xs, long long ys, hipStream_t s, double* qpart = nullptr,
-                         long long qstride = 0) {
+                         long long qstride = 0, long long css = 0) {
   prof_mark(s, "los_fwd_items");
   if (p->nitems > 0) {
     for (int v = 0; v < K;) {
       const int g = kgroup(K - v);
       const T* xv = (const T*)x + v * xs;
+      const T* cv = cs ? (const T*)cs + v * css : nullptr;
       double* pv = part + v;  // slot-major partials, K per slot
       switch (g) {
-        case 8: fwd_items_k<T, 8>(p, xv, (const T*)cs, pv, xs, K, s); break;
-        case 4: fwd_items_k<T, 4>(p, xv, (const T*)cs, pv, xs, K, s); break;
-        case 2: fwd_items_k<T, 2>(p, xv, (const T*)cs, pv, xs, K, s); break;
-        default: fwd_items_k<T, 1>(p, xv, (const T*)cs, pv, xs, K, s); break;
+        case 8: fwd_items_k<T, 8>(p, xv, cv, pv, xs, K, css, s); break;
+        case 4: fwd_items_k<T, 4>(p, xv, cv, pv, xs, K, css, s); break;
+        case 2: fwd_items_k<T, 2>(p, xv, cv, pv, xs, K, css, s); break;
+        default: fwd_items_k<T, 1>(p, xv, cv, pv, xs, K, css, s); break;
       }
       v += g;
     }
@@ -401,16 +403,18 @@ static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, c
 
 template <typename T, typename IDX>
 static void los_adjoint_idx(const nft_los_plan* p, const IDX* li, const void* y, const void* cs, const void* rs,
-                            void* out, double scale, int K, long long ys, long long os, hipStream_t s) {
+                            void* out, double scale, int K, long long ys, long long os, hipStream_t s,
+                            long long rss = 0) {
   for (int v = 0; v < K;) {
     const int g = kgroup(K - v);
     const T* yv = (const T*)y + v * ys;
+    const T* rv = rs ? (const T*)rs + v * rss : nullptr;
     T* ov = (T*)out + v * os;
     switch (g) {
-      case 8: adj_boxes_k<T, IDX, 8>(p, li, yv, (const T*)cs, (const T*)rs, ov, scale, ys, os, s); break;
-      case 4: adj_boxes_k<T, IDX, 4>(p, li, yv, (const T*)cs, (const T*)rs, ov, scale, ys, os, s); break;
-      case 2: adj_boxes_k<T, IDX, 2>(p, li, yv, (const T*)cs, (const T*)rs, ov, scale, ys, os, s); break;
-      default: adj_boxes_k<T, IDX, 1>(p, li, yv, (const T*)cs, (const T*)rs, ov, scale, ys, os, s); break;
+      case 8: adj_boxes_k<T, IDX, 8>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, s); break;
+      case 4: adj_boxes_k<T, IDX, 4>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, s); break;
+      case 2: adj_boxes_k<T, IDX, 2>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, s); break;
+      default: adj_boxes_k<T, IDX, 1>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, s); break;
     }
     v += g;
   }
@@ -418,13 +422,14 @@ static void los_adjoint_idx(const nft_los_plan* p, const IDX* li, const void* y,
 
 template <typename T>
 static int los_adjoint_t(const nft_los_plan* p, const void* y, const void* cs, const void* rs, void* out, double scale,
-                         int K, long long ys, long long os, hipStream_t s) {
+                         int K, long long ys, long long os, hipStream_t s, long long rss = 0) {
   if (p->nbox <= 0) return NFT_OK;
   prof_mark(s, "los_adj_boxes");
   if (p->lidx8)
-    los_adjoint_idx<T, unsigned char>(p, (const unsigned char*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s);
+    los_adjoint_idx<T, unsigned char>(p, (const unsigned char*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s, rss);
   else
-    los_adjoint_idx<T, unsigned short>(p, (const unsigned short*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s);
+    los_adjoint_idx<T, unsigned short>(p, (const unsigned short*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s,
+                                       rss);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
@@ -508,6 +513,45 @@ int nft_los_adjoint_batched(const nft_los_plan* p, const void* y, const void* co
 int nft_los_adjoint(const nft_los_plan* p, const void* y, const void* colscale, const void* rowscale, void* out,
                     int dtype, double scale, hipStream_t stream) {
   return nft_los_adjoint_batched(p, y, colscale, rowscale, out, dtype, scale, 1, 0, 0, stream);
+}
+
+int nft_los_forward_ex(const nft_los_plan* p, const void* x, const void* colscale, int64_t colscale_stride,
+                       const void* rowscale, void* y, void* ws, int dtype, double scale, int nvec, int64_t x_stride,
+                       int64_t y_stride, double* qpart, int64_t qstride, hipStream_t stream) {
+  int st = check_plan(p);
+  if (st != NFT_OK) return st;
+  if (nvec < 1 || nvec > LOS_KMAX || colscale_stride < 0 || (qpart && qstride < nft_los_quad_blocks(p))) {
+    set_last_error("nft_los_forward_ex: 1 <= nvec <= %d, colscale_stride >= 0, qstride >= nft_los_quad_blocks",
+                   LOS_KMAX);
+    return NFT_ERR_ARG;
+  }
+  if (dtype == 0)
+    return los_forward_t<double>(p, x, colscale, rowscale, y, (double*)ws, scale, nvec, x_stride, y_stride, stream,
+                                 qpart, qstride, colscale_stride);
+  if (dtype == 1)
+    return los_forward_t<float>(p, x, colscale, rowscale, y, (double*)ws, scale, nvec, x_stride, y_stride, stream,
+                                qpart, qstride, colscale_stride);
+  set_last_error("nft_los_forward_ex: bad dtype %d", dtype);
+  return NFT_ERR_ARG;
+}
+
+int nft_los_adjoint_ex(const nft_los_plan* p, const void* y, const void* colscale, const void* rowscale,
+                       int64_t rowscale_stride, void* out, int dtype, double scale, int nvec, int64_t y_stride,
+                       int64_t out_stride, hipStream_t stream) {
+  int st = check_plan(p);
+  if (st != NFT_OK) return st;
+  if (nvec < 1 || nvec > LOS_KMAX || rowscale_stride < 0) {
+    set_last_error("nft_los_adjoint_ex: 1 <= nvec <= %d, rowscale_stride >= 0", LOS_KMAX);
+    return NFT_ERR_ARG;
+  }
+  if (dtype == 0)
+    return los_adjoint_t<double>(p, y, colscale, rowscale, out, scale, nvec, y_stride, out_stride, stream,
+                                 rowscale_stride);
+  if (dtype == 1)
+    return los_adjoint_t<float>(p, y, colscale, rowscale, out, scale, nvec, y_stride, out_stride, stream,
+                                rowscale_stride);
+  set_last_error("nft_los_adjoint_ex: bad dtype %d", dtype);
+  return NFT_ERR_ARG;
 }
 
 }  // extern "C"

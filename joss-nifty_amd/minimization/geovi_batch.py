@@ -41,6 +41,8 @@ draw_samples keeps the per-sample path."""
 import copy
 import math
 
+import os
+
 import numpy as np
 import torch
 
@@ -180,6 +182,11 @@ class _CFStage:
         return Q
 
 
+# a pointwise stage in front of the LOS response rides in the LOS kernels
+# (NFT_FUSE_PTW=0: separate multiplies, for measurement)
+_FUSE_PTW = os.environ.get("NFT_FUSE_PTW", "1") != "0"
+
+
 class _PtwStage:
     def __init__(self, name, args, kwargs):
         from ..pointwise import ptw_dict
@@ -238,7 +245,16 @@ class _LinStage:
         return _los_adj(self.v, G.reshape(k, -1)).reshape((k,) + self.dshape)
 
 
-def _los_fwd(R, V):
+def _pixel_rows(d, k, a, b):
+    """rows a:b of a pointwise derivative shared (1 row) or one per vector"""
+    if d is None:
+        return None
+    return d.reshape(1, -1) if d.shape[0] == 1 else d.reshape(k, -1)[a:b]
+
+
+def _los_fwd(R, V, d=None):
+    """R (d * V) row by row; d (the derivative of a pointwise stage in front
+    of R) is applied as the kernel loads the pixels (nft_los_forward_ex)."""
     from ..library.los_response import LOS_KMAX
     plan = R._box_plan()
     k = V.shape[0]
@@ -246,11 +262,16 @@ def _los_fwd(R, V):
     y = torch.empty((k, R.target.shape[0]), dtype=V.dtype, device=V.device)
     for a in range(0, k, LOS_KMAX):
         b = min(k, a + LOS_KMAX)
-        _native.los_forward_batched(plan, V[a:b], y[a:b])
+        if d is None:
+            _native.los_forward_batched(plan, V[a:b], y[a:b])
+        else:
+            _native.los_forward_ex(plan, V[a:b], y[a:b], colscale=_pixel_rows(d, k, a, b))
     return y
 
 
-def _los_adj(R, Y):
+def _los_adj(R, Y, d=None):
+    """d * R^T Y row by row (d applied as the pixels are stored,
+    nft_los_adjoint_ex)."""
     from ..library.los_response import LOS_KMAX
     plan = R._box_plan()
     k = Y.shape[0]
@@ -259,7 +280,10 @@ def _los_adj(R, Y):
     out = torch.empty((k, npix), dtype=Y.dtype, device=Y.device)
     for a in range(0, k, LOS_KMAX):
         b = min(k, a + LOS_KMAX)
-        _native.los_adjoint_batched(plan, Y[a:b], out[a:b])
+        if d is None:
+            _native.los_adjoint_batched(plan, Y[a:b], out[a:b])
+        else:
+            _native.los_adjoint_ex(plan, Y[a:b], out[a:b], rowscale=_pixel_rows(d, k, a, b))
     return out
 
 
@@ -314,17 +338,41 @@ class Pipeline:
         """batch state from [(states, row), ...]"""
         return [type(s).stack([(st[j], r) for st, r in rows]) for j, s in enumerate(self.stages)]
 
+    def _fused_ptw_los(self, i, d, U):
+        """stage i pointwise and stage i + 1 the LOS response: the derivative
+        d is folded into the LOS kernel's pixel loads / stores"""
+        if i + 1 >= len(self.stages) or not isinstance(self.stages[i], _PtwStage):
+            return False
+        nx = self.stages[i + 1]
+        if not (isinstance(nx, _LinStage) and nx.kind == "los" and _FUSE_PTW):
+            return False
+        return d.dtype == U.dtype and d.is_contiguous() and d.shape[0] in (1, U.shape[0])
+
     def jvp(self, states, V):
         U = self.stages[0].jvp(states[0], V)
-        for s, st in zip(self.stages[1:], states[1:]):
+        i = 1
+        while i < len(self.stages):
+            s, st = self.stages[i], states[i]
+            if self._fused_ptw_los(i, st, U):
+                U = _los_fwd(self.stages[i + 1].v, U.reshape(U.shape[0], -1), st)
+                i += 2
+                continue
             U = s.jvp(st, U)
+            i += 1
         return U
 
     def vjp(self, states, G, Q):
         """Q (k, size) zero-padded packed rows = J^T G"""
         U = G
-        for s, st in zip(reversed(self.stages[1:]), reversed(states[1:])):
+        i = len(self.stages) - 1
+        while i >= 1:
+            s, st = self.stages[i], states[i]
+            if i >= 2 and self._fused_ptw_los(i - 1, states[i - 1], U):
+                U = _los_adj(s.v, U.reshape(U.shape[0], -1), states[i - 1]).reshape((U.shape[0],) + s.dshape)
+                i -= 2
+                continue
             U = s.vjp(st, U)
+            i -= 1
         return self.stages[0].vjp(states[0], U, Q)
 
 
