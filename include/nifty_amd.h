@@ -363,6 +363,34 @@ int nft_amp_vjp_batched(const nft_amp_const* c, const nft_amp_const* item_consts
                         const nft_amp_out* out, double* ws, int nrhs, int64_t lat_stride,
                         int64_t g_stride, hipStream_t stream);
 
+/* Amplitude model (device pointers, fp64; M = B - 2): the operator chain of
+ * src/library/correlated_fields_simple.py:85-127 (_Normalization, _SlopeRemover,
+ * _TwoLogIntegrations, the LognormalTransform / NormalTransform scalings) with
+ * its fixed per-bin vectors:
+ *   vslope = relative log k-lengths, sc = vslope / vslope[B-1], mult = mode
+ *   multiplicity                                          [B]
+ *   lv = log-volumes, sqrt_lv = sqrt(lv), shift0 = lv^2/12  [M]  (has_flex) */
+typedef struct nft_amp_model {
+  const double *vslope, *sc, *mult, *lv, *sqrt_lv, *shift0;
+  double lm_f, ls_f, mu_s, sig_s, lm_x, ls_x, lm_a, ls_a, lm_o, ls_o, total_volume;
+  int64_t B;
+  int has_flex, has_asp, has_zm;
+} nft_amp_model;
+/* Amplitude value at nrow latent points (lat pointers advance by lat_stride
+ * per row; a NULL key is an absent model component) and, for each row, the
+ * constants of its linearisation: a[r * a_stride + b] (B values),
+ * buf[r * buf_stride ..] = c0, sf, p0, p1, p2 [M each], Qf, Qa, mspec, An [B
+ * each] (buf_stride >= nft_amp_forward_buf(B)), and item_consts[r] -- a DEVICE
+ * nft_amp_const pointing into buf and the model, with fl, S and zm set: the
+ * item_consts argument of nft_amp_jvp_batched / nft_amp_vjp_batched.  No value
+ * goes through the host.  ws: nrow * nft_amp_workspace(B) bytes. */
+int64_t nft_amp_forward_buf(int64_t B);
+int nft_amp_forward_batched(const nft_amp_model* model, const double* x_fl, const double* x_sl,
+                            const double* x_flex, const double* x_asp, const double* x_zm,
+                            const double* x_spec, int64_t lat_stride, int nrow, double* a,
+                            int64_t a_stride, double* buf, int64_t buf_stride,
+                            nft_amp_const* item_consts, double* ws, hipStream_t stream);
+
 /* ---- launch profiler (HIP events) -------------------------------------- */
 /* Between nft_prof_begin and nft_prof_end every hot-path kernel launch
  * records a HIP event on its stream just before the launch; nft_prof_end

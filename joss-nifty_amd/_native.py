@@ -66,6 +66,8 @@ SIGNATURES = {
     "nft_amp_vjp": (_i, [_p, _p, _p, _p, _p]),
     "nft_amp_jvp_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _p]),
     "nft_amp_vjp_batched": (_i, [_p, _p, _p, _p, _p, _i, _i64, _i64, _p]),
+    "nft_amp_forward_buf": (_i64, [_i64]),
+    "nft_amp_forward_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _p, _i64, _p, _i64, _p, _p, _p]),
 }
 
 
@@ -92,6 +94,14 @@ class AmpConst(ctypes.Structure):
     _fields_ = [(n, _p) for n in ("c0", "sf", "p0", "p1", "p2", "lv", "vslope", "sc", "Qf", "Qa",
                                   "mspec", "An")] + \
                [(n, _d) for n in ("fl", "S", "ls_f", "sig_s", "zm", "ls_o", "total_volume")] + \
+               [("B", _i64), ("has_flex", _i), ("has_asp", _i), ("has_zm", _i)]
+
+
+class AmpModel(ctypes.Structure):
+    """nft_amp_model (include/nifty_amd.h)."""
+    _fields_ = [(n, _p) for n in ("vslope", "sc", "mult", "lv", "sqrt_lv", "shift0")] + \
+               [(n, _d) for n in ("lm_f", "ls_f", "mu_s", "sig_s", "lm_x", "ls_x", "lm_a", "ls_a", "lm_o", "ls_o",
+                                  "total_volume")] + \
                [("B", _i64), ("has_flex", _i), ("has_asp", _i), ("has_zm", _i)]
 
 

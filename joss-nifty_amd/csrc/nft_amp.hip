@@ -986,6 +986,270 @@ static int vjp_fused_try(const AmpConst& c, const AmpConst* dcs, int nr, const A
   return NFT_OK;
 }
 
+
+// ------------------------------------------------------------------ forward
+// Amplitude value and linearisation constants at nrow latent points
+// (correlated_fields_simple.py:81-125 of the reference): per row
+//   F1  sf, sq0, the coefficient vectors c0/p0/p1/p2; block scans of
+//       at1 = xs1*sf (value) and p2 (flexibility constant)
+//   F2  t = (c + c_prev)/2*lv + x0 for the three TwoLog chains (value, Qf, Qa
+//       -- Qa's first cumsum is of zeros); block scans of t
+//   F3  SlopeRemove, apre = vslope*avgsl + ..., spec = exp(apre),
+//       mspec = mult*spec, partial sums of mspec
+//   F4  S = sum of the partials in index order, An = sqrt(spec/S), a, and the
+//       row's device nft_amp_const.
+// Operation order per element follows the tensor formulation op by op
+// (contraction off), so the values are those of the torch restatement up to
+// the summation order of the scans and of S.
+using AmpModel = nft_amp_model;
+
+struct FwdLat {
+  const double *fl, *sl, *flex, *asp, *zm, *spec;
+  long long ls;
+};
+
+struct FwdScal {
+  double fl, avgsl, flex, asp, zm;
+};
+
+__device__ __forceinline__ FwdScal fwd_scalars(const AmpModel& m, const FwdLat& x, long long r) {
+#pragma clang fp contract(off)
+  FwdScal v;
+  const long long o = r * x.ls;
+  v.fl = exp(m.lm_f + m.ls_f * x.fl[o]);
+  v.avgsl = m.mu_s + m.sig_s * x.sl[o];
+  v.flex = m.has_flex ? exp(m.lm_x + m.ls_x * x.flex[o]) : 0.0;
+  v.asp = m.has_asp ? exp(m.lm_a + m.ls_a * x.asp[o]) : 0.0;
+  v.zm = m.has_zm ? exp(m.lm_o + m.ls_o * x.zm[o]) : 0.0;
+  return v;
+}
+
+// per-row views of the output buffer and the workspace
+struct FwdRow {
+  double *c0, *sf, *p0, *p1, *p2, *Qf, *Qa, *mspec, *An;
+  double *loc_v, *loc_f, *loc_a, *tot1v, *tot1f, *tot2v, *tot2f, *tot2a, *part;
+};
+
+__device__ __forceinline__ FwdRow fwd_row(long long B, double* buf, long long bs, double* ws, long long wsd,
+                                          long long r) {
+  const long long M = B - 2;
+  const int nbM = (int)((M + ABLK - 1) / ABLK) > 0 ? (int)((M + ABLK - 1) / ABLK) : 1;
+  FwdRow w;
+  double* b = buf + r * bs;
+  w.c0 = b;
+  w.sf = b + M;
+  w.p0 = b + 2 * M;
+  w.p1 = b + 3 * M;
+  w.p2 = b + 4 * M;
+  w.Qf = b + 5 * M;
+  w.Qa = w.Qf + B;
+  w.mspec = w.Qa + B;
+  w.An = w.mspec + B;
+  double* q = ws + r * wsd;
+  w.loc_v = q;
+  w.loc_f = q + M;
+  w.loc_a = q + 2 * M;
+  w.tot1v = q + 3 * M;
+  w.tot1f = w.tot1v + nbM + 1;
+  w.tot2v = w.tot1f + nbM + 1;
+  w.tot2f = w.tot2v + nbM + 1;
+  w.tot2a = w.tot2f + nbM + 1;
+  w.part = w.tot2a + nbM + 1;
+  return w;
+}
+
+// F1 (first scans in the Qf / Qa slots of buf: F3 overwrites them)
+__global__ __launch_bounds__(AT) void amp_fwd_1(AmpModel m, FwdLat x, double* buf, long long bs, double* ws,
+                                                long long wsd) {
+#pragma clang fp contract(off)
+  __shared__ double sh[2 * AT];
+  const long long r = blockIdx.y;
+  const FwdScal sc = fwd_scalars(m, x, r);
+  const FwdRow w = fwd_row(m.B, buf, bs, ws, wsd, r);
+  const double* xs = x.spec + r * x.ls;
+  const long long M = m.B - 2;
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x;
+  double va[AE], vf[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long j = j0 + (long long)k * AT;
+    va[k] = vf[k] = 0.0;
+    if (j < M) {
+      const double sf = m.sqrt_lv[j] * sc.flex;
+      const double sq0 = m.has_asp ? sqrt(m.shift0[j] + sc.asp) : sqrt(m.shift0[j]);
+      w.sf[j] = sf;
+      w.c0[j] = sf * sq0;
+      w.p0[j] = xs[j] * sf * (m.ls_x * sq0);
+      w.p2[j] = xs[M + j] * sf * m.ls_x;
+      if (m.has_asp) w.p1[j] = xs[j] * sf * sc.asp * m.ls_a / (2. * sq0);
+      va[k] = xs[M + j] * sf;
+      vf[k] = w.p2[j];
+    }
+  }
+  const double ta = block_scan<false>(va, sh);
+  const double tf = block_scan<false>(vf, sh);
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long j = j0 + (long long)k * AT;
+    if (j < M) {
+      w.Qf[j] = va[k];
+      w.Qa[j] = vf[k];
+    }
+  }
+  if (threadIdx.x == 0) {
+    w.tot1v[blockIdx.x] = ta;
+    w.tot1f[blockIdx.x] = tf;
+  }
+}
+
+// F2
+__global__ __launch_bounds__(AT) void amp_fwd_2(AmpModel m, FwdLat x, double* buf, long long bs, double* ws,
+                                                long long wsd) {
+#pragma clang fp contract(off)
+  __shared__ double sh[2 * AT];
+  const long long r = blockIdx.y;
+  const FwdRow w = fwd_row(m.B, buf, bs, ws, wsd, r);
+  const double* xs = x.spec + r * x.ls;
+  const long long M = m.B - 2;
+  const int nb = (int)((M + ABLK - 1) / ABLK);
+  const double cv = carry_in<false>(w.tot1v, blockIdx.x, nb, sh);
+  const double cf = carry_in<false>(w.tot1f, blockIdx.x, nb, sh);
+  const long long j0 = (long long)blockIdx.x * ABLK + threadIdx.x;
+  double tv[AE], tf[AE], ta[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long j = j0 + (long long)k * AT;
+    tv[k] = tf[k] = ta[k] = 0.0;
+    if (j < M) {
+      const double sf = w.sf[j];
+      const double u1 = xs[M + j] * sf;
+      const double c1 = w.Qf[j] + cv;
+      const double at0 = m.has_asp ? xs[j] * sf * sqrt(m.shift0[j] + fwd_scalars(m, x, r).asp)
+                                   : xs[j] * sf * sqrt(m.shift0[j]);
+      tv[k] = (c1 + (c1 - u1)) / 2 * m.lv[j] + at0;
+      const double c2 = w.Qa[j] + cf;
+      tf[k] = (c2 + (c2 - w.p2[j])) / 2 * m.lv[j] + w.p0[j];
+      ta[k] = m.has_asp ? w.p1[j] : 0.0;
+    }
+  }
+  const double Tv = block_scan<false>(tv, sh);
+  const double Tf = block_scan<false>(tf, sh);
+  const double Ta = block_scan<false>(ta, sh);
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long j = j0 + (long long)k * AT;
+    if (j < M) {
+      w.loc_v[j] = tv[k];
+      w.loc_f[j] = tf[k];
+      w.loc_a[j] = ta[k];
+    }
+  }
+  if (threadIdx.x == 0) {
+    w.tot2v[blockIdx.x] = Tv;
+    w.tot2f[blockIdx.x] = Tf;
+    w.tot2a[blockIdx.x] = Ta;
+  }
+}
+
+// F3
+__global__ __launch_bounds__(AT) void amp_fwd_3(AmpModel m, FwdLat x, double* buf, long long bs, double* ws,
+                                                long long wsd) {
+#pragma clang fp contract(off)
+  __shared__ double sh[2 * AT];
+  const long long r = blockIdx.y;
+  const FwdScal sc = fwd_scalars(m, x, r);
+  const FwdRow w = fwd_row(m.B, buf, bs, ws, wsd, r);
+  const long long B = m.B, M = B - 2;
+  const int nbM = m.has_flex ? (int)((M + ABLK - 1) / ABLK) : 0;
+  const long long b0 = (long long)blockIdx.x * ABLK;
+  const int blk0 = b0 >= 2 ? (int)((b0 - 2) / ABLK) : 0;
+  double T[3] = {0, 0, 0}, c0_[3] = {0, 0, 0}, c1_[3] = {0, 0, 0};
+  double* tot[3] = {w.tot2v, w.tot2f, w.tot2a};
+  double* loc[3] = {w.loc_v, w.loc_f, w.loc_a};
+  if (m.has_flex) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      T[q] = carry_in<false>(tot[q], nbM, nbM, sh);
+      c0_[q] = carry_in<false>(tot[q], blk0, nbM, sh);
+      c1_[q] = c0_[q] + (blk0 < nbM ? tot[q][blk0] : 0.0);
+    }
+  }
+  double acc = 0;
+  for (int k = 0; k < AE; ++k) {
+    const long long b = b0 + threadIdx.x + (long long)k * AT;
+    if (b >= B) continue;
+    double tl[3] = {0, 0, 0};
+    if (m.has_flex && b >= 2) {
+      const long long j = b - 2;
+      const bool first = (int)(j / ABLK) == blk0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) tl[q] = loc[q][j] + (first ? c0_[q] : c1_[q]);
+    }
+    double apre = m.vslope[b] * sc.avgsl;
+    if (m.has_flex) {
+      apre = apre + (tl[0] - T[0] * m.sc[b]);
+      w.Qf[b] = tl[1] - T[1] * m.sc[b];
+      if (m.has_asp) w.Qa[b] = tl[2] - T[2] * m.sc[b];
+    }
+    const double spec = exp(apre);
+    const double ms = m.mult[b] * spec;
+    w.mspec[b] = ms;
+    w.An[b] = spec;
+    acc += ms;
+  }
+  const double t = block_total(acc, sh);
+  if (threadIdx.x == 0) w.part[blockIdx.x] = t;
+}
+
+// F4
+__global__ __launch_bounds__(AT) void amp_fwd_4(AmpModel m, FwdLat x, double* buf, long long bs, double* ws,
+                                                long long wsd, double* a, long long as, nft_amp_const* dcs,
+                                                int npart) {
+#pragma clang fp contract(off)
+  __shared__ double sh[2 * AT];
+  const long long r = blockIdx.y;
+  const FwdScal sc = fwd_scalars(m, x, r);
+  const FwdRow w = fwd_row(m.B, buf, bs, ws, wsd, r);
+  double s = 0;
+  for (int i = threadIdx.x; i < npart; i += AT) s += w.part[i];
+  const double S = block_total(s, sh);
+  const double inv = 1. / S;
+  double* ar = a + r * as;
+  for (long long b = (long long)blockIdx.x * AT + threadIdx.x; b < m.B; b += (long long)gridDim.x * AT) {
+    const double An = sqrt(w.An[b] * inv);
+    w.An[b] = An;
+    ar[b] = (b == 0 ? (m.has_zm ? sc.zm : 0.0) : sc.fl * An) * m.total_volume;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    nft_amp_const c;
+    const bool fx = m.has_flex != 0;
+    c.c0 = fx ? w.c0 : nullptr;
+    c.sf = fx ? w.sf : nullptr;
+    c.p0 = fx ? w.p0 : nullptr;
+    c.p1 = fx && m.has_asp ? w.p1 : nullptr;
+    c.p2 = fx ? w.p2 : nullptr;
+    c.lv = fx ? m.lv : nullptr;
+    c.vslope = m.vslope;
+    c.sc = m.sc;
+    c.Qf = fx ? w.Qf : nullptr;
+    c.Qa = fx && m.has_asp ? w.Qa : nullptr;
+    c.mspec = w.mspec;
+    c.An = w.An;
+    c.fl = sc.fl;
+    c.S = S;
+    c.ls_f = m.ls_f;
+    c.sig_s = m.sig_s;
+    c.zm = m.has_zm ? sc.zm : 0.0;
+    c.ls_o = m.has_zm ? m.ls_o : 0.0;
+    c.total_volume = m.total_volume;
+    c.B = m.B;
+    c.has_flex = m.has_flex;
+    c.has_asp = m.has_asp;
+    c.has_zm = m.has_zm;
+    dcs[r] = c;
+  }
+}
+
 }  // namespace nft
 
 using namespace nft;
@@ -1088,6 +1352,40 @@ int nft_amp_barrier_probe(int nbar, int G, hipStream_t s) {
   if (G <= 0) G = resident_cap((const void*)amp_vjp_fused<4, false>);
   prof_mark(s, "amp_barrier_probe");
   hipLaunchKernelGGL(amp_barrier_probe, dim3(G), dim3(AT), 0, s, nbar);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int64_t nft_amp_forward_buf(int64_t B) { return 5 * (B - 2) + 4 * B; }
+
+int nft_amp_forward_batched(const nft_amp_model* model, const double* x_fl, const double* x_sl, const double* x_flex,
+                            const double* x_asp, const double* x_zm, const double* x_spec, int64_t lat_stride,
+                            int nrow, double* a, int64_t a_stride, double* buf, int64_t buf_stride,
+                            nft_amp_const* item_consts, double* ws, hipStream_t s) {
+  if (!model || nrow < 1 || model->B < 3 || !x_fl || !x_sl || !a || !buf || !item_consts || !ws ||
+      buf_stride < nft_amp_forward_buf(model->B) || a_stride < (nrow > 1 ? model->B : 0) ||
+      (model->has_flex && (!x_flex || !x_spec)) || (model->has_asp && (!x_asp || !model->has_flex)) ||
+      (model->has_zm && !x_zm)) {
+    set_last_error("nft_amp_forward_batched: invalid arguments");
+    return NFT_ERR_ARG;
+  }
+  const AmpModel& m = *model;
+  const long long B = m.B, M = B - 2;
+  const long long wsd = (long long)(nft_amp_workspace(B) / sizeof(double));
+  const FwdLat x{x_fl, x_sl, x_flex, x_asp, x_zm, x_spec, lat_stride};
+  const unsigned ny = (unsigned)nrow;
+  const int nbM = nblk(M, ABLK), nbB = nblk(B, ABLK);
+  if (m.has_flex) {
+    prof_mark(s, "amp_fwd_1");
+    hipLaunchKernelGGL(amp_fwd_1, dim3(nbM, ny), dim3(AT), 0, s, m, x, buf, buf_stride, ws, wsd);
+    prof_mark(s, "amp_fwd_2");
+    hipLaunchKernelGGL(amp_fwd_2, dim3(nbM, ny), dim3(AT), 0, s, m, x, buf, buf_stride, ws, wsd);
+  }
+  prof_mark(s, "amp_fwd_3");
+  hipLaunchKernelGGL(amp_fwd_3, dim3(nbB, ny), dim3(AT), 0, s, m, x, buf, buf_stride, ws, wsd);
+  prof_mark(s, "amp_fwd_4");
+  hipLaunchKernelGGL(amp_fwd_4, dim3(std::min(nblk(B, AT), 1024), ny), dim3(AT), 0, s, m, x, buf, buf_stride, ws,
+                     wsd, a, (long long)a_stride, item_consts, nbB);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

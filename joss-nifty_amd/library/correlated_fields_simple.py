@@ -51,8 +51,49 @@ def _t(a):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=config.device())
 
 
+# amplitude forward + linearisation constants in native passes
+# (NFT_AMP_NATIVE_FWD=0: the torch formulation, for A/B comparisons)
+_AMP_NATIVE_FWD = os.environ.get("NFT_AMP_NATIVE_FWD", "1") != "0"
+
 # folded prologue gather (NFT_PRO_FOLD=0 restores the per-pixel pindex gather)
 _PRO_FOLD = os.environ.get("NFT_PRO_FOLD", "1") != "0"
+
+class AmpLin:
+    """Linearisation points of the amplitude made on the device
+    (_AmplitudeModel.forward_rows): values a (k, B), the per-row constant
+    vectors (buf) and k device nft_amp_const structs pointing into them.
+    Stands in for the host AmpConst wherever the native JVP/VJP takes one:
+    `host` carries B and the flags for the launch geometry, the kernels read
+    every value from the device structs (item_consts)."""
+
+    def __init__(self, amp, a, buf, dconst, k):
+        import ctypes
+        self.a, self.buf, self.dconst, self.k = a, buf, dconst, k
+        self.keep = None
+        self.size = ctypes.sizeof(_native.AmpConst)
+        h = _native.AmpConst()
+        h.B = amp.B
+        h.has_flex, h.has_asp, h.has_zm = int(amp.has_flex), int(amp.has_asp), int(amp.has_zm)
+        self.host = h
+        self._rep = {}
+
+    @property
+    def B(self):
+        return self.host.B
+
+    def row_bytes(self, r):
+        return self.dconst[r * self.size:(r + 1) * self.size]
+
+    def items(self, k, row=0):
+        """device pointer of k consecutive structs: row `row` shared by k
+        right-hand sides"""
+        if self.k == 1 and k == 1:
+            return self.dconst.data_ptr()
+        key = (k, row)
+        if key not in self._rep:
+            self._rep[key] = self.row_bytes(row).repeat(k)
+        return self._rep[key].data_ptr()
+
 
 class _AmplitudeModel:
     """Amplitude A(theta) on the PowerSpace, its JVP and VJP (B-sized math)."""
@@ -181,7 +222,10 @@ class _AmplitudeModel:
     def native_const(self, c):
         """Per-bin constants of the linearisation at the expansion point for
         the native JVP/VJP kernels (nft_amp_*, include/nifty_amd.h).  Returns
-        (AmpConst, keep-alive dict of the device tensors it points to)."""
+        (AmpConst, keep-alive dict of the device tensors it points to); an
+        AmpLin from forward_rows is its own constant set."""
+        if isinstance(c, AmpLin):
+            return c, None
         keep = {}
         if self.has_flex:
             xs, sf, sq0 = c["xs"], c["sf"], c["sq0"]
@@ -210,6 +254,60 @@ class _AmplitudeModel:
         k.has_flex, k.has_asp, k.has_zm = int(self.has_flex), int(self.has_asp), int(self.has_zm)
         return k, keep
 
+    # ------------------------------------------------- native forward
+    def native_model(self):
+        """nft_amp_model of this amplitude (fixed per-bin vectors + scalars)"""
+        nm = getattr(self, "_nm", None)
+        if nm is None:
+            k = _native.AmpModel()
+            keep = dict(vslope=self.vslope, sc=self.sc, mult=self.mult)
+            if self.has_flex:
+                keep.update(lv=self.lv, sqrt_lv=self.sqrt_lv, shift0=self.shift0)
+            keep = {n: v.contiguous() for n, v in keep.items()}
+            for n in ("vslope", "sc", "mult", "lv", "sqrt_lv", "shift0"):
+                setattr(k, n, keep[n].data_ptr() if n in keep else None)
+            k.lm_f, k.ls_f, k.mu_s, k.sig_s = self.lm_f, self.ls_f, self.mu_s, self.sig_s
+            if self.has_flex:
+                k.lm_x, k.ls_x = self.lm_x, self.ls_x
+            if self.has_asp:
+                k.lm_a, k.ls_a = self.lm_a, self.ls_a
+            if self.has_zm:
+                k.lm_o, k.ls_o = self.lm_o, self.ls_o
+            k.total_volume = self.total_vol
+            k.B = self.B
+            k.has_flex, k.has_asp, k.has_zm = int(self.has_flex), int(self.has_asp), int(self.has_zm)
+            nm = self._nm = (k, keep)
+        return nm[0]
+
+    def forward_rows(self, at, k, lat_stride, device):
+        """Amplitude values and linearisation constants at k latent points in
+        one native pass (nft_amp_forward_batched): at(key) -> device pointer of
+        row 0's key or None, rows lat_stride elements apart.  Nothing is read
+        back to the host."""
+        import ctypes
+        lib = _native.load()
+        nbuf = int(lib.nft_amp_forward_buf(self.B))
+        a = torch.empty((k, self.B), dtype=torch.float64, device=device)
+        buf = torch.empty((k, nbuf), dtype=torch.float64, device=device)
+        dconst = torch.empty(k * ctypes.sizeof(_native.AmpConst), dtype=torch.uint8, device=device)
+        ws = _native.workspace(k * lib.nft_amp_workspace(self.B), device, "amp")
+        P = ctypes.c_void_p
+        _native._check(lib.nft_amp_forward_batched(
+            ctypes.byref(self.native_model()), P(at(self.k_fl)), P(at(self.k_sl)), P(at(self.k_flex)),
+            P(at(self.k_asp)), P(at(self.k_zm)), P(at(self.k_spec)), int(lat_stride), k, P(a.data_ptr()), self.B,
+            P(buf.data_ptr()), nbuf, P(dconst.data_ptr()), P(ws.data_ptr()), _native.stream_ptr()))
+        return AmpLin(self, a, buf, dconst, k)
+
+    def forward_native(self, lat):
+        """forward_rows at one latent point given as a dict key -> tensor"""
+        vals = {kk: v.contiguous() for kk, v in lat.items() if kk in self.domain_dict}
+
+        def at(key):
+            return vals[key].data_ptr() if key in vals else None
+        lin = self.forward_rows(at, 1, 0, next(iter(vals.values())).device)
+        lin.keep = vals
+        return lin
+
     def _ptrs(self, D, off):
         """base pointers of the amplitude keys of packed row 0 of D (or None)"""
         def at(key):
@@ -224,6 +322,10 @@ class _AmplitudeModel:
         import ctypes
         at = self._ptrs(D, off)
         k, size = D.shape
+        if isinstance(const, AmpLin):
+            if item_consts is None:
+                item_consts = const.items(k)
+            const = const.host
         lib = _native.load()
         ws = _native.workspace(k * lib.nft_amp_workspace(self.B), D.device, "amp")
         P = ctypes.c_void_p
@@ -237,6 +339,10 @@ class _AmplitudeModel:
         """Q[b] amplitude keys = shift * D[b] + J_amp^T g[b]."""
         import ctypes
         k, size = Q.shape
+        if isinstance(const, AmpLin):
+            if item_consts is None:
+                item_consts = const.items(k)
+            const = const.host
         lib = _native.load()
         ws = _native.workspace(k * lib.nft_amp_workspace(self.B), Q.device, "amp")
         atq = self._ptrs(Q, off)
@@ -254,6 +360,21 @@ class _AmplitudeModel:
         return Q
 
     def native_jvp(self, const, t, da):
+        if isinstance(const, AmpLin):
+            import ctypes
+            lib = _native.load()
+            ws = _native.workspace(lib.nft_amp_workspace(self.B), da.device, "amp")
+            P = ctypes.c_void_p
+
+            def ptr(key):
+                v = t.get(key)
+                return P(v.data_ptr() if v is not None else None)
+            _native.require_device(da, *[v for v in t.values()])
+            _native._check(lib.nft_amp_jvp_batched(
+                ctypes.byref(const.host), P(const.items(1)), ptr(self.k_fl), ptr(self.k_sl), ptr(self.k_flex),
+                ptr(self.k_asp), ptr(self.k_zm), ptr(self.k_spec), P(da.data_ptr()), P(ws.data_ptr()), 1, 0, 0, 1,
+                _native.stream_ptr()))
+            return da
         g = t.get
         _native.amp_jvp(const, g(self.k_fl), g(self.k_sl), g(self.k_flex), g(self.k_asp),
                         g(self.k_zm), g(self.k_spec), da)
@@ -270,6 +391,15 @@ class _AmplitudeModel:
                 if d is not None and shift != 0.0:
                     setattr(o, "d" + short, d[key].data_ptr())
         o.shift = float(shift)
+        if isinstance(const, AmpLin):
+            import ctypes
+            lib = _native.load()
+            ws = _native.workspace(lib.nft_amp_workspace(self.B), g.device, "amp")
+            _native.require_device(g)
+            _native._check(lib.nft_amp_vjp_batched(
+                ctypes.byref(const.host), ctypes.c_void_p(const.items(1)), ctypes.c_void_p(g.data_ptr()),
+                ctypes.byref(o), ctypes.c_void_p(ws.data_ptr()), 1, 0, 0, _native.stream_ptr()))
+            return out
         _native.amp_vjp(const, g, o)
         return out
 
@@ -559,7 +689,13 @@ class _CorrelatedFieldModel(Operator):
         return self._layout
 
     def _value(self, lat):
-        a, c = self.amp.forward(lat)
+        if _AMP_TORCH or not _AMP_NATIVE_FWD:
+            a, c = self.amp.forward(lat)
+        else:
+            # amplitude and its linearisation constants on the device in one
+            # pass (nft_amp_forward_batched), no host round trip
+            c = self.amp.forward_native(lat)
+            a = c.a[0]
         afull = torch.empty(self.harmonic_partner.shape, dtype=a.dtype, device=a.device)
         b = self.bins
         _native.bin_gather(a, b.pindex, afull, 1, b.npix, b.nbin, 1)

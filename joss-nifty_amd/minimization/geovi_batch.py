@@ -77,6 +77,17 @@ def _rowdots(pairs):
 from ..library.correlated_fields_simple import _PRO_FOLD  # noqa: E402
 
 
+def _items(st, k):
+    """device nft_amp_const array for k right-hand sides: the state's own rows,
+    or its single linearisation point shared by all k"""
+    if st["k"] != 1 or k == 1:
+        return st["dconst"].data_ptr()
+    rep = st.setdefault("rep", {})
+    if k not in rep:
+        rep[k] = st["dconst"].repeat(k)
+    return rep[k].data_ptr()
+
+
 class _CFStage:
     """The fused correlated-field model (library/correlated_fields_simple.py)
     evaluated on a batch of packed latent rows."""
@@ -94,18 +105,14 @@ class _CFStage:
         return X[:, self.xo:self.xo + self.N].reshape((X.shape[0],) + self.grid)
 
     def fwd(self, X):
-        m, lay = self.m, self.lay
+        m = self.m
         k = X.shape[0]
         amp = m.amp
-        a_list, consts, keeps = [], [], []
-        for i in range(k):
-            v = lay.views(X[i])
-            a, c = amp.forward({kk: v[kk] for kk in amp.domain_dict})
-            const, keep = amp.native_const(c)
-            a_list.append(a)
-            consts.append(const)
-            keeps.append(keep)
-        A = torch.stack(a_list)
+        X = X.contiguous()
+        # all rows' amplitudes and linearisation constants in one native pass
+        # (nft_amp_forward_batched; device structs, no host round trip)
+        lin = amp.forward_rows(amp._ptrs(X, self.off), k, X.shape[1], X.device)
+        A = lin.a
         afull = torch.empty((k,) + self.grid, dtype=A.dtype, device=A.device)
         b = m.bins
         _native.bin_gather(A, b.pindex, afull, k, b.npix, b.nbin, 1)
@@ -115,22 +122,20 @@ class _CFStage:
         _native.hartley_fused(s, self.axes, m.c_h, x=u, convention=hartley_convention_code(), shape=s.shape)
         if m.offset_mean is not None:
             s = s + m.offset_mean
-        raw = b"".join(bytes(c) for c in consts)
-        dconst = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(X.device)
-        return s, dict(afull=afull, X=X, consts=consts, keeps=keeps, dconst=dconst, k=k)
+        return s, dict(afull=afull, X=X, lin=lin, lins=[lin], dconst=lin.dconst, k=k)
 
     @staticmethod
     def stack(states):
         """one batch state from per-sample (state, row) pairs"""
         if len(states) == 1 and states[0][0]["k"] == 1:
             return states[0][0]
+        if all(st is states[0][0] for st, _ in states) and [r for _, r in states] == list(range(states[0][0]["k"])):
+            return states[0][0]
         afull = torch.stack([st["afull"][r] for st, r in states])
         X = torch.stack([st["X"][r] for st, r in states])
-        consts = [st["consts"][r] for st, r in states]
-        keeps = [st["keeps"][r] for st, r in states]
-        raw = b"".join(bytes(c) for c in consts)
-        dconst = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(X.device)
-        return dict(afull=afull, X=X, consts=consts, keeps=keeps, dconst=dconst, k=len(states))
+        dconst = torch.cat([st["lin"].row_bytes(r) for st, r in states])
+        lins = [ln for st, _ in states for ln in st["lins"]]
+        return dict(afull=afull, X=X, lin=states[0][0]["lin"], lins=lins, dconst=dconst, k=len(states))
 
     def jvp(self, st, V):
         """(k, grid) = J_cf(x_b) V[b]; st shared (k = 1) or per item"""
@@ -144,11 +149,11 @@ class _CFStage:
         Xs = st["X"]
         if shared:
             da = torch.empty((B, k), dtype=torch.float64, device=V.device)
-            m.amp.native_jvp_batched(st["consts"][0], V, self.off, da, interleave=True)
+            m.amp.native_jvp_batched(st["lin"], V, self.off, da, interleave=True, item_consts=_items(st, k))
             batch = dict(period=N, x=size, c=1, c_elem=k)
         else:
             da = torch.empty((k, B), dtype=torch.float64, device=V.device)
-            m.amp.native_jvp_batched(st["consts"][0], V, self.off, da, item_consts=st["dconst"].data_ptr())
+            m.amp.native_jvp_batched(st["lin"], V, self.off, da, item_consts=_items(st, k))
             batch = dict(period=N, x=size, c=B, a=N, b=Xs.shape[1])
         pro = dict(a=st["afull"], x=V[0, self.xo:], b=Xs[0, self.xo:], c=da, index=m.bins.pindex)
         jb = m.jbins
@@ -177,8 +182,7 @@ class _CFStage:
                               convention=hartley_convention_code(), shape=(k,) + self.grid, batch=batch)
         ga = torch.empty((k, m.amp.B), dtype=G.dtype, device=G.device)
         m.jbins.scatter(w, ga, k)
-        m.amp.native_vjp_batched(st["consts"][0], ga, Q, self.off,
-                                 item_consts=None if shared else st["dconst"].data_ptr())
+        m.amp.native_vjp_batched(st["lin"], ga, Q, self.off, item_consts=_items(st, k))
         return Q
 
 

@@ -1,0 +1,113 @@
+"""Wall time of the phases of one bench step (draw_samples + SampledKLEnergy
+at the C3 size) and how busy the GPU is inside each: the phases are timed
+with a device synchronisation at their ends, the GPU busy time is the union
+of the kernel intervals torch.profiler records.  Usage:
+python tools/step_phases.py"""
+import sys
+import time
+from collections import defaultdict
+
+import torch
+
+sys.path.insert(0, ".")
+import bench  # noqa: E402
+
+WALL = defaultdict(float)
+CNT = defaultdict(int)
+
+
+def timed(obj, name, label):
+    f = getattr(obj, name)
+
+    def w(*a, **k):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        r = f(*a, **k)
+        if hasattr(r, "__next__"):     # generators (refine): drain them
+            r = list(r)
+        torch.cuda.synchronize()
+        WALL[label] += time.perf_counter() - t
+        CNT[label] += 1
+        return r
+    setattr(obj, name, w)
+
+
+def main():
+    import nifty_amd as ift
+    from nifty_amd.minimization import geovi_batch
+    ift.config.set_device("cuda:0")
+    cf, Rr, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
+    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=100))
+    mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=2), max_cg_iterations=50)
+    ift.random.push_sseq_from_seed(1000)
+
+    def step():
+        sl = ift.draw_samples(pos, H, mini, 4, True)
+        ift.SampledKLEnergyClass(sl, H, [], None, True)
+        torch.cuda.synchronize()
+    step()
+    step()
+    timed(geovi_batch, "kl_batch", "kl_batch (KL value + gradient)")
+    timed(geovi_batch, "plan", "geovi plan (f_lh at the position)")
+    orig_plan = geovi_batch.plan
+
+    def plan(*a, **k):
+        gb = orig_plan(*a, **k)
+        timed(gb, "refine", "geovi refine (NewtonCG, batched)")
+        return gb
+    geovi_batch.plan = plan
+    from nifty_amd.operators import sampling_enabler as se
+    timed(se.SamplingEnabler, "solve_rhs", "linear sampling CG (batched)")
+    timed(se.SamplingEnabler, "draw_rhs", "draw_rhs (sample right-hand sides)")
+    from nifty_amd.minimization import sample_list
+    timed(sample_list.ResidualSampleList, "__init__", "ResidualSampleList")
+    # one step without the profiler: the phase wall times
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    step()
+    print(f"unprofiled step {1e3 * (time.perf_counter() - t):.1f} ms")
+    for k, v in WALL.items():
+        print(f"  {k:40s} {v * 1e3:9.1f} ms  ({CNT.get(k, 1)} calls)")
+    WALL.clear()
+    CNT.clear()
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        sl = ift.draw_samples(pos, H, mini, 4, True)
+        torch.cuda.synchronize()
+        WALL["draw_samples total"] += time.perf_counter() - t
+        t1 = time.perf_counter()
+        ift.SampledKLEnergyClass(sl, H, [], None, True)
+        torch.cuda.synchronize()
+        WALL["SampledKLEnergy"] += time.perf_counter() - t1
+    WALL["step"] = time.perf_counter() - t
+    ivs = []
+    by = defaultdict(float)
+    for ev in prof.events():
+        if ev.device_type == torch.autograd.DeviceType.CUDA and ev.time_range.elapsed_us() > 0:
+            ivs.append((ev.time_range.start, ev.time_range.end))
+            nm = ev.name
+            grp = "nft" if ("nft" in nm or "los_" in nm or "amp_" in nm or "cg_" in nm or "fft" in nm
+                            or "r2c" in nm or "c2c" in nm or "bin_" in nm) else "torch/other"
+            by[grp] += ev.time_range.elapsed_us()
+    ivs.sort()
+    busy, cur = 0.0, None
+    for a, b in ivs:
+        if cur is None or a > cur[1]:
+            if cur:
+                busy += cur[1] - cur[0]
+            cur = [a, b]
+        else:
+            cur[1] = max(cur[1], b)
+    if cur:
+        busy += cur[1] - cur[0]
+    span = (ivs[-1][1] - ivs[0][0]) if ivs else 0
+    print(f"step wall {WALL['step'] * 1e3:.1f} ms; GPU busy {busy / 1e3:.1f} ms of a {span / 1e3:.1f} ms kernel span "
+          f"({len(ivs)} kernels); kernel time nft {by['nft'] / 1e3:.1f} ms, other {by['torch/other'] / 1e3:.1f} ms")
+    for k, v in WALL.items():
+        print(f"  {k:40s} {v * 1e3:9.1f} ms  ({CNT.get(k, 1)} calls)")
+
+
+if __name__ == "__main__":
+    main()

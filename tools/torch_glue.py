@@ -25,12 +25,13 @@ def main():
     step()
     step()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                 experimental_config=torch._C._profiler._ExperimentalConfig(verbose=True)) as prof:
         step()
     agg = defaultdict(lambda: [0, 0.0])
     # leaf aten ops only (aten::to -> _to_copy -> copy_ would count thrice),
     # attributed to the innermost nifty_amd frame of their Python stack
-    for ev in prof.key_averages(group_by_stack_n=12):
+    for ev in prof.events():
         if not ev.name.startswith("aten::") or ev.self_device_time_total <= 0:
             continue
         site = "?"
@@ -39,7 +40,7 @@ def main():
                 site = fr.split("/")[-1]
                 break
         key = (ev.name, site)
-        agg[key][0] += ev.count
+        agg[key][0] += 1
         agg[key][1] += ev.self_device_time_total
     tot = sum(v[1] for v in agg.values())
     print(f"aten GPU time in one step: {tot / 1e3:.1f} ms")
