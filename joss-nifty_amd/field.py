@@ -20,8 +20,17 @@ def _to_tensor(val, dtype=None):
         arr = arr.astype(utilities.numpy_dtype(utilities.torch_dtype(dtype)), copy=False)
     if arr.dtype == np.float16:
         arr = arr.astype(np.float32)
+    dev = torch.device(config.device())
+    if dev.type == "cuda":
+        # a prefetched draw in page-locked memory (random._pin): async DMA
+        from .random import take_pinned
+        t = take_pinned(arr)
+        if t is not None:
+            return t.to(dev, non_blocking=True)
+        if arr.ndim > 0 and arr.flags.c_contiguous and arr.flags.writeable:
+            return torch.from_numpy(arr).to(dev)    # the upload is the copy
     # (np.ascontiguousarray would promote 0-d arrays to 1-d)
-    return torch.from_numpy(np.array(arr, order="C", copy=True)).to(config.device())
+    return torch.from_numpy(np.array(arr, order="C", copy=True)).to(dev)
 
 
 class Field:

@@ -100,7 +100,9 @@ def _capture(fn):
     cur = torch.cuda.current_stream()
     _CAPTURE_STREAM.wait_stream(cur)
     with torch.cuda.stream(_CAPTURE_STREAM):
-        g.capture_begin()
+        # thread-local capture: the background RNG thread may page-lock host
+        # memory (random._pin) while the main thread captures
+        g.capture_begin(capture_error_mode="thread_local")
         try:
             fn()
         finally:

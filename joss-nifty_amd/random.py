@@ -190,9 +190,47 @@ _lock = threading.Lock()
 last_script = None
 
 
+# Large prefetched draws are written into page-locked host memory on the
+# background thread, so the Field upload of a served array is an asynchronous
+# DMA instead of a pageable copy the host waits for (field._to_tensor looks the
+# pinned tensor up by address).  The served array is a view of that memory:
+# the same values, only where they live differs.
+_PIN_BYTES = 1 << 20
+_pinned = {}
+
+
+def _pin(a):
+    if not isinstance(a, np.ndarray) or a.nbytes < _PIN_BYTES or a.dtype.kind not in "fc":
+        return a
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return a
+        t = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+    except Exception:     # no page-locked memory available: serve the plain array
+        return a
+    v = t.numpy()
+    with _lock:
+        _pinned[v.ctypes.data] = t
+        while len(_pinned) > 64:
+            _pinned.pop(next(iter(_pinned)))
+    return v
+
+
+def take_pinned(arr):
+    """the page-locked tensor behind a served prefetched draw, or None"""
+    if not _pinned or not isinstance(arr, np.ndarray):
+        return None
+    with _lock:
+        t = _pinned.pop(arr.ctypes.data, None)
+    if t is None or tuple(t.shape) != arr.shape or t.numpy().dtype != arr.dtype:
+        return None
+    return t
+
+
 def _run_script(sseq, script):
     g = np.random.default_rng(sseq)
-    return [getattr(g, name)(*args, **dict(kw)) for (name, args, kw) in script]
+    return [_pin(getattr(g, name)(*args, **dict(kw))) for (name, args, kw) in script]
 
 
 def predict_spawn(n, parent=None):

@@ -13,7 +13,7 @@ from conftest import ROOT, golden
 
 def _header_symbols():
     txt = open(os.path.join(ROOT, "include", "nifty_amd.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:const char\*|void|int|size_t)\s+(nft_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const char\*|void|int|int64_t|size_t)\s+(nft_\w+)\s*\(", txt, re.M)))
 
 
 def test_library_exports_every_header_symbol():

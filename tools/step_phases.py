@@ -60,6 +60,15 @@ def main():
     timed(se.SamplingEnabler, "solve_rhs", "linear sampling CG (batched)")
     timed(se.SamplingEnabler, "draw_rhs", "draw_rhs (sample right-hand sides)")
     from nifty_amd.minimization import sample_list
+    # inside draw_rhs: waiting for the background RNG, host->device uploads,
+    # the likelihood draw J^T xi and the gradient J^T J s
+    import nifty_amd.random as rnd
+    import nifty_amd.field as fld
+    from nifty_amd.operators import sandwich_operator as sw
+    timed(rnd, "_take", "  rng: wait for prefetched draws")
+    timed(fld, "_to_tensor", "  host->device uploads (_to_tensor)")
+    timed(sw.SandwichOperator, "draw_sample", "  likelihood draw (J^T xi)")
+    timed(sw.SandwichOperator, "apply", "  SandwichOperator.apply")
     timed(sample_list.ResidualSampleList, "__init__", "ResidualSampleList")
     # one step without the profiler: the phase wall times
     torch.cuda.synchronize()
