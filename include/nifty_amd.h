@@ -316,6 +316,18 @@ int nft_cg_direction_dd_batched(void* d, const void* r, int64_t n, int64_t vstri
                                 hipStream_t stream);
 int nft_fold_partials(const double* part, int nb, int nrhs, double* out, int64_t out_stride,
                       hipStream_t stream);
+/* The CG update split over segments of the packed vectors (pointers offset by
+ * the caller), so that the update of one segment can run while another
+ * segment's q is still being formed (the amplitude keys' VJP on a second
+ * stream while the grid segment updates).  The segment's nft_cg_dd_blocks(n)
+ * partial blocks land at [blk0, blk0 + nb) of each RHS's 3 x nbtot partial
+ * array (r.r, x.r, x.b rows); nft_cg_finalize_batched folds all nbtot in
+ * index order and records gamma / alpha / flags as nft_cg_update_batched
+ * does.  Per element the arithmetic is that of nft_cg_update_batched. */
+int nft_cg_update_seg_batched(void* x, void* r, const void* d, const void* q, const void* b, int64_t n,
+                              int64_t vstride, int nrhs, int dtype, double shift, const double* sc,
+                              double* part, int nbtot, int blk0, hipStream_t stream);
+int nft_cg_finalize_batched(const double* part, int nbtot, int nrhs, double* sc, hipStream_t stream);
 
 /* ---- correlated-field amplitude Jacobian ------------------------------ */
 /* Constants of the amplitude linearisation at one expansion point (all device

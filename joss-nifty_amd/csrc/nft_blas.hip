@@ -151,11 +151,11 @@ __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T*
                                                            const T* __restrict__ q,
                                                            const T* __restrict__ b, long long n, long long vs,
                                                            T shift, const double* __restrict__ sc,
-                                                           double* __restrict__ part) {
+                                                           double* __restrict__ part, int nbtot, int blk0) {
   __shared__ double sh[3 * (RED_NT / 64)];
   const long long o = (long long)blockIdx.y * vs;
   sc += blockIdx.y * NFT_CG_NSCALARS;
-  part += (long long)blockIdx.y * 3 * gridDim.x;
+  part += (long long)blockIdx.y * 3 * nbtot + blk0;
   x += o;
   r += o;
   d += o;
@@ -184,10 +184,9 @@ __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T*
   }
   block_sum<3>(v, sh);
   if (threadIdx.x == 0) {
-    const int nb = gridDim.x;
-    part[0 * nb + blockIdx.x] = v[0];
-    part[1 * nb + blockIdx.x] = v[1];
-    part[2 * nb + blockIdx.x] = v[2];
+    part[0 * nbtot + blockIdx.x] = v[0];
+    part[1 * nbtot + blockIdx.x] = v[1];
+    part[2 * nbtot + blockIdx.x] = v[2];
   }
 }
 
@@ -427,17 +426,50 @@ int nft_cg_update_batched(void* x, void* r, const void* d, const void* q, const 
   if (dtype == 0)
     hipLaunchKernelGGL(cg_update_kernel<double>, grid, dim3(RED_NT), 0, stream, (double*)x, (double*)r,
                        (const double*)d, (const double*)q, (const double*)b, (long long)n, (long long)vstride,
-                       shift, sc, part);
+                       shift, sc, part, nb, 0);
   else if (dtype == 1)
     hipLaunchKernelGGL(cg_update_kernel<float>, grid, dim3(RED_NT), 0, stream, (float*)x, (float*)r,
                        (const float*)d, (const float*)q, (const float*)b, (long long)n, (long long)vstride,
-                       (float)shift, sc, part);
+                       (float)shift, sc, part, nb, 0);
   else {
     set_last_error("nft_cg_update: bad dtype %d", dtype);
     return NFT_ERR_ARG;
   }
   prof_mark(stream, "cg_finalize_kernel");
   hipLaunchKernelGGL(cg_finalize_kernel, dim3(nrhs), dim3(RED_NT), 0, stream, part, nb, sc);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_update_seg_batched(void* x, void* r, const void* d, const void* q, const void* b, int64_t n,
+                              int64_t vstride, int nrhs, int dtype, double shift, const double* sc, double* part,
+                              int nbtot, int blk0, hipStream_t stream) {
+  const int nb = red_blocks(n);
+  if (blk0 < 0 || blk0 + nb > nbtot || !part) {
+    set_last_error("nft_cg_update_seg: partial blocks [%d, %d) outside [0, %d)", blk0, blk0 + nb, nbtot);
+    return NFT_ERR_ARG;
+  }
+  const dim3 grid(nb, nrhs);
+  prof_mark(stream, "cg_update_kernel");
+  if (dtype == 0)
+    hipLaunchKernelGGL(cg_update_kernel<double>, grid, dim3(RED_NT), 0, stream, (double*)x, (double*)r,
+                       (const double*)d, (const double*)q, (const double*)b, (long long)n, (long long)vstride,
+                       shift, sc, part, nbtot, blk0);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(cg_update_kernel<float>, grid, dim3(RED_NT), 0, stream, (float*)x, (float*)r,
+                       (const float*)d, (const float*)q, (const float*)b, (long long)n, (long long)vstride,
+                       (float)shift, sc, part, nbtot, blk0);
+  else {
+    set_last_error("nft_cg_update_seg: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_finalize_batched(const double* part, int nbtot, int nrhs, double* sc, hipStream_t stream) {
+  prof_mark(stream, "cg_finalize_kernel");
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(nrhs), dim3(RED_NT), 0, stream, part, nbtot, sc);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

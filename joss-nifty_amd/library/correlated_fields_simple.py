@@ -554,39 +554,91 @@ class CFJacobian(LinearOperator):
             if qpart is not None:
                 raise NotImplementedError("data-space curvature partials: fp64 only")
             return self._metric_flat_batch32(D, Q, W, shift)
+        da = self.mv_amp_jvp(D)
+        w = self.mv_grid(D, da, Q, W, shift, qpart)
+        self.mv_amp_vjp(D, w, Q, shift)
+        return Q
+
+    # The three phases of metric_flat_batch.  Only mv_grid touches the grid
+    # segment of D and Q; the amplitude phases read / write the amplitude keys
+    # alone, so a caller may run them on a second stream next to the grid
+    # segment's CG work (fused_cg.FusedCGBatch).  Their buffers persist per
+    # batch size: no allocation is freed while another stream may use it.
+    def _mv_bufs(self, k):
+        bufs = getattr(self, "_mvb", None)
+        if bufs is None or bufs["k"] != k:
+            grid = tuple(self._afull.shape)
+            dt = self._afull.dtype
+            B = self._m.amp.B
+            fold = self._m.jbins.fold
+            bufs = self._mvb = dict(k=k, da=torch.empty((B, k), dtype=torch.float64, device=self.device),
+                                    s=torch.empty((k,) + grid, dtype=dt, device=self.device),
+                                    w=torch.empty((k,) + grid, dtype=dt, device=self.device),
+                                    wf=torch.empty((k, fold["nf"]) if fold else (1,), dtype=dt,
+                                                   device=self.device),
+                                    ga=torch.empty((k, B), dtype=dt, device=self.device))
+        return bufs
+
+    def mv_amp_jvp(self, D):
+        """dA (B, k) of the k rows of D, bin-major interleaved: the
+        prologue's bin gather reads one contiguous run per pixel for all k"""
+        m = self._m
+        k = D.shape[0]
+        da = self._mv_bufs(k)["da"]
+        m.amp.native_jvp_batched(self._const(), D, dict(zip(self.layout.keys, self.layout.offsets)), da,
+                                 interleave=True)
+        return da
+
+    def mv_grid(self, D, da, Q, W, shift=0.0, qpart=None):
+        """forward transform (with the prologue), W, adjoint transform: the
+        grid segment of Q and w = xi0 * v for the amplitude VJP"""
         m = self._m
         lay = self.layout
         k, size = D.shape
-        amp = m.amp
-        B = amp.B
+        bufs = self._mv_bufs(k)
         grid = tuple(self._afull.shape)
         N = self._afull.numel()
-        off = dict(zip(lay.keys, lay.offsets))
-        xo = off[m.k_xi]
+        xo = dict(zip(lay.keys, lay.offsets))[m.k_xi]
         axes = tuple(range(1, 1 + len(grid)))
         conv = hartley_convention_code()
-        const = self._const()
-        # dA interleaved bin-major: the prologue's bin gather reads one
-        # contiguous run per pixel for all k right-hand sides
-        da = torch.empty((B, k), dtype=torch.float64, device=self.device)
-        amp.native_jvp_batched(const, D, off, da, interleave=True)
-        s = torch.empty((k,) + grid, dtype=self._afull.dtype, device=self.device)
+        s = bufs["s"]
         pro = dict(a=self._afull, x=D[0, xo:], b=self._xi0, **self._pro_bins(da, k))
         _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
                               batch=dict(period=N, x=size, c=1, c_elem=k))
         g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
         g = g.contiguous()
-        w = torch.empty((k,) + grid, dtype=self._afull.dtype, device=self.device)
+        w = bufs["w"]
         epi = dict(a=self._afull, b=self._xi0, out2=w)
         bt = dict(period=N, out=size, out2=N)
         if shift != 0.0:
             epi.update(d=D[0, xo:], shift=shift)
             bt["d"] = size
         _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt)
-        ga = torch.empty((k, B), dtype=w.dtype, device=self.device)
-        m.jbins.scatter(w, ga, k)
-        amp.native_vjp_batched(const, ga, Q, off, D, shift)
+        return w
+
+    def mv_fold(self, w):
+        """the mirror fold of w (the bandwidth-bound half of the bin sums)"""
+        k = w.shape[0]
+        return self._m.jbins.fold_into(w, self._mv_bufs(k)["wf"], k)
+
+    def mv_amp_vjp(self, D, w, Q, shift=0.0, folded=None):
+        """bin sums of w (folded: mv_fold's result, if already formed) and the
+        amplitude VJP into Q's amplitude keys"""
+        m = self._m
+        k = Q.shape[0]
+        ga = self._mv_bufs(k)["ga"]
+        m.jbins.scatter_from(self.mv_fold(w) if folded is None else folded, ga, k)
+        m.amp.native_vjp_batched(self._const(), ga, Q, dict(zip(self.layout.keys, self.layout.offsets)), D, shift)
         return Q
+
+    def grid_segment(self):
+        """[start, stop) of the grid key ('xi') in the packed layout, padding
+        included: the amplitude keys lie outside it"""
+        lay = self.layout
+        i = lay.keys.index(self._m.k_xi)
+        o = lay.offsets[i]
+        stop = lay.offsets[i + 1] if i + 1 < len(lay.keys) else lay.size
+        return o, stop
 
     supports_fp32 = True
 

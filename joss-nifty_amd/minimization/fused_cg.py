@@ -15,6 +15,7 @@ forming q = q' + shift d first), so the matvec never reads d a second time.
 All scalars stay on the device; one 16-double D2H read per iteration feeds the
 host-side controller, exactly as the reference decides on host floats.
 """
+import ctypes
 import math
 import os
 
@@ -238,12 +239,20 @@ class FusedCG:
             return energy, ctl.CONVERGED
 
         nq = _quad_blocks(core, self.W, x.dtype, (ctl,))
+        split = None
         if nq:
             nbd = int(lib.nft_cg_dd_blocks(n))
             pq = torch.empty((1, nbd + nq), dtype=torch.float64, device=x.device)
+            if _SPLIT and x.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
+                # FusedCGBatch's split iteration with k = 1 (same partial layout)
+                split = _SplitIteration(lib, core, self.W, n, 1, nq, sh, b is not None)
 
         def body(with_dir):
             s_ = _native.stream_ptr()
+            if with_dir and split is not None:
+                split(x.view(1, -1), r.view(1, -1), d.view(1, -1), q.view(1, -1),
+                      b.view(1, -1) if b is not None else None, sc.view(1, -1))
+                return
             if with_dir and nq:
                 # the same kernels and partial layout as FusedCGBatch with k = 1
                 chk(lib.nft_cg_direction_dd_batched(P(d), P(r), n, n, 1, dt, P(sc), sh, P(pq), nbd + nq, s_))
@@ -356,6 +365,101 @@ def fused_cg_batch_or_none(energies, controllers, nreset):
     return FusedCGBatch(core, W, shift, controllers, nreset).run(energies)
 
 
+# Split iteration of the batched solve (data-space curvature only, opt-in
+# NFT_CG_SPLIT=1): the amplitude keys' JVP / VJP chains -- a dozen small
+# latency-bound launches, ~190 us per iteration at 2048^2 x 4 RHS -- on a
+# second (high-priority) stream next to the grid segment's direction and
+# update passes.  Measured (tools/split_check.py, rocprofv3 kernel trace): the
+# streams do overlap, but the side chain's bin scatter and scans slow from 36
+# to ~145 us under the grid update's full-bandwidth stream (their gathers
+# wait on a saturated memory system), so the iteration gains ~1 % (1232 ->
+# 1222 us graph replay): off by default.
+_SPLIT = os.environ.get("NFT_CG_SPLIT", "0") == "1"
+_SIDE = None
+
+
+def _side_stream():
+    global _SIDE
+    if _SIDE is None:
+        # high priority: the grid segment's streaming kernels occupy every CU,
+        # so the side stream's short launches must win the freed slots
+        _SIDE = torch.cuda.Stream(priority=-1)
+    return _SIDE
+
+
+class _SplitIteration:
+    """One CG iteration of FusedCGBatch with the packed vectors cut into the
+    grid segment G (the 'xi' key) and the amplitude segments A (the keys before
+    and after it):
+
+      main:  dir(A) | dir(G)        | grid matvec, fold curv, mirror fold | update(G)  | finalize
+      side:         | amplitude JVP |                                     | bin sums, amplitude VJP, update(A)
+
+    The per-element arithmetic is that of the one-stream iteration; the dot
+    partials of the three segments are folded in one fixed order."""
+
+    def __init__(self, lib, core, W, n, k, nq, shift, with_b):
+        self.lib, self.core, self.W = lib, core, W
+        self.n, self.k, self.nq, self.shift = n, k, nq, shift
+        g0, g1 = core.grid_segment()
+        rng = [(0, g0), (g0, g1), (g1, n)]
+        self.ranges = [(o, e - o) for o, e in rng if e > o]
+        nb = [int(lib.nft_cg_dd_blocks(ln)) for _, ln in self.ranges]
+        self.blk0 = [sum(nb[:i]) for i in range(len(nb))]
+        self.nbtot = sum(nb)
+        dev = core.device
+        self.PQ = torch.empty((k, self.nbtot + nq), dtype=torch.float64, device=dev)
+        self.UP = torch.empty((k, 3 * self.nbtot), dtype=torch.float64, device=dev)
+        self.grid_i = [i for i, (o, _) in enumerate(self.ranges) if o == g0][0]
+
+    def _dir(self, i, D, Rr, SC, s_):
+        o, ln = self.ranges[i]
+        e = 8  # fp64 bytes
+        _native._check(self.lib.nft_cg_direction_dd_batched(
+            ctypes.c_void_p(D.data_ptr() + o * e), ctypes.c_void_p(Rr.data_ptr() + o * e), ln, self.n, self.k, 0,
+            _native.ptr(SC), self.shift, ctypes.c_void_p(self.PQ.data_ptr() + self.blk0[i] * 8),
+            self.PQ.stride(0), s_))
+
+    def _update(self, i, X, Rr, D, Q, Bu, SC, s_):
+        o, ln = self.ranges[i]
+        e = 8
+        P = ctypes.c_void_p
+        _native._check(self.lib.nft_cg_update_seg_batched(
+            P(X.data_ptr() + o * e), P(Rr.data_ptr() + o * e), P(D.data_ptr() + o * e), P(Q.data_ptr() + o * e),
+            P(Bu.data_ptr() + o * e) if Bu is not None else P(0), ln, self.n, self.k, 0, self.shift,
+            _native.ptr(SC), _native.ptr(self.UP), self.nbtot, self.blk0[i], s_))
+
+    def __call__(self, X, Rr, D, Q, Bu, SC):
+        core, lib = self.core, self.lib
+        main = torch.cuda.current_stream()
+        side = _side_stream()
+        amp_i = [i for i in range(len(self.ranges)) if i != self.grid_i]
+        s_ = _native.stream_ptr()
+        for i in amp_i:
+            self._dir(i, D, Rr, SC, s_)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            da = core.mv_amp_jvp(D)
+        self._dir(self.grid_i, D, Rr, SC, s_)
+        main.wait_stream(side)
+        w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbtot:])
+        _native._check(lib.nft_fold_partials(_native.ptr(self.PQ), self.nbtot + self.nq, self.k,
+                                             ctypes.c_void_p(SC.data_ptr() + _native.CG_CURV * 8),
+                                             _native.CG_NSCALARS, s_))
+        # the mirror fold streams as much as the grid update: it stays on the
+        # main stream; the side stream gets the latency-bound rest
+        wf = core.mv_fold(w)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            core.mv_amp_vjp(D, w, Q, 0.0, folded=wf)
+            ss = _native.stream_ptr()
+            for i in amp_i:
+                self._update(i, X, Rr, D, Q, Bu, SC, ss)
+        self._update(self.grid_i, X, Rr, D, Q, Bu, SC, s_)
+        main.wait_stream(side)
+        _native._check(lib.nft_cg_finalize_batched(_native.ptr(self.UP), self.nbtot, self.k, _native.ptr(SC), s_))
+
+
 class FusedCGBatch(FusedCG):
     """k independent conjugate-gradient solves with the same metric, run in
     lock step: every iteration is ONE batched matvec (the LOS matrix, the FFT
@@ -461,12 +565,18 @@ class FusedCGBatch(FusedCG):
         Bu = Bv if any(_reads_value(c) for c in self.controllers) else None
 
         nq = _quad_blocks(core, self.W, X.dtype, self.controllers)
+        split = None
         if nq:
             nbd = int(lib.nft_cg_dd_blocks(n))
             PQ = torch.empty((k, nbd + nq), dtype=torch.float64, device=dev)
+            if _SPLIT and X.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
+                split = _SplitIteration(lib, core, self.W, n, k, nq, sh, Bu is not None)
 
         def body(with_dir):
             s_ = _native.stream_ptr()
+            if with_dir and split is not None:
+                split(X, Rr, D, Q, Bu, SC)
+                return
             if with_dir and nq:
                 # curvature from the data space: shift * d.d partials while d is
                 # formed, (J d).W(J d) partials in the LOS forward reduce

@@ -100,6 +100,24 @@ class BinIndex:
         return _native.bin_scatter(wf, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
                                    order=f["order"])
 
+    def fold_into(self, w, wf, pre):
+        """first half of scatter: the mirror fold of w into wf (pre, nf);
+        returns the operand of scatter_from (wf, or w without a fold)"""
+        f = self.fold
+        if f is None:
+            return w
+        _native.bin_fold(w, wf, pre, f["shape"])
+        return wf
+
+    def scatter_from(self, src, out, pre):
+        """second half of scatter: the bin sums of fold_into's result"""
+        f = self.fold
+        if f is None:
+            return _native.bin_scatter(src, self.perm, self.offsets, out, pre, self.npix, self.nbin, 1,
+                                       order=self.gather_order)
+        return _native.bin_scatter(src, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
+                                   order=f["order"])
+
     # pixel-ordered chunk gathers: measured no faster than the sorted ones at
     # 2048^2 (the chunk kernel is bound by its per-bin phase, not by gather
     # divergence), so only the precomputed chunk bounds are used by default

@@ -16,23 +16,62 @@ WALL = defaultdict(float)
 CNT = defaultdict(int)
 
 
+PROFILE = {}      # label -> torch.profiler results of that phase (--phase LABEL)
+
+
+def _busy(prof):
+    ivs, by = [], defaultdict(lambda: [0, 0.0])
+    for ev in prof.events():
+        if ev.device_type == torch.autograd.DeviceType.CUDA and ev.time_range.elapsed_us() > 0:
+            ivs.append((ev.time_range.start, ev.time_range.end))
+            by[ev.name][0] += 1
+            by[ev.name][1] += ev.time_range.elapsed_us()
+    ivs.sort()
+    busy, cur = 0.0, None
+    for a, b in ivs:
+        if cur is None or a > cur[1]:
+            if cur:
+                busy += cur[1] - cur[0]
+            cur = [a, b]
+        else:
+            cur[1] = max(cur[1], b)
+    if cur:
+        busy += cur[1] - cur[0]
+    return busy, len(ivs), by
+
+
 def timed(obj, name, label):
     f = getattr(obj, name)
 
     def w(*a, **k):
         torch.cuda.synchronize()
+        prof = None
+        if PROFILE.get("want") and PROFILE["want"] in label and "done" not in PROFILE:
+            from torch.profiler import ProfilerActivity, profile
+            prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
+            prof.__enter__()
         t = time.perf_counter()
         r = f(*a, **k)
         if hasattr(r, "__next__"):     # generators (refine): drain them
             r = list(r)
         torch.cuda.synchronize()
-        WALL[label] += time.perf_counter() - t
+        el = time.perf_counter() - t
+        WALL[label] += el
         CNT[label] += 1
+        if prof is not None:
+            prof.__exit__(None, None, None)
+            PROFILE["done"] = True
+            busy, n, by = _busy(prof)
+            print(f"[{label}] wall {el * 1e3:.1f} ms (profiled), GPU busy {busy / 1e3:.1f} ms, {n} kernels")
+            for nm, (c, us) in sorted(by.items(), key=lambda kv: -kv[1][1])[:25]:
+                print(f"    {us / 1e3:8.2f} ms {c:5d}  {nm[:90]}")
         return r
     setattr(obj, name, w)
 
 
 def main():
+    if "--phase" in sys.argv:
+        PROFILE["want"] = sys.argv[sys.argv.index("--phase") + 1]
     import nifty_amd as ift
     from nifty_amd.minimization import geovi_batch
     ift.config.set_device("cuda:0")
