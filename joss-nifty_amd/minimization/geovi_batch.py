@@ -164,8 +164,9 @@ class _CFStage:
                               shape=out.shape, batch=batch)
         return out
 
-    def vjp(self, st, G, Q):
-        """Q[b] (packed rows, padding zero) = J_cf(x_b)^T G[b]"""
+    def vjp(self, st, G, Q, d=None, shift=0.0):
+        """Q[b] (packed rows, padding zero) = J_cf(x_b)^T G[b] (+ shift * d[b],
+        added as the transform stores and inside the amplitude VJP)"""
         from ..ducc_dispatch import hartley_convention_code
         m = self.m
         k = G.shape[0]
@@ -178,11 +179,15 @@ class _CFStage:
         batch = dict(period=N, out=size, out2=N)
         if not shared:
             batch.update(ea=N, eb=Xs.shape[1])
+        if d is not None and shift != 0.0:
+            epi.update(d=d[0, self.xo:], shift=shift)
+            batch["d"] = d.shape[1]
         _native.hartley_fused(Q[0, self.xo:], self.axes, m.c_h, x=G.contiguous(), epi=epi,
                               convention=hartley_convention_code(), shape=(k,) + self.grid, batch=batch)
         ga = torch.empty((k, m.amp.B), dtype=G.dtype, device=G.device)
         m.jbins.scatter(w, ga, k)
-        m.amp.native_vjp_batched(st["lin"], ga, Q, self.off, item_consts=_items(st, k))
+        m.amp.native_vjp_batched(st["lin"], ga, Q, self.off, D=d, shift=shift if d is not None else 0.0,
+                                 item_consts=_items(st, k))
         return Q
 
 
@@ -365,8 +370,9 @@ class Pipeline:
             i += 1
         return U
 
-    def vjp(self, states, G, Q):
-        """Q (k, size) zero-padded packed rows = J^T G"""
+    def vjp(self, states, G, Q, d=None, shift=0.0):
+        """Q (k, size) zero-padded packed rows = J^T G (+ shift * d, fused into
+        the correlated field's adjoint)"""
         U = G
         i = len(self.stages) - 1
         while i >= 1:
@@ -377,7 +383,7 @@ class Pipeline:
                 continue
             U = s.vjp(st, U)
             i -= 1
-        return self.stages[0].vjp(states[0], U, Q)
+        return self.stages[0].vjp(states[0], U, Q, d, shift)
 
 
 # ------------------------------------------------------------------ energies
@@ -451,19 +457,19 @@ class GeoVIBatch:
                 Q[:, a:b] = 0.0
         return Q
 
-    def _J0T(self, F):
-        return self.pipe.vjp(self.st0, F, self._latent(F.shape[0], F.device))
+    def _J0T(self, F, plus=None):
+        """J0^T F (+ plus, added inside the adjoint: bitwise the separate add)"""
+        return self.pipe.vjp(self.st0, F, self._latent(F.shape[0], F.device), plus, 1.0)
 
-    def _JT(self, states, G):
-        return self.pipe.vjp(states, G, self._latent(G.shape[0], G.device))
+    def _JT(self, states, G, plus=None):
+        return self.pipe.vjp(states, G, self._latent(G.shape[0], G.device), plus, 1.0)
 
     def evaluate(self, X, M):
         """values, |gradient|, gradients and per-sample states at the rows of X"""
         F, states = self.pipe.fwd(X)
         Rr = self._J0T(F)
         Rr.add_(X).sub_(M)
-        G = self._JT(states, self._J0(Rr))
-        G.add_(Rr)
+        G = self._JT(states, self._J0(Rr), plus=Rr)
         k = X.shape[0]
         h = _rowdots([(Rr, Rr), (G, G)])
         vals = [0.5 * float(h[0, i]) for i in range(k)]
@@ -473,10 +479,8 @@ class GeoVIBatch:
     def metric_batch(self, states):
         """callable (D, Q) -> Q = M_b D for the stacked per-sample states"""
         def mv(D, Q):
-            U = self._J0T(self.pipe.jvp(states, D))
-            U.add_(D)
-            self.pipe.vjp(states, self._J0(U), Q)   # overwrites every key segment
-            Q.add_(U)
+            U = self._J0T(self.pipe.jvp(states, D), plus=D)
+            self.pipe.vjp(states, self._J0(U), Q, U, 1.0)   # overwrites every key segment
             return Q
         return mv
 
