@@ -65,7 +65,14 @@ extern "C" {
 #define NFT_CG_XB 5 /* x.b */
 #define NFT_CG_FLAG 6 /* 1.0: curvature/alpha guard tripped, x and r left unchanged */
 #define NFT_CG_DD 7   /* d.d (fused sampling metric) */
-#define NFT_CG_DONE 8 /* set by the host: this right-hand side has stopped (batched solves) */
+#define NFT_CG_DONE 8 /* this right-hand side has stopped (batched solves): set by the host when
+                        * its controller stops, by the update's finalize (value 2) when the
+                        * step is terminal whatever the controller says (curvature/alpha guard
+                        * tripped; with NFT_CG_AUTO also a zero, negative or NaN new gamma) */
+#define NFT_CG_ITER 9 /* steps finalized since the solve started (the host may queue several
+                       * steps between reads) */
+#define NFT_CG_AUTO 10 /* set by the host while it queues several steps: a zero, negative or
+                        * NaN new gamma freezes the RHS too (DONE = 2; the guard always does) */
 #define NFT_CG_NSCALARS 16
 
 const char* nft_last_error(void);

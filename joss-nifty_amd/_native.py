@@ -112,7 +112,7 @@ class AmpOut(ctypes.Structure):
     _fields_ = [(n, _p) for n in ("fl", "sl", "flex", "asp", "zm", "spec",
                                   "dfl", "dsl", "dflex", "dasp", "dzm", "dspec")] + [("shift", _d)]
 
-CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD, CG_DONE = range(9)
+CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD, CG_DONE, CG_ITER, CG_AUTO = range(11)
 CG_NSCALARS = 16
 
 _lib = None

@@ -209,12 +209,19 @@ __global__ __launch_bounds__(RED_NT) void cg_finalize_kernel(const double* __res
     const bool ok = (curv == curv) && curv != 0.0 && (alpha >= 0.0) && (alpha == alpha);
     sc[NFT_CG_ALPHA] = alpha;
     sc[NFT_CG_FLAG] = ok ? 0.0 : 1.0;
+    sc[NFT_CG_ITER] += 1.0;
     if (ok) {
       sc[NFT_CG_GPREV] = gprev;
       sc[NFT_CG_GAMMA] = v[0];
       sc[NFT_CG_XR] = v[1];
       sc[NFT_CG_XB] = v[2];
     }
+    // terminal whatever the controller decides (conjugate_gradient.py:84-118:
+    // ERROR on the guard, CONVERGED on gamma == 0, ERROR on gamma < 0 / NaN):
+    // freeze now, so steps the host queued behind this one leave it alone
+    // (the gamma test only while the host queues several steps: a residual
+    // refresh step recomputes gamma after this finalize)
+    if (!ok || (sc[NFT_CG_AUTO] != 0.0 && !(v[0] > 0.0))) sc[NFT_CG_DONE] = 2.0;
   }
 }
 

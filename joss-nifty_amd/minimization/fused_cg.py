@@ -143,6 +143,25 @@ def _count_only(ctl):
             and ctl._tol_rel_gradnorm is None)
 
 
+def _count_silent(ctl):
+    """a count-only controller that logs nothing: its checks read no energy"""
+    return _count_only(ctl) and ctl._name is None and ctl._iteration_limit is not None
+
+
+class _CountOnlyState:
+    """energy stand-in for the checks of a queued chunk: count-only
+    controllers read nothing from it (any read fails loudly)"""
+
+    def __getattr__(self, name):
+        raise RuntimeError(f"count-only controller read energy.{name} in a queued CG chunk")
+
+
+_COUNT_ONLY_STATE = _CountOnlyState()
+
+# queued CG iterations between host reads (NFT_CG_CHUNK=0: one read per step)
+CHUNK = os.environ.get("NFT_CG_CHUNK", "1") != "0"
+
+
 def _quad_blocks(core, W, dtype, controllers=()):
     """partials per RHS of the metric's data-space quadratic form, or 0"""
     if not CURV_DATA or dtype != torch.float64 or not callable(W):
@@ -593,7 +612,19 @@ class FusedCGBatch(FusedCG):
         graph = None
         ii = 0
         first = True
+        # several graph replays per host read while every live controller only
+        # counts (_count_silent) and no decision trace is recorded
+        from . import trace
+        chunkable = CHUNK and not trace.active() and all(_count_silent(self.controllers[j]) for j in active)
+        iter_seen = np.zeros(k)
         while active:
+            if chunkable and graph is not None and ii + 2 < self.nreset:
+                m = min(min(self.controllers[j]._iteration_limit - self.controllers[j]._itcount for j in active),
+                        self.nreset - 1 - ii)
+                if m > 1:
+                    iter_seen = self._chunk(graph, m, SC, host, iter_seen, active, finish)
+                    ii += m
+                    continue
             self.niter += 1
             ConjugateGradient.iterations_total += len(active)
             ii += 1
@@ -630,6 +661,7 @@ class FusedCGBatch(FusedCG):
             host.copy_(SC, non_blocking=True)
             torch.cuda.current_stream().synchronize()
             h = host.numpy()
+            iter_seen = h[:, _native.CG_ITER].copy()
             for j in list(active):
                 ctl = self.controllers[j]
                 hj = h[j]
@@ -680,3 +712,56 @@ class FusedCGBatch(FusedCG):
                     finish(j, status)
                     active.remove(j)
         return X, results
+
+    def _chunk(self, graph, m, SC, host, iter_seen, active, finish):
+        """m queued iterations (graph replays) and one host read.  A terminal
+        step (guard tripped, gamma zero / negative / NaN) freezes its RHS on
+        the device (NFT_CG_DONE = 2, with NFT_CG_AUTO set); every RHS's
+        controller then sees exactly the checks a one-step loop would have
+        made, in order -- count-only controllers read nothing but the count."""
+        NS = _native
+        SC[:, NS.CG_AUTO] = 1.0
+        for _ in range(m):
+            graph.replay()
+        SC[:, NS.CG_AUTO] = 0.0
+        self.niter += m
+        host.copy_(SC, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        h = host.numpy()
+        for j in list(active):
+            ctl = self.controllers[j]
+            hj = h[j]
+            p = int(round(hj[NS.CG_ITER] - iter_seen[j]))
+            ConjugateGradient.iterations_total += p
+            frozen = hj[NS.CG_DONE] == 2.0
+            status = None
+            for t in range(p - 1 if frozen else p):
+                st = ctl.check(_COUNT_ONLY_STATE)
+                if st != ctl.CONTINUE:
+                    if t != p - 1:
+                        raise RuntimeError("count-only controller stopped inside a queued chunk")
+                    status = st
+            if frozen:
+                if hj[NS.CG_FLAG] != 0.0:
+                    curv = hj[NS.CG_CURV]
+                    if np.isnan(curv):
+                        logger.error("Error: ConjugateGradient: curv==NaN")
+                    elif curv == 0.:
+                        logger.error("Error: ConjugateGradient: curv==0.")
+                    else:
+                        logger.error("Error: ConjugateGradient: alpha<0.")
+                    status = ctl.ERROR
+                else:
+                    gamma = float(hj[NS.CG_GAMMA])
+                    if np.isnan(gamma):
+                        logger.error("Error: ConjugateGradient: gamma==NaN")
+                        status = ctl.ERROR
+                    elif gamma < 0:
+                        logger.error("Positive definiteness of preconditioner violated!")
+                        status = ctl.ERROR
+                    else:
+                        status = ctl.CONVERGED
+            if status is not None:
+                finish(j, status)
+                active.remove(j)
+        return h[:, NS.CG_ITER].copy()
