@@ -335,3 +335,22 @@ def test_checkpoint_roundtrip_cpu(tmp_path):
     s2 = ift.random.spawn_sseq(2)
     assert [s.spawn_key for s in s1] == [s.spawn_key for s in s2]
     ift.random.pop_sseq()
+
+
+def test_abi_host_code_under_asan():
+    """The C ABI's host code (argument validation, workspace sizing, plan
+    arithmetic, error formatting) built with AddressSanitizer (host side
+    only, -Xarch_host -fsanitize=address) and driven through every entry
+    point whose work ends on the host (tests/asan/abi_host_driver.cpp)."""
+    import shutil
+    import subprocess
+    if shutil.which("make") is None or not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc / make not available")
+    d = os.path.join(ROOT, "tests", "asan")
+    b = subprocess.run(["make", "-C", d, "-j8"], capture_output=True, text=True, timeout=900)
+    assert b.returncode == 0, b.stderr[-2000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0")
+    r = subprocess.run([os.path.join(d, "build", "abi_host_driver")], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert r.returncode == 0 and "abi host checks: ok" in r.stdout, (r.stdout, r.stderr[-2000:])
