@@ -116,6 +116,9 @@ def probe_setup(ift, lh, pos, k):
     return core, W, shift, X
 
 
+_CARRY_CACHE = {}
+
+
 def cg_iteration(lib, core, W, shift, bufs, k):
     """One batched CG iteration as FusedCGBatch.body runs it inside the timed
     loop: direction, batched matvec, curvature, update (+ their folds); the
@@ -127,6 +130,16 @@ def cg_iteration(lib, core, W, shift, bufs, k):
     P = _native.ptr
     s_ = _native.stream_ptr()
     nq = _quad_blocks(core, W, X.dtype)
+    from nifty_amd.minimization.fused_cg import _CarryIteration
+    if nq and X.dtype == torch.float64 and _CarryIteration.supported(core, k):
+        # FusedCGBatch's iteration: the grid segment's update inside the
+        # adjoint transform's epilogue (no b stream: count-only controllers)
+        key = (id(core), k, n)
+        it = _CARRY_CACHE.get(key)
+        if it is None:
+            it = _CARRY_CACHE[key] = _CarryIteration(lib, core, W, n, k, nq, shift)
+        it(X, R, D, Q, SC)
+        return
     if nq:
         nbd = int(lib.nft_cg_dd_blocks(n))
         PQ = torch.empty((k, nbd + nq), dtype=torch.float64, device=X.device)
@@ -222,6 +235,13 @@ def byte_model(cf, R, k, n_lat):
         # x, r, d, q in; x, r out (b is not streamed: the probe passes none,
         # and the sampling CG's value-blind controllers skip it too)
         "cg_update_kernel": 6 * 8 * k * n_lat,
+        # the amplitude keys' update (the grid segment's rides in the
+        # epilogue): two launches, the keys before and after the grid
+        # segment; per launch the model carries half of their bytes
+        "cg_update_seg": 3 * 8 * k * (n_lat - N),
+        # unpack + the grid segment's CG update: half spectrum (k), A, xi0;
+        # x, r, d in (k), x, r and w = xi0*v out (k) -- q is not stored
+        "fft_unpack+cg": 16 * k * Hh + 16 * N + 48 * k * N,
     }
 
 

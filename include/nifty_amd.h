@@ -219,7 +219,29 @@ typedef struct nft_hartley_fuse {
    * d = 2, no per-element index read).  Requires the transform axes to be
    * all of an item's axes. */
   int64_t pro_folded;
+  /* CG update carried by the epilogue (cg_x != NULL; batched adjoint of the
+   * sampling metric with the curvature already known, nft_hartley_cg_blocks
+   * > 0 for the geometry): for every output element j of item b, with
+   * q = epi_a[j] * h (the value the epilogue would store in out, which is
+   * then NOT written) and alpha = sc[GAMMA] / sc[CURV] of item b (scalar
+   * block b * NFT_CG_NSCALARS of cg_sc, guards as nft_cg_update_batched):
+   *   x[b * cg_stride + j] -= alpha d[..];  r[..] -= alpha (q + cg_shift d[..])
+   * and per transform tile the partials r.r, x.r (x.b = 0) land at
+   * cg_part[b * 3 * cg_nbtot + c * cg_nbtot + cg_blk0 + tile] for c = 0, 1, 2
+   * -- nft_cg_finalize_batched folds them with the other segments'. */
+  void *cg_x, *cg_r;
+  const void* cg_d;
+  const double* cg_sc;
+  double* cg_part;
+  int64_t cg_stride;
+  double cg_shift;
+  int32_t cg_nbtot, cg_blk0;
 } nft_hartley_fuse;
+
+/* Partial blocks per item of the CG-carrying epilogue for a batched
+ * Hartley transform of this geometry (leading batch axis not among `axes`),
+ * or 0 when its last pass cannot carry the update. */
+int nft_hartley_cg_blocks(int ndim, const int64_t* shape, int naxes, const int* axes, int dtype);
 
 int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes,
                                 int dtype, size_t* bytes);

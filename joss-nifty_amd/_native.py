@@ -66,6 +66,7 @@ SIGNATURES = {
     "nft_amp_vjp": (_i, [_p, _p, _p, _p, _p]),
     "nft_amp_jvp_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _p]),
     "nft_amp_vjp_batched": (_i, [_p, _p, _p, _p, _p, _i, _i64, _i64, _p]),
+    "nft_hartley_cg_blocks": (_i, [_i, _p, _i, _p, _i]),
     "nft_cg_update_seg_batched": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i, _i, _d, _p, _p, _i, _i, _p]),
     "nft_cg_finalize_batched": (_i, [_p, _i, _i, _p, _p]),
     "nft_amp_forward_buf": (_i64, [_i64]),
@@ -79,7 +80,9 @@ class HartleyFuse(ctypes.Structure):
                                   "epi_out2")] + [("epi_shift", _d)] + \
                [(n, _i64) for n in ("batch_period", "x_bstride", "c_bstride", "out_bstride", "d_bstride",
                                     "out2_bstride", "c_estride", "a_bstride", "b_bstride", "ea_bstride",
-                                    "eb_bstride", "pro_folded")]
+                                    "eb_bstride", "pro_folded")] + \
+               [(n, _p) for n in ("cg_x", "cg_r", "cg_d", "cg_sc", "cg_part")] + \
+               [("cg_stride", _i64), ("cg_shift", _d), ("cg_nbtot", ctypes.c_int32), ("cg_blk0", ctypes.c_int32)]
 
 
 class LosPlan(ctypes.Structure):
@@ -318,7 +321,14 @@ def spmv_scaled(indptr, indices, weights, rowblocks, x, y, colscale=None, rowsca
     return y
 
 
-def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None):
+def hartley_cg_blocks(shape, axes, dtype):
+    """partial blocks per item of the CG-carrying epilogue for a batched
+    transform of `shape` (leading batch axis) over `axes`, 0 if unsupported"""
+    nd, sh, na, ax = _shape_args(tuple(shape), tuple(axes))
+    return int(load().nft_hartley_cg_blocks(nd, sh, na, ax, dtype_code(dtype)))
+
+
+def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None, cg=None):
     """out = epilogue(scale * Hartley(prologue)) with
     pro = dict(a=, x=, b=, c=, index=) (or fold=True and c per fundamental
     cell instead of index, nft_hartley_fuse.pro_folded) and
@@ -348,6 +358,18 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
             tens.append(v)
             setattr(f, fld, v.data_ptr() if v is not None else None)
         f.epi_shift = float(epi.get("shift", 0.0))
+    if cg:
+        # the CG update carried by the epilogue (nft_hartley_fuse.cg_*):
+        # x / r / d are strided base pointers of the grid segment
+        for k, fld in (("x", "cg_x"), ("r", "cg_r"), ("d", "cg_d"), ("sc", "cg_sc"), ("part", "cg_part")):
+            v = cg[k]
+            if not v.is_cuda:
+                raise NativeError("nifty_amd hot-path ops run on the GPU only; no CPU fallback exists")
+            setattr(f, fld, v.data_ptr())
+        f.cg_stride = int(cg["stride"])
+        f.cg_shift = float(cg["shift"])
+        f.cg_nbtot = int(cg["nbtot"])
+        f.cg_blk0 = int(cg["blk0"])
     if batch:
         for t in tens:
             if t is not None and not t.is_cuda:

@@ -71,13 +71,21 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   FastArgs<T> b = a;
   b.ntiles = ntiles;
   b.bgroup = 0;
+  if (a.f.cg) {
+    // the CG update rides only in the strided unpack pass, one item per tile
+    if (KIND != K_UNPACK || ROWS || a.los != 0 || a.f.nb < 1 || a.g.O != a.f.nb || ntiles % a.g.O != 0) {
+      set_last_error("CG-carrying epilogue: needs the strided unpack pass with one item per tile");
+      return NFT_ERR_UNSUPPORTED;
+    }
+    b.f.ctr = ntiles / a.g.O;
+  }
   {
     // batch items sharing prologue / epilogue operands: keep one tile's items on one XCD
     const FuseArgs& f = a.f;
     const bool shared = (f.pro && ((f.pa && !f.sa) || (f.pb && !f.sb))) || (f.epi && ((f.ea && !f.sea) || (f.eb && !f.seb)));
     // measured slower at 2048^2 with 4 items (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us): opt-in
     static const bool on = getenv("NFT_BATCH_REMAP") != nullptr;
-    if (on && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) b.bgroup = f.nb;
+    if (on && shared && !f.cg && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) b.bgroup = f.nb;
   }
   // persistent grid (plain R2C rows): per_cu workgroups per CU
   static int ncu = 0;
@@ -92,7 +100,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   static const int per_cu = getenv("NFT_FFT_WG_PER_CU") ? atoi(getenv("NFT_FFT_WG_PER_CU")) : 8;
   static const char* const kind_name[4] = {"fft_c2c", "fft_r2c", "fft_h1d", "fft_unpack"};
   static const char* const kind_fused[4] = {"fft_c2c", "fft_r2c+pro", "fft_h1d+fused", "fft_unpack+epi"};
-  prof_mark(s, (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
+  prof_mark(s, a.f.cg ? "fft_unpack+cg" : (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
   bool launched = false;
   if constexpr (persist_ok<N, NT, KIND>()) {
     if (!launched && !a.f.pro) {

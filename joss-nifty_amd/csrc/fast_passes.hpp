@@ -40,6 +40,16 @@ struct FuseArgs {
   // (all transform axes), fundamental-cell strides fs[] (C order over n/2+1)
   int fnd;
   long long fn[3], fs[3];
+  // CG update carried by the unpack epilogue (nft_hartley_fuse.cg_*)
+  int cg;
+  void *cx, *cr;
+  const void* cd;
+  const double* csc;
+  double* cpart;
+  long long cst;   // row stride of x / r / d
+  double cshift;
+  int cnbtot, cblk0;
+  long long ctr;   // tiles per item of the carrying pass (set by the launcher)
 };
 
 // element index into pc of item-element j: its bin (pidx[j]) or, folded, the
@@ -93,6 +103,29 @@ __device__ __forceinline__ void fuse_store(const FuseArgs& f, T* out, long long 
   if (f.ed) r += (T)f.eshift * ((const T*)f.ed)[b * f.sd + j];
   out[b * f.so + j] = r;
   if (f.out2) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
+}
+
+// epilogue store that carries the CG update instead of storing q = ea * h:
+// the per-element arithmetic of cg_update_kernel (nft_blas.hip) on the value
+// q that pass would have read back
+template <typename T>
+__device__ __forceinline__ void fuse_store_cg(const FuseArgs& f, long long i, T h, T al, bool ok, T shift,
+                                              double& rr, double& xr) {
+  long long b, j;
+  fuse_split(f, i, b, j);
+  const T q = f.ea ? ((const T*)f.ea)[b * f.sea + j] * h : h;
+  if (f.out2) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
+  const long long e = b * f.cst + j;
+  T xi = ((T*)f.cx)[e], ri = ((T*)f.cr)[e];
+  if (ok) {
+    const T di = ((const T*)f.cd)[e];
+    xi = xi - al * di;
+    ri = ri - al * (q + shift * di);
+    ((T*)f.cx)[e] = xi;
+    ((T*)f.cr)[e] = ri;
+  }
+  rr += (double)ri * (double)ri;
+  xr += (double)xi * (double)ri;
 }
 
 template <typename T> struct FastArgs {
@@ -371,18 +404,68 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       __syncthreads();
       const T sg = (T)a.sigma, sc = a.scale;
       const int Nf = a.Nfull;
+      if (!a.f.cg) {
 #pragma unroll
-      for (int r = 0; r < VPT; ++r) {
-        int l, x;
-        lx_of(r, l, x);
-        const UnpackLine u = lines[l];
-        if (!u.valid) continue;
-        const C f = lds[l * PITCH + padx<PS>(x)];
-        const int k = (int)m * a.km + x * a.kx;
-        fuse_store<T>(a.f, out, u.base + (long long)k * a.rs, sc * (f.x + sg * f.y));
-        if (u.mirror) {
-          const int km = (k == 0) ? 0 : Nf - k;
-          fuse_store<T>(a.f, out, u.mbase + (long long)km * a.rs, sc * (f.x - sg * f.y));
+        for (int r = 0; r < VPT; ++r) {
+          int l, x;
+          lx_of(r, l, x);
+          const UnpackLine u = lines[l];
+          if (!u.valid) continue;
+          const C f = lds[l * PITCH + padx<PS>(x)];
+          const int k = (int)m * a.km + x * a.kx;
+          fuse_store<T>(a.f, out, u.base + (long long)k * a.rs, sc * (f.x + sg * f.y));
+          if (u.mirror) {
+            const int km = (k == 0) ? 0 : Nf - k;
+            fuse_store<T>(a.f, out, u.mbase + (long long)km * a.rs, sc * (f.x - sg * f.y));
+          }
+        }
+      } else {
+        // one item per tile (los = 0): its step length from its CG scalars
+        const long long item = o;
+        const double* scb = a.f.csc + item * NFT_CG_NSCALARS;
+        const double curv = scb[NFT_CG_CURV], gprev = scb[NFT_CG_GAMMA];
+        const double alpha = gprev / curv;
+        const bool ok = (curv == curv) && curv != 0.0 && (alpha >= 0.0) && (alpha == alpha) &&
+                        scb[NFT_CG_DONE] == 0.0;
+        const T al = (T)alpha, shift = (T)a.f.cshift;
+        double rr = 0.0, xr = 0.0;
+#pragma unroll
+        for (int r = 0; r < VPT; ++r) {
+          int l, x;
+          lx_of(r, l, x);
+          const UnpackLine u = lines[l];
+          if (!u.valid) continue;
+          const C f = lds[l * PITCH + padx<PS>(x)];
+          const int k = (int)m * a.km + x * a.kx;
+          fuse_store_cg<T>(a.f, u.base + (long long)k * a.rs, sc * (f.x + sg * f.y), al, ok, shift, rr, xr);
+          if (u.mirror) {
+            const int km = (k == 0) ? 0 : Nf - k;
+            fuse_store_cg<T>(a.f, u.mbase + (long long)km * a.rs, sc * (f.x - sg * f.y), al, ok, shift, rr, xr);
+          }
+        }
+        // fixed-order block sums (wave shuffles, then the waves in order)
+        __shared__ double cgsh[2 * (NT / 64)];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          rr += __shfl_down(rr, off, 64);
+          xr += __shfl_down(xr, off, 64);
+        }
+        if ((tid & 63) == 0) {
+          cgsh[2 * (tid >> 6)] = rr;
+          cgsh[2 * (tid >> 6) + 1] = xr;
+        }
+        __syncthreads();
+        if (tid == 0) {
+          double s0 = 0.0, s1 = 0.0;
+          for (int w = 0; w < NT / 64; ++w) {
+            s0 += cgsh[2 * w];
+            s1 += cgsh[2 * w + 1];
+          }
+          const long long nbt = a.f.cnbtot;
+          double* pp = a.f.cpart + item * 3 * nbt + a.f.cblk0 + (t - item * a.f.ctr);
+          pp[0] = s0;
+          pp[nbt] = s1;
+          pp[2 * nbt] = 0.0;
         }
       }
     }

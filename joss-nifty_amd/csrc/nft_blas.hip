@@ -457,7 +457,7 @@ int nft_cg_update_seg_batched(void* x, void* r, const void* d, const void* q, co
     return NFT_ERR_ARG;
   }
   const dim3 grid(nb, nrhs);
-  prof_mark(stream, "cg_update_kernel");
+  prof_mark(stream, "cg_update_seg");
   if (dtype == 0)
     hipLaunchKernelGGL(cg_update_kernel<double>, grid, dim3(RED_NT), 0, stream, (double*)x, (double*)r,
                        (const double*)d, (const double*)q, (const double*)b, (long long)n, (long long)vstride,

@@ -503,7 +503,7 @@ static bool v2_multi_ok(const Geo& g, const std::vector<int>& ax) {
 // of each item cost more than the re-reads save), so off by default
 static int epi_los(const fast::FuseArgs* fz, long long O) {
   static const int want = getenv("NFT_EPI_LO") ? atoi(getenv("NFT_EPI_LO")) : 0;
-  if (!fz || !fz->epi || fz->P <= 0 || fz->nb < 2) return 0;
+  if (!fz || !fz->epi || fz->cg || fz->P <= 0 || fz->nb < 2) return 0;
   if ((fz->ea && fz->sea) || (fz->eb && fz->seb)) return 0;
   int los = want;
   while (los > 0 && (O % (1LL << los)) != 0) --los;
@@ -567,6 +567,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
     if (fz) {
       a.f = *fz;
       a.f.epi = 0;
+      a.f.cg = 0;
     }
     if ((st = launch<T>(K_R2C, true, N, a, s)) != NFT_OK) return st;
   }
@@ -872,6 +873,11 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     int st = hartley_v2<T>(in, out, g, ax, sigma, scale, ws, ws_bytes, s, &f);
     if (st != NFT_FALLBACK) return st;
   }
+  if (f.cg) {
+    set_last_error("nft_hartley_fused: the CG-carrying epilogue needs the engine-v2 unpack pass "
+                   "(nft_hartley_cg_blocks == 0 for this geometry)");
+    return NFT_ERR_UNSUPPORTED;
+  }
   const long long n = prod(g.shape, 0, g.nd);
   const unsigned nb = (unsigned)std::min<long long>((n + 255) / 256, 65536);
   const void* src = in;
@@ -1061,12 +1067,64 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
       set_last_error("nft_hartley_fused: incomplete fusion spec");
       return NFT_ERR_ARG;
     }
+    f.cg = 0;
+    if (fz->cg_x) {
+      if (!fz->cg_r || !fz->cg_d || !fz->cg_sc || !fz->cg_part || fz->cg_nbtot < 1 || fz->cg_blk0 < 0 ||
+          f.P <= 0 || f.ed || !f.epi ||
+          nft_hartley_cg_blocks(ndim, shape, naxes, axes, dtype) + fz->cg_blk0 > fz->cg_nbtot) {
+        set_last_error("nft_hartley_fused: incomplete or unsupported CG epilogue spec");
+        return NFT_ERR_ARG;
+      }
+      f.cg = 1;
+      f.cx = fz->cg_x;
+      f.cr = fz->cg_r;
+      f.cd = fz->cg_d;
+      f.csc = fz->cg_sc;
+      f.cpart = fz->cg_part;
+      f.cst = fz->cg_stride;
+      f.cshift = fz->cg_shift;
+      f.cnbtot = fz->cg_nbtot;
+      f.cblk0 = fz->cg_blk0;
+    }
   }
   const int sigma = convention == 0 ? 1 : -1;
   if (dtype == 0) return hartley_fused_impl<double>(f, in, out, g, ax, sigma, scale, workspace, ws_bytes, hws, stream);
   if (dtype == 1) return hartley_fused_impl<float>(f, in, out, g, ax, sigma, scale, workspace, ws_bytes, hws, stream);
   set_last_error("bad dtype %d", dtype);
   return NFT_ERR_ARG;
+}
+
+int nft_hartley_cg_blocks(int ndim, const int64_t* shape, int naxes, const int* axes, int dtype) {
+  using namespace fast;
+  Geo g;
+  std::vector<int> ax;
+  if (parse_axes(ndim, shape, naxes, axes, g, ax) != NFT_OK) return 0;
+  const int m = (int)ax.size();
+  const int last = g.nd - 1;
+  // a leading batch axis and the engine-v2 strided last pass along ax[0] = 1
+  if (m < 2 || g.nd != m + 1 || ax[0] != 1 || (dtype != 0 && dtype != 1)) return 0;
+  const int h = ax[m - 1];
+  if (h != last || !rows_supported((int)g.shape[h])) return 0;
+  for (int k = 1; k < m - 1; ++k)
+    if (!strided_supported((int)g.shape[ax[k]])) return 0;
+  const int N0 = (int)g.shape[ax[0]];
+  long long cs[MAXD];
+  half_shape(g, h, cs);
+  const long long I = prod(cs, ax[0] + 1, g.nd);
+  long long M = 1;
+  int N = N0;
+  if (!(strided_supported(N0) || longcol_supported(N0))) {
+    if (!fourstep_supported(N0)) return 0;
+    int N1, N2;
+    fourstep_split(N0, N1, N2);
+    M = N1;
+    N = N2;
+  }
+  const int NT = nt_strided(N);
+  const long long L = (long long)NT * fast::VPT / N;
+  if (L < 1) return 0;
+  const long long tiles = M * ((I + L - 1) / L);
+  return tiles > 0x3fffffffLL ? 0 : (int)tiles;
 }
 
 int nft_fft_c2c(const void* in, void* out, int ndim, const int64_t* shape, int naxes, const int* axes,

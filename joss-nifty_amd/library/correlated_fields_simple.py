@@ -589,9 +589,21 @@ class CFJacobian(LinearOperator):
                                  interleave=True)
         return da
 
-    def mv_grid(self, D, da, Q, W, shift=0.0, qpart=None):
+    def cg_blocks(self, k):
+        """partial blocks per item of the CG-carrying adjoint epilogue at
+        this grid (nft_hartley_cg_blocks), 0 if unsupported"""
+        cache = self.__dict__.setdefault("_cgb", {})
+        if k not in cache:
+            grid = tuple(self._afull.shape)
+            cache[k] = _native.hartley_cg_blocks((k,) + grid, tuple(range(1, 1 + len(grid))), self._afull.dtype)
+        return cache[k]
+
+    def mv_grid(self, D, da, Q, W, shift=0.0, qpart=None, after_w=None, cg=None):
         """forward transform (with the prologue), W, adjoint transform: the
-        grid segment of Q and w = xi0 * v for the amplitude VJP"""
+        grid segment of Q and w = xi0 * v for the amplitude VJP.
+        after_w: called between W and the adjoint (the curvature fold);
+        cg: the grid segment's CG update carried by the adjoint's epilogue
+        (nft_hartley_fuse.cg_*) -- Q's grid segment is then not written."""
         m = self._m
         lay = self.layout
         k, size = D.shape
@@ -607,13 +619,16 @@ class CFJacobian(LinearOperator):
                               batch=dict(period=N, x=size, c=1, c_elem=k))
         g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
         g = g.contiguous()
+        if after_w is not None:
+            after_w()
         w = bufs["w"]
         epi = dict(a=self._afull, b=self._xi0, out2=w)
         bt = dict(period=N, out=size, out2=N)
         if shift != 0.0:
             epi.update(d=D[0, xo:], shift=shift)
             bt["d"] = size
-        _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt)
+        _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt,
+                              cg=cg)
         return w
 
     def mv_fold(self, w):

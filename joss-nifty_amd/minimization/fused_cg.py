@@ -262,12 +262,18 @@ class FusedCG:
         if nq:
             nbd = int(lib.nft_cg_dd_blocks(n))
             pq = torch.empty((1, nbd + nq), dtype=torch.float64, device=x.device)
-            if _SPLIT and x.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
+            if x.dtype == torch.float64 and not _reads_value(ctl) and _CarryIteration.supported(core, 1):
+                # FusedCGBatch's iteration with k = 1 (same partial layout)
+                split = _CarryIteration(lib, core, self.W, n, 1, nq, sh)
+            elif _SPLIT and x.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
                 # FusedCGBatch's split iteration with k = 1 (same partial layout)
                 split = _SplitIteration(lib, core, self.W, n, 1, nq, sh, b is not None)
 
         def body(with_dir):
             s_ = _native.stream_ptr()
+            if with_dir and isinstance(split, _CarryIteration):
+                split(x.view(1, -1), r.view(1, -1), d.view(1, -1), q.view(1, -1), sc.view(1, -1))
+                return
             if with_dir and split is not None:
                 split(x.view(1, -1), r.view(1, -1), d.view(1, -1), q.view(1, -1),
                       b.view(1, -1) if b is not None else None, sc.view(1, -1))
@@ -479,6 +485,73 @@ class _SplitIteration:
         _native._check(lib.nft_cg_finalize_batched(_native.ptr(self.UP), self.nbtot, self.k, _native.ptr(SC), s_))
 
 
+# The grid segment's CG update carried by the adjoint transform's epilogue
+# (data-space curvature: alpha is known before the adjoint): q's grid segment
+# is neither stored nor read back (NFT_CG_CARRY=0: separate update pass)
+_CARRY = os.environ.get("NFT_CG_CARRY", "1") != "0"
+
+
+class _CarryIteration:
+    """One CG iteration (k RHS, count-only controllers, no energy values)
+    with the update of the grid segment G (the 'xi' key) inside the adjoint
+    transform's last pass:
+
+      dir + d.d partials | amplitude JVP | forward transform, W (LOS with the
+      (R J d).C(R J d) partials), curvature fold | adjoint transform whose
+      epilogue updates x, r on G and writes its r.r, x.r partials per tile |
+      bin sums, amplitude VJP | update of the amplitude segments | finalize
+
+    The per-element arithmetic is that of the separate update; the dot
+    partials are [amplitude keys before G][G's tiles][keys after G], folded
+    in that order.  The same for k = 1 (FusedCG) and k > 1 (FusedCGBatch)."""
+
+    def __init__(self, lib, core, W, n, k, nq, shift):
+        self.lib, self.core, self.W = lib, core, W
+        self.n, self.k, self.nq, self.shift = n, k, nq, shift
+        g0, g1 = core.grid_segment()
+        self.g0 = g0
+        tiles = core.cg_blocks(k)
+        nb0 = int(lib.nft_cg_dd_blocks(g0)) if g0 > 0 else 0
+        nb1 = int(lib.nft_cg_dd_blocks(n - g1)) if n > g1 else 0
+        self.amp = [(o, e - o, blk) for (o, e), blk in (((0, g0), 0), ((g1, n), nb0 + tiles)) if e > o]
+        self.tiles_blk0 = nb0
+        self.nbtot = nb0 + tiles + nb1
+        self.nbd = int(lib.nft_cg_dd_blocks(n))
+        dev = core.device
+        self.PQ = torch.empty((k, self.nbd + nq), dtype=torch.float64, device=dev)
+        self.UP = torch.empty((k, 3 * self.nbtot), dtype=torch.float64, device=dev)
+
+    @staticmethod
+    def supported(core, k):
+        return _CARRY and hasattr(core, "cg_blocks") and core.cg_blocks(k) > 0
+
+    def __call__(self, X, Rr, D, Q, SC):
+        core, lib = self.core, self.lib
+        P = _native.ptr
+        s_ = _native.stream_ptr()
+        n, k = self.n, self.k
+        _native._check(lib.nft_cg_direction_dd_batched(P(D), P(Rr), n, n, k, 0, P(SC), self.shift, P(self.PQ),
+                                                       self.nbd + self.nq, s_))
+        da = core.mv_amp_jvp(D)
+
+        def fold():
+            _native._check(lib.nft_fold_partials(P(self.PQ), self.nbd + self.nq, k,
+                                                 ctypes.c_void_p(SC.data_ptr() + _native.CG_CURV * 8),
+                                                 _native.CG_NSCALARS, _native.stream_ptr()))
+        g0 = self.g0
+        cg = dict(x=X[0, g0:], r=Rr[0, g0:], d=D[0, g0:], sc=SC, part=self.UP, stride=n, shift=self.shift,
+                  nbtot=self.nbtot, blk0=self.tiles_blk0)
+        w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbd:], after_w=fold, cg=cg)
+        core.mv_amp_vjp(D, w, Q, 0.0)
+        Pv = ctypes.c_void_p
+        for o, ln, blk in self.amp:
+            e = 8 * o
+            _native._check(lib.nft_cg_update_seg_batched(
+                Pv(X.data_ptr() + e), Pv(Rr.data_ptr() + e), Pv(D.data_ptr() + e), Pv(Q.data_ptr() + e), Pv(0),
+                ln, n, k, 0, self.shift, P(SC), P(self.UP), self.nbtot, blk, s_))
+        _native._check(lib.nft_cg_finalize_batched(P(self.UP), self.nbtot, k, P(SC), s_))
+
+
 class FusedCGBatch(FusedCG):
     """k independent conjugate-gradient solves with the same metric, run in
     lock step: every iteration is ONE batched matvec (the LOS matrix, the FFT
@@ -588,11 +661,16 @@ class FusedCGBatch(FusedCG):
         if nq:
             nbd = int(lib.nft_cg_dd_blocks(n))
             PQ = torch.empty((k, nbd + nq), dtype=torch.float64, device=dev)
-            if _SPLIT and X.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
+            if X.dtype == torch.float64 and Bu is None and _CarryIteration.supported(core, k):
+                split = _CarryIteration(lib, core, self.W, n, k, nq, sh)
+            elif _SPLIT and X.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
                 split = _SplitIteration(lib, core, self.W, n, k, nq, sh, Bu is not None)
 
         def body(with_dir):
             s_ = _native.stream_ptr()
+            if with_dir and isinstance(split, _CarryIteration):
+                split(X, Rr, D, Q, SC)
+                return
             if with_dir and split is not None:
                 split(X, Rr, D, Q, Bu, SC)
                 return

@@ -62,6 +62,14 @@ def main():
             two()
         torch.cuda.synchronize()
         return
+    if "--trace-graph" in sys.argv:   # graph replays of the one-stream iteration
+        for _ in range(3):
+            one()
+        g = fused_cg._capture(one)
+        for _ in range(5):
+            g.replay()
+        torch.cuda.synchronize()
+        return
     for name, fn in (("one-stream", one), ("split", two), ("amp chains only", amp_only)):
         res[name + " eager"] = timeit(fn)
         g = fused_cg._capture(fn)
