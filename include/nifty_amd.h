@@ -236,6 +236,20 @@ typedef struct nft_hartley_fuse {
   int64_t cg_stride;
   double cg_shift;
   int32_t cg_nbtot, cg_blk0;
+  /* CG direction carried by the folded prologue (dir_r != NULL, pro_folded,
+   * batched): pro_x holds each item's previous direction d and is
+   * overwritten with d = max(0, gamma / gprev) d + r (item b's scalar block
+   * b * NFT_CG_NSCALARS of dir_sc; unchanged, partial 0, when its DONE is set)
+   * before the prologue reads it, and dir_part[b * dir_pstride + dir_blk0 +
+   * block] = dir_shift * (the block's sum of d^2), block <
+   * ceil(prod(n_a / 2 + 1) / 256) -- the d.d partials of
+   * nft_cg_direction_dd_batched for the grid segment. */
+  const void* dir_r;
+  const double* dir_sc;
+  double* dir_part;
+  int64_t dir_pstride;
+  double dir_shift;
+  int32_t dir_blk0, dir_pad;
 } nft_hartley_fuse;
 
 /* Partial blocks per item of the CG-carrying epilogue for a batched

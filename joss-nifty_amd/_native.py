@@ -82,7 +82,9 @@ class HartleyFuse(ctypes.Structure):
                                     "out2_bstride", "c_estride", "a_bstride", "b_bstride", "ea_bstride",
                                     "eb_bstride", "pro_folded")] + \
                [(n, _p) for n in ("cg_x", "cg_r", "cg_d", "cg_sc", "cg_part")] + \
-               [("cg_stride", _i64), ("cg_shift", _d), ("cg_nbtot", ctypes.c_int32), ("cg_blk0", ctypes.c_int32)]
+               [("cg_stride", _i64), ("cg_shift", _d), ("cg_nbtot", ctypes.c_int32), ("cg_blk0", ctypes.c_int32)] + \
+               [(n, _p) for n in ("dir_r", "dir_sc", "dir_part")] + \
+               [("dir_pstride", _i64), ("dir_shift", _d), ("dir_blk0", ctypes.c_int32), ("dir_pad", ctypes.c_int32)]
 
 
 class LosPlan(ctypes.Structure):
@@ -352,6 +354,17 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
             tens.append(v)
             setattr(f, fld, v.data_ptr() if v is not None else None)
         f.pro_folded = 1 if pro.get("fold") else 0
+        dr = pro.get("dir")
+        if dr:
+            # the CG direction carried by the folded prologue (nft_hartley_fuse.dir_*)
+            for k, fld in (("r", "dir_r"), ("sc", "dir_sc"), ("part", "dir_part")):
+                v = dr[k]
+                if not v.is_cuda:
+                    raise NativeError("nifty_amd hot-path ops run on the GPU only; no CPU fallback exists")
+                setattr(f, fld, v.data_ptr())
+            f.dir_pstride = int(dr["pstride"])
+            f.dir_shift = float(dr["shift"])
+            f.dir_blk0 = int(dr["blk0"])
     if epi:
         for k, fld in (("a", "epi_a"), ("d", "epi_d"), ("b", "epi_b"), ("out2", "epi_out2")):
             v = epi.get(k)

@@ -50,6 +50,13 @@ struct FuseArgs {
   double cshift;
   int cnbtot, cblk0;
   long long ctr;   // tiles per item of the carrying pass (set by the launcher)
+  // CG direction carried by the folded prologue (nft_hartley_fuse.dir_*)
+  const void* dr;
+  const double* dsc;
+  double* dpart;
+  long long dps;
+  double dshift;
+  int dblk0;
 };
 
 // element index into pc of item-element j: its bin (pidx[j]) or, folded, the

@@ -754,6 +754,27 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
   using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   const bool vec = f.ce == nb && f.sc == 1 && (nb & 1) == 0 && nb <= 8;
   const int D = f.fnd;
+  // the CG direction update carried here (f.dr): d = max(0, gamma/gprev) d + r
+  // per item, written back to px, d.d accumulated per item (nb <= 8)
+  const bool dirc = f.dr != nullptr;
+  T* __restrict__ pd = const_cast<T*>(px);
+  const T* __restrict__ pr = (const T*)f.dr;
+  T bt[8];
+  bool live[8];
+  double dd[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    dd[b] = 0.0;
+    bt[b] = (T)0;
+    live[b] = false;
+    if (dirc && b < nb) {
+      const double* scb = f.dsc + b * NFT_CG_NSCALARS;
+      live[b] = scb[NFT_CG_DONE] == 0.0;
+      double beta = scb[NFT_CG_GAMMA] / scb[NFT_CG_GPREV];
+      if (!(beta > 0.0)) beta = 0.0;
+      bt[b] = (T)beta;
+    }
+  }
   for (long long c = (long long)blockIdx.x * 256 + threadIdx.x; c < ncell; c += (long long)gridDim.x * 256) {
     unsigned cc[3], nn[3], rest = (unsigned)c;
     for (int a = D - 1; a >= 0; --a) {
@@ -791,7 +812,21 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
       if (dup) continue;
       const T a = pa ? pa[j] : (T)1;
       const T bj = pb[j];
-      if (vec) {
+      if (dirc) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          if (b >= nb) break;
+          T v = px[b * f.sx + j];
+          if (live[b]) {
+            v = bt[b] * v + pr[b * f.sx + j];
+            pd[b * f.sx + j] = v;
+            dd[b] += (double)v * (double)v;
+          }
+          if (pa) v *= a;
+          v += bj * (vec ? cv[b] : pc[b * f.sc + ix]);
+          u[b * P + j] = v;
+        }
+      } else if (vec) {
         for (int b = 0; b < nb; ++b) {
           T v = px[b * f.sx + j];
           if (pa) v *= a;
@@ -808,6 +843,23 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
       }
     }
   }
+  if (dirc) {
+    // per item: wave shuffles, then the four waves in order (fixed order)
+    __shared__ double dsh[4][8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      double v = dd[b];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if ((threadIdx.x & 63) == 0) dsh[threadIdx.x >> 6][b] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)nb) {
+      const int b = threadIdx.x;
+      const double t = ((dsh[0][b] + dsh[1][b]) + dsh[2][b]) + dsh[3][b];
+      f.dpart[b * f.dps + f.dblk0 + blockIdx.x] = live[b] ? f.dshift * t : 0.0;
+    }
+  }
 }
 
 template <typename T>
@@ -822,7 +874,7 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
   // gathers, 32 B per pixel from a 10 MB table, stay latency-bound inside
   // the FFT workgroup) -- opt-in, NFT_PRO_PAIRS=1
   static const bool pairs = getenv("NFT_PRO_PAIRS") != nullptr;
-  if (!v1_only && pairs && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && f.nb >= 1 &&
+  if (!v1_only && pairs && !f.dr && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && f.nb >= 1 &&
       (long long)f.nb * f.P == ntot && v2_multi_ok(g, ax)) {
     // R2C row pass with the prologue, the items' rows paired as in the plain pass
     const int N = (int)g.shape[g.nd - 1];
@@ -843,7 +895,12 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
       if (st != 1) return st;
     }
   }
-  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && f.nb > 1 &&
+  if (f.dr && !(f.fnd > 0 && f.pb && !v1_only && !no_split && f.sa == 0 && f.sb == 0 && f.P > 0 &&
+                (long long)f.nb * f.P == ntot && ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T))) {
+    set_last_error("nft_hartley_fused: the direction carried by the prologue needs the folded batched prologue pass");
+    return NFT_ERR_UNSUPPORTED;
+  }
+  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && (f.nb > 1 || f.dr) &&
       (long long)f.nb * f.P == ntot &&
       ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
     T* u = (T*)((char*)ws + align256(hws));
@@ -1066,6 +1123,21 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     if ((f.pb && (!f.pc || !f.pidx)) || (f.out2 && !f.eb)) {
       set_last_error("nft_hartley_fused: incomplete fusion spec");
       return NFT_ERR_ARG;
+    }
+    f.dr = nullptr;
+    if (fz->dir_r) {
+      if (!fz->pro_folded || !f.pb || f.P <= 0 || f.nb < 1 || f.nb > 8 || !fz->dir_sc || !fz->dir_part ||
+          fz->dir_blk0 < 0 || fz->dir_pstride < fz->dir_blk0 + 1) {
+        set_last_error("nft_hartley_fused: the direction carried by the prologue needs a folded, batched "
+                       "prologue (<= 8 items) and its scalars / partials");
+        return NFT_ERR_ARG;
+      }
+      f.dr = fz->dir_r;
+      f.dsc = fz->dir_sc;
+      f.dpart = fz->dir_part;
+      f.dps = fz->dir_pstride;
+      f.dshift = fz->dir_shift;
+      f.dblk0 = fz->dir_blk0;
     }
     f.cg = 0;
     if (fz->cg_x) {

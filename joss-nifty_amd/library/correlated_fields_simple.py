@@ -598,12 +598,23 @@ class CFJacobian(LinearOperator):
             cache[k] = _native.hartley_cg_blocks((k,) + grid, tuple(range(1, 1 + len(grid))), self._afull.dtype)
         return cache[k]
 
-    def mv_grid(self, D, da, Q, W, shift=0.0, qpart=None, after_w=None, cg=None):
+    def dir_blocks(self, k):
+        """d.d partial blocks of the CG direction carried by the folded
+        prologue (nft_hartley_fuse.dir_*), 0 where the prologue is not folded"""
+        jb = self._m.jbins
+        if not (_PRO_FOLD and jb.fold is not None) or not (1 <= k <= 8):
+            return 0
+        ncell = int(np.prod([n // 2 + 1 for n in jb.fold["shape"]]))
+        return (ncell + 255) // 256
+
+    def mv_grid(self, D, da, Q, W, shift=0.0, qpart=None, after_w=None, cg=None, pro_dir=None):
         """forward transform (with the prologue), W, adjoint transform: the
         grid segment of Q and w = xi0 * v for the amplitude VJP.
         after_w: called between W and the adjoint (the curvature fold);
         cg: the grid segment's CG update carried by the adjoint's epilogue
-        (nft_hartley_fuse.cg_*) -- Q's grid segment is then not written."""
+        (nft_hartley_fuse.cg_*) -- Q's grid segment is then not written.
+        pro_dir: the grid segment's CG direction update carried by the folded
+        prologue (nft_hartley_fuse.dir_*): D's grid segment is updated in place."""
         m = self._m
         lay = self.layout
         k, size = D.shape
@@ -615,6 +626,8 @@ class CFJacobian(LinearOperator):
         conv = hartley_convention_code()
         s = bufs["s"]
         pro = dict(a=self._afull, x=D[0, xo:], b=self._xi0, **self._pro_bins(da, k))
+        if pro_dir is not None:
+            pro["dir"] = pro_dir
         _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
                               batch=dict(period=N, x=size, c=1, c_elem=k))
         g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W

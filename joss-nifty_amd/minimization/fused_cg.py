@@ -489,6 +489,9 @@ class _SplitIteration:
 # (data-space curvature: alpha is known before the adjoint): q's grid segment
 # is neither stored nor read back (NFT_CG_CARRY=0: separate update pass)
 _CARRY = os.environ.get("NFT_CG_CARRY", "1") != "0"
+# ... and the grid segment's direction update inside the folded prologue
+# (NFT_CG_CARRY_DIR=0: a separate direction pass)
+_CARRY_DIR = os.environ.get("NFT_CG_CARRY_DIR", "1") != "0"
 
 
 class _CarryIteration:
@@ -516,7 +519,17 @@ class _CarryIteration:
         self.amp = [(o, e - o, blk) for (o, e), blk in (((0, g0), 0), ((g1, n), nb0 + tiles)) if e > o]
         self.tiles_blk0 = nb0
         self.nbtot = nb0 + tiles + nb1
-        self.nbd = int(lib.nft_cg_dd_blocks(n))
+        # the direction: the grid segment's inside the folded prologue when
+        # available (d.d partials [keys before][prologue blocks][keys after]),
+        # else one pass over the whole vector
+        pb = core.dir_blocks(k) if (_CARRY_DIR and hasattr(core, "dir_blocks")) else 0
+        if pb:
+            self.dirs = [(o, e - o, blk) for (o, e), blk in (((0, g0), 0), ((g1, n), nb0 + pb)) if e > o]
+            self.pro_blk0 = nb0
+            self.nbd = nb0 + pb + nb1
+        else:
+            self.dirs = None
+            self.nbd = int(lib.nft_cg_dd_blocks(n))
         dev = core.device
         self.PQ = torch.empty((k, self.nbd + nq), dtype=torch.float64, device=dev)
         self.UP = torch.empty((k, 3 * self.nbtot), dtype=torch.float64, device=dev)
@@ -530,8 +543,19 @@ class _CarryIteration:
         P = _native.ptr
         s_ = _native.stream_ptr()
         n, k = self.n, self.k
-        _native._check(lib.nft_cg_direction_dd_batched(P(D), P(Rr), n, n, k, 0, P(SC), self.shift, P(self.PQ),
-                                                       self.nbd + self.nq, s_))
+        Pv = ctypes.c_void_p
+        pstride = self.nbd + self.nq
+        pro_dir = None
+        if self.dirs is None:
+            _native._check(lib.nft_cg_direction_dd_batched(P(D), P(Rr), n, n, k, 0, P(SC), self.shift, P(self.PQ),
+                                                           pstride, s_))
+        else:
+            for o, ln, blk in self.dirs:
+                _native._check(lib.nft_cg_direction_dd_batched(
+                    Pv(D.data_ptr() + 8 * o), Pv(Rr.data_ptr() + 8 * o), ln, n, k, 0, P(SC), self.shift,
+                    Pv(self.PQ.data_ptr() + 8 * blk), pstride, s_))
+            pro_dir = dict(r=Rr[0, self.g0:], sc=SC, part=self.PQ, pstride=pstride, shift=self.shift,
+                           blk0=self.pro_blk0)
         da = core.mv_amp_jvp(D)
 
         def fold():
@@ -541,9 +565,8 @@ class _CarryIteration:
         g0 = self.g0
         cg = dict(x=X[0, g0:], r=Rr[0, g0:], d=D[0, g0:], sc=SC, part=self.UP, stride=n, shift=self.shift,
                   nbtot=self.nbtot, blk0=self.tiles_blk0)
-        w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbd:], after_w=fold, cg=cg)
+        w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbd:], after_w=fold, cg=cg, pro_dir=pro_dir)
         core.mv_amp_vjp(D, w, Q, 0.0)
-        Pv = ctypes.c_void_p
         for o, ln, blk in self.amp:
             e = 8 * o
             _native._check(lib.nft_cg_update_seg_batched(
