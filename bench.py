@@ -193,7 +193,7 @@ def cg_iteration_wall(lib, core, W, shift, bufs, k, reps=20):
     return t0.elapsed_time(t1) * 1e3 / reps, split is not None
 
 
-def byte_model(cf, R, k, n_lat):
+def byte_model(cf, R, k, n_lat, dir_carried=False):
     """Algorithmic bytes per launch (fp64, every operand array counted once per
     launch; arrays shared by the k right-hand sides -- amplitude, xi0, pindex,
     the LOS matrix and its scales -- once).  DESIGN.md §3."""
@@ -216,6 +216,8 @@ def byte_model(cf, R, k, n_lat):
         "pro_batch": 8 * k * N + 8 * N + 8 * N + 4 * N + 8 * k * B + 8 * k * N,
         # folded: the cell's bin (N_f), dA gathered per mirror class; no pindex
         "pro_fold": 8 * k * N + 8 * N + 8 * N + 4 * Nf + 8 * k * B + 8 * k * N,
+        # ... carrying the grid segment's CG direction: d, r in, d out (k)
+        "pro_fold+dir": 24 * k * N + 8 * N + 8 * N + 4 * Nf + 8 * k * B + 8 * k * N,
         "fft_r2c": 8 * k * N + 16 * k * Hh,
         "fft_c2c": 2 * 16 * k * Hh,
         "fft_unpack": 16 * k * Hh + 8 * k * N,
@@ -230,7 +232,9 @@ def byte_model(cf, R, k, n_lat):
         # perm over the cell, cell values (k), bin offsets, sums (k)
         "bin_scatter": 4 * Nf + 8 * k * Nf + 4 * B + 8 * k * B,
         "cg_dir_kernel": 3 * 8 * k * n_lat,
-        "cg_dir_dd": 3 * 8 * k * n_lat,
+        # whole vector, or (direction carried by the prologue) two launches
+        # over the keys before / after the grid segment, half their bytes each
+        "cg_dir_dd": 3 * 8 * k * (n_lat if not dir_carried else (n_lat - N) // 2),
         "curv_partial": 2 * 8 * k * n_lat,
         # x, r, d, q in; x, r out (b is not streamed: the probe passes none,
         # and the sampling CG's value-blind controllers skip it too)
@@ -280,7 +284,10 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
         a = acc.setdefault(lab, [0, 0.0])
         a[0] += 1
         a[1] += ms
-    model = byte_model(cf, R, k, n_lat)
+    from nifty_amd.minimization import fused_cg
+    dcar = bool(fused_cg._CARRY and fused_cg._CARRY_DIR and getattr(core, "dir_blocks", lambda k: 0)(k) > 0
+                and _CARRY_CACHE)
+    model = byte_model(cf, R, k, n_lat, dir_carried=dcar)
     out = {}
     tot_us, tot_b = 0.0, 0
     for lab, (cnt, tot) in acc.items():

@@ -910,7 +910,7 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     if (f.fnd > 0 && f.pb) {
       long long ncell = 1;
       for (int a = 0; a < f.fnd; ++a) ncell *= f.fn[a] / 2 + 1;
-      prof_mark(s, "pro_fold");
+      prof_mark(s, f.dr ? "pro_fold+dir" : "pro_fold");
       hipLaunchKernelGGL(pro_fold_kernel<T>, dim3((unsigned)((ncell + 255) / 256)), dim3(256), 0, s, f, u, f.P, f.nb,
                          ncell);
     } else {
