@@ -23,6 +23,9 @@
 //        sums pixel t's run; the box tile is written coalesced.
 //
 // All reductions run in a fixed order: deterministic, no atomics.
+#include <algorithm>
+#include <cstdlib>
+
 #include "nft_api_internal.hpp"
 
 namespace nft {
@@ -356,9 +359,145 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   }
 }
 
+// Persistent, prefetching variant for K > 1: workgroup w processes items
+// w, w + G, w + 2G, ... and loads the next item's entries, pixel values and
+// segment bounds into registers while the current one is summed from LDS
+// (one item per workgroup leaves each workgroup a load -> barrier -> sum ->
+// store chain with nothing to overlap).  Same products and summation order
+// per segment and vector as los_fwd_items (bitwise).
+template <typename T, int K>
+__global__ __launch_bounds__(256) void los_fwd_items_pf(nft_los_plan p, const T* __restrict__ x,
+                                                        const T* __restrict__ cs, double* __restrict__ part,
+                                                        long long xs, int pk, long long css) {
+#pragma clang fp contract(off)
+  static_assert(K > 1, "the persistent variant serves batched launches");
+  constexpr int PER = LOS_CAP_F / 256;
+  constexpr int RND = LOS_SEG_ROUNDS;
+  __shared__ double u[K][256];
+  __shared__ float ew[LOS_CAP_F];
+  __shared__ unsigned char el[LOS_CAP_F];
+  const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
+  const int t = threadIdx.x;
+  const int sub = t & 3;
+  // the item in flight (registers)
+  int e0n, nn, s0n, s1n;
+  float wv[PER];
+  unsigned char lv[PER];
+  double xv[K];
+  int san[RND], sbn[RND], son[RND];
+  auto load = [&](int it) {
+    const int box = p.item_box[it];
+    bool ok;
+    const long long px = g.pixel(box, t, ok);
+    s0n = p.item_seg[it];
+    s1n = p.item_seg[it + 1];
+    e0n = p.item_ent[it];
+    nn = p.item_ent[it + 1] - e0n;
+    const bool st = nn <= LOS_CAP_F;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = t + i * 256;
+      wv[i] = (st && k < nn) ? p.ent_wf[e0n + k] : 0.f;
+      lv[i] = (st && k < nn) ? p.ent_loc[e0n + k] : 0;
+    }
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      double v = 0.0;
+      if (ok) {
+        v = (double)x[b * xs + px];
+        if (cs) v *= (double)cs[b * css + px];
+      }
+      xv[b] = v;
+    }
+    const int sq = s0n + (t >> 2);
+#pragma unroll
+    for (int r = 0; r < RND; ++r) {
+      const int s = sq + 64 * r;
+      san[r] = s < s1n ? p.seg_ent[s] - e0n : 0;
+      sbn[r] = s < s1n ? p.seg_ent[s + 1] - e0n : 0;
+      son[r] = s < s1n ? p.seg_slot[s] : 0;
+    }
+  };
+  int it = blockIdx.x;
+  if (it < p.nitems) load(it);
+  while (it < p.nitems) {
+    // stage the current item, keep its segment bounds
+    const int e0 = e0n, n = nn, s0 = s0n, s1 = s1n;
+    const bool staged = n <= LOS_CAP_F;
+    int sa[RND], sb[RND], so[RND];
+#pragma unroll
+    for (int r = 0; r < RND; ++r) {
+      sa[r] = san[r];
+      sb[r] = sbn[r];
+      so[r] = son[r];
+    }
+#pragma unroll
+    for (int b = 0; b < K; ++b) u[b][t] = xv[b];
+    if (staged) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int k = t + i * 256;
+        if (k < n) {
+          ew[k] = wv[i];
+          el[k] = lv[i];
+        }
+      }
+    }
+    __syncthreads();
+    const int nx = it + (int)gridDim.x;
+    if (nx < p.nitems) load(nx);  // in flight while this item is summed
+    auto segk = [&](int slot, int a, int e) {
+      double acc[K];
+#pragma unroll
+      for (int b = 0; b < K; ++b) acc[b] = 0.0;
+      for (int k = a + sub; k < e; k += 4) {
+        const double w = staged ? (double)ew[k] : (double)p.ent_wf[e0 + k];
+        const int l = staged ? el[k] : p.ent_loc[e0 + k];
+#pragma unroll
+        for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[b][l];
+      }
+#pragma unroll
+      for (int b = 0; b < K; ++b) {
+        double v = acc[b];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        if ((b & 3) == sub) part[(long long)slot * pk + b] = v;
+      }
+    };
+    const int sq = s0 + (t >> 2);
+#pragma unroll
+    for (int r = 0; r < RND; ++r)
+      if (sq + 64 * r < s1) segk(so[r], sa[r], sb[r]);
+    for (int s = sq + 64 * RND; s < s1; s += 64) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
+    __syncthreads();  // LDS free for the next item
+    it = nx;
+  }
+}
+
 template <typename T, int K>
 static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* part, long long xs, int pk,
                         long long css, hipStream_t s) {
+  if constexpr (K > 1) {
+    // opt-in (NFT_LOS_PF=1, NFT_LOS_PF_WG workgroups per CU, default 8):
+    // measured slower at 4 x 2048^2 / 16384 lines (CG iteration 1257 ->
+    // 1310 / 1306 / 1291 us at 8 / 4 / 16 workgroups per CU) -- one item per
+    // workgroup, dispatched by the hardware, keeps more loads in flight
+    static const int pf = getenv("NFT_LOS_PF") ? atoi(getenv("NFT_LOS_PF")) : 0;
+    if (pf > 0) {
+      static int grid = 0;
+      if (grid == 0) {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+          ncu = 256;
+        const int per = getenv("NFT_LOS_PF_WG") ? atoi(getenv("NFT_LOS_PF_WG")) : 8;
+        grid = ncu * (per > 0 ? per : 8);
+      }
+      const unsigned gsz = (unsigned)std::min<long long>(p->nitems, grid);
+      hipLaunchKernelGGL((los_fwd_items_pf<T, K>), dim3(gsz), dim3(256), 0, s, *p, x, cs, part, xs, pk, css);
+      return;
+    }
+  }
   hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, pk,
                      css);
 }
