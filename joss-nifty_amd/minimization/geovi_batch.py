@@ -73,6 +73,23 @@ def _rowdots(pairs):
     return out.cpu().numpy()
 
 
+def _pairdots(pairs):
+    """[(a, b), ...] of 1-D device vectors -> host array of their fp64 dot
+    products (nft_dot per pair, one D2H copy; each equals the row of a
+    batched nft_dot_batched bit for bit)"""
+    lib = _native.load()
+    nmax = max(a.numel() for a, _ in pairs)
+    out = torch.empty(len(pairs), dtype=torch.float64, device=pairs[0][0].device)
+    ws = _native.workspace(lib.nft_reduce_workspace(nmax), out.device, "pairdot")
+    P = _native.ptr
+    for i, (a, b) in enumerate(pairs):
+        a, b = a.contiguous(), b.contiguous()
+        assert a.shape == b.shape
+        _native._check(lib.nft_dot(P(a), P(b), a.numel(), _native.dtype_code(a.dtype), P(out[i:]), P(ws),
+                                   _native.stream_ptr()))
+    return out.cpu().numpy()
+
+
 # ------------------------------------------------------------------ stages
 from ..library.correlated_fields_simple import _PRO_FOLD  # noqa: E402
 
@@ -491,6 +508,7 @@ class GeoVIBatch:
         X = torch.stack(starts)
         M = torch.stack(means)
         self._M = {i: M[i] for i in range(k)}
+        self._Mall = M
         vals, gn, G, states = self.evaluate(X, M)
         gens, pending, results = [], {}, [None] * k
         for i in range(k):
@@ -530,8 +548,14 @@ class GeoVIBatch:
             results[i] = e.value
 
     def _serve_at(self, reqs):
-        X = torch.stack([r[1].x + r[2] * r[3].v for _, r in reqs])
-        M = torch.stack([self._M[r[1].sample] for _, r in reqs])
+        # rows x + alpha p formed in place (alpha p, then + x: the reference's
+        # two roundings), no stacking copy
+        X = torch.empty((len(reqs), self.layout.size), dtype=reqs[0][1][1].x.dtype, device=self.x0.device)
+        for j, (_, r) in enumerate(reqs):
+            torch.mul(r[3].v, r[2], out=X[j])
+            X[j].add_(r[1].x)
+        idx = [r[1].sample for _, r in reqs]
+        M = self._Mall if idx == list(range(self._Mall.shape[0])) else self._Mall[idx]
         vals, gn, G, states = self.evaluate(X, M)
         out = {}
         for j, (i, r) in enumerate(reqs):
@@ -544,9 +568,9 @@ class GeoVIBatch:
         return out
 
     def _serve_dd(self, reqs):
-        G = torch.stack([r[1].g for _, r in reqs])
-        P = torch.stack([r[2].v for _, r in reqs])
-        h = _rowdots([(G, P)])[0]
+        # one dot per request on the rows where they live (bitwise the
+        # batched dot of the stacked rows, without the stacking copies)
+        h = _pairdots([(r[1].g, r[2].v) for _, r in reqs])
         return {i: float(h[j]) for j, (i, _) in enumerate(reqs)}
 
     def _serve_dir(self, reqs):
