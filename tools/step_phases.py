@@ -76,8 +76,12 @@ def main():
     from nifty_amd.minimization import geovi_batch
     ift.config.set_device("cuda:0")
     cf, Rr, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
-    H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=100))
-    mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=2), max_cg_iterations=50)
+    if "--demo" in sys.argv:     # SURVEY 8(d)'s demo controllers (bench.py demo_step)
+        H = ift.StandardHamiltonian(lh, ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=100))
+        mini = ift.NewtonCG(ift.AbsDeltaEnergyController(deltaE=0.5, convergence_level=2, iteration_limit=15))
+    else:
+        H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=100))
+        mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=2), max_cg_iterations=50)
     ift.random.push_sseq_from_seed(1000)
 
     def step():
@@ -95,6 +99,9 @@ def main():
         timed(gb, "refine", "geovi refine (NewtonCG, batched)")
         return gb
     geovi_batch.plan = plan
+    timed(geovi_batch.GeoVIBatch, "_serve_dir", "  refine: Newton directions (batched CG)")
+    timed(geovi_batch.GeoVIBatch, "_serve_at", "  refine: energies at trial points")
+    timed(geovi_batch.GeoVIBatch, "_serve_dd", "  refine: directional derivatives")
     from nifty_amd.operators import sampling_enabler as se
     timed(se.SamplingEnabler, "solve_rhs", "linear sampling CG (batched)")
     timed(se.SamplingEnabler, "draw_rhs", "draw_rhs (sample right-hand sides)")
