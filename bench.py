@@ -193,7 +193,7 @@ def cg_iteration_wall(lib, core, W, shift, bufs, k, reps=20):
     return t0.elapsed_time(t1) * 1e3 / reps, split is not None
 
 
-def byte_model(cf, R, k, n_lat, dir_carried=False):
+def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False):
     """Algorithmic bytes per launch (fp64, every operand array counted once per
     launch; arrays shared by the k right-hand sides -- amplitude, xi0, pindex,
     the LOS matrix and its scales -- once).  DESIGN.md §3."""
@@ -222,13 +222,14 @@ def byte_model(cf, R, k, n_lat, dir_carried=False):
         "fft_c2c": 2 * 16 * k * Hh,
         "fft_unpack": 16 * k * Hh + 8 * k * N,
         # epilogue: out = A*v (k), out2 = xi0*v (k), reads A, xi0
-        "fft_unpack+epi": 16 * k * Hh + 16 * N + 16 * k * N,
+        "fft_unpack+epi": 16 * k * Hh + 16 * N + 8 * k * N + 8 * k * (Hh if pairs else N),
         # 5 B per nonzero, 12 B segment descriptors, x (k) and the column scale, partials (k)
         "los_fwd_items": 5 * nnz + 12 * nseg + 8 * (k + 1) * N + 8 * k * nseg,
         "los_fwd_reduce": 8 * k * nseg + 8 * k * nlos,
         "los_adj_boxes": 5 * nnz + 4 * nseg + 2 * 257 * nbox + 8 * (k + 1) * N,
-        # mirror fold: w (k) in, folded cell (k) out
-        "bin_fold": 8 * k * N + 8 * k * Nf,
+        # mirror fold: w (k) in -- the half grid of point-mirror pair sums
+        # with epi_out2_pairs -- folded cell (k) out
+        "bin_fold": 8 * k * (Hh if pairs else N) + 8 * k * Nf,
         # perm over the cell, cell values (k), bin offsets, sums (k)
         "bin_scatter": 4 * Nf + 8 * k * Nf + 4 * B + 8 * k * B,
         "cg_dir_kernel": 3 * 8 * k * n_lat,
@@ -245,7 +246,7 @@ def byte_model(cf, R, k, n_lat, dir_carried=False):
         "cg_update_seg": 3 * 8 * k * (n_lat - N),
         # unpack + the grid segment's CG update: half spectrum (k), A, xi0;
         # x, r, d in (k), x, r and w = xi0*v out (k) -- q is not stored
-        "fft_unpack+cg": 16 * k * Hh + 16 * N + 48 * k * N,
+        "fft_unpack+cg": 16 * k * Hh + 16 * N + 40 * k * N + 8 * k * (Hh if pairs else N),
     }
 
 
@@ -287,7 +288,7 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
     from nifty_amd.minimization import fused_cg
     dcar = bool(fused_cg._CARRY and fused_cg._CARRY_DIR and getattr(core, "dir_blocks", lambda k: 0)(k) > 0
                 and _CARRY_CACHE)
-    model = byte_model(cf, R, k, n_lat, dir_carried=dcar)
+    model = byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(getattr(core, "_pairs", lambda k: 0)(k)))
     out = {}
     tot_us, tot_b = 0.0, 0
     for lab, (cnt, tot) in acc.items():

@@ -156,6 +156,13 @@ int nft_bin_scatter_ordered(const void* in, const int* perm, const int* offsets,
  * in: (pre, shape[0..ndim-1]); out: (pre, shape[a]/2 + 1 ...); 1 <= ndim <= 3.
  * Fixed summation order (deterministic), not np.bincount's order: the bin sums
  * agree with the reference to rounding (rtol ~1e-15), not bitwise. */
+/* The mirror fold of nft_bin_fold from point-mirror pair sums on the half
+ * grid (nft_hartley_fuse.epi_out2_pairs; shape = the FULL grid): per
+ * fundamental cell the sum of the half-grid entries at the sign flips of all
+ * but the last axis (2^(d-1) reads instead of 2^d).  Equal to nft_bin_fold to
+ * rounding (the images are added in pairs). */
+int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
+                      hipStream_t stream);
 int nft_bin_fold(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
                  hipStream_t stream);
 
@@ -250,6 +257,13 @@ typedef struct nft_hartley_fuse {
   int64_t dir_pstride;
   double dir_shift;
   int32_t dir_blk0, dir_pad;
+  /* 1: epi_out2 receives point-mirror PAIR SUMS on the half grid (the
+   * transform's last axis n -> n/2 + 1): out2[item][row][c] = epi_b * h at
+   * (row, c) + epi_b * h at its point mirror (-row, -c), c <= n/2; a column
+   * that is its own mirror (c = 0, n/2) holds the single value.  Half the
+   * second output's bytes; nft_bin_fold_half completes the mirror fold from
+   * it (engine-v2 strided unpack pass only). */
+  int64_t epi_out2_pairs;
 } nft_hartley_fuse;
 
 /* Partial blocks per item of the CG-carrying epilogue for a batched

@@ -40,6 +40,7 @@ SIGNATURES = {
     "nft_bin_scatter": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_bin_chunk": (_i, []),
     "nft_bin_fold": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
+    "nft_bin_fold_half": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_scatter_ordered": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
     "nft_csr_rowblocks": (_i, [_p, _i64, _p, _i64, ctypes.POINTER(_i64)]),
@@ -84,7 +85,8 @@ class HartleyFuse(ctypes.Structure):
                [(n, _p) for n in ("cg_x", "cg_r", "cg_d", "cg_sc", "cg_part")] + \
                [("cg_stride", _i64), ("cg_shift", _d), ("cg_nbtot", ctypes.c_int32), ("cg_blk0", ctypes.c_int32)] + \
                [(n, _p) for n in ("dir_r", "dir_sc", "dir_part")] + \
-               [("dir_pstride", _i64), ("dir_shift", _d), ("dir_blk0", ctypes.c_int32), ("dir_pad", ctypes.c_int32)]
+               [("dir_pstride", _i64), ("dir_shift", _d), ("dir_blk0", ctypes.c_int32), ("dir_pad", ctypes.c_int32)] + \
+               [("epi_out2_pairs", _i64)]
 
 
 class LosPlan(ctypes.Structure):
@@ -290,6 +292,16 @@ def bin_fold(src, out, pre, shape):
     return out
 
 
+def bin_fold_half(src, out, pre, shape):
+    """Mirror fold onto (pre, *[n//2+1]) from point-mirror pair sums on the
+    half grid (pre, *shape[:-1], shape[-1]//2+1) (nft_bin_fold_half)."""
+    lib = load()
+    require_device(src, out)
+    sh = (ctypes.c_int64 * len(shape))(*shape)
+    _check(lib.nft_bin_fold_half(ptr(src), ptr(out), pre, len(shape), sh, dtype_code(src.dtype), stream_ptr()))
+    return out
+
+
 def spmv_csr(indptr, indices, weights, x, y, scale=1.0):
     lib = load()
     require_device(indptr, indices, weights, x, y)
@@ -371,6 +383,7 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
             tens.append(v)
             setattr(f, fld, v.data_ptr() if v is not None else None)
         f.epi_shift = float(epi.get("shift", 0.0))
+        f.epi_out2_pairs = 1 if epi.get("pairs") else 0
     if cg:
         # the CG update carried by the epilogue (nft_hartley_fuse.cg_*):
         # x / r / d are strided base pointers of the grid segment

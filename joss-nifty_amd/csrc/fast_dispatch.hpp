@@ -71,6 +71,10 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   FastArgs<T> b = a;
   b.ntiles = ntiles;
   b.bgroup = 0;
+  if (a.f.o2h && (KIND != K_UNPACK || ROWS) && a.f.epi) {
+    set_last_error("out2 pair sums: only the strided unpack pass stores them");
+    return NFT_ERR_UNSUPPORTED;
+  }
   if (a.f.cg) {
     // the CG update rides only in the strided unpack pass, one item per tile
     if (KIND != K_UNPACK || ROWS || a.los != 0 || a.f.nb < 1 || a.g.O != a.f.nb || ntiles % a.g.O != 0) {

@@ -50,6 +50,10 @@ struct FuseArgs {
   double cshift;
   int cnbtot, cblk0;
   long long ctr;   // tiles per item of the carrying pass (set by the launcher)
+  // out2 as point-mirror pair sums on the half grid (nft_hartley_fuse.epi_out2_pairs):
+  // out2[b * s2 + row * nh + col] = eb*h at (row, col) + eb*h at the point mirror
+  int o2h;
+  long long nlast, nh;
   // CG direction carried by the folded prologue (nft_hartley_fuse.dir_*)
   const void* dr;
   const double* dsc;
@@ -109,7 +113,24 @@ __device__ __forceinline__ void fuse_store(const FuseArgs& f, T* out, long long 
   T r = f.ea ? ((const T*)f.ea)[b * f.sea + j] * h : h;
   if (f.ed) r += (T)f.eshift * ((const T*)f.ed)[b * f.sd + j];
   out[b * f.so + j] = r;
-  if (f.out2) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
+  if (f.out2 && !f.o2h) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
+}
+
+// point-mirror pair sum of the second epilogue output on the half grid: the
+// element at flat index ib (column <= n_last / 2) and, when the line has one,
+// its point mirror im (the same thread stores both in the unpack pass)
+template <typename T>
+__device__ __forceinline__ void fuse_store_pair(const FuseArgs& f, long long ib, T hb, bool mir, long long im, T hm) {
+  long long b, j;
+  fuse_split(f, ib, b, j);
+  T w = ((const T*)f.eb)[b * f.seb + j] * hb;
+  if (mir) {
+    long long b2, j2;
+    fuse_split(f, im, b2, j2);
+    w += ((const T*)f.eb)[b2 * f.seb + j2] * hm;
+  }
+  const long long row = j / f.nlast, col = j - row * f.nlast;
+  ((T*)f.out2)[b * f.s2 + row * f.nh + col] = w;
 }
 
 // epilogue store that carries the CG update instead of storing q = ea * h:
@@ -121,7 +142,7 @@ __device__ __forceinline__ void fuse_store_cg(const FuseArgs& f, long long i, T 
   long long b, j;
   fuse_split(f, i, b, j);
   const T q = f.ea ? ((const T*)f.ea)[b * f.sea + j] * h : h;
-  if (f.out2) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
+  if (f.out2 && !f.o2h) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
   const long long e = b * f.cst + j;
   T xi = ((T*)f.cx)[e], ri = ((T*)f.cr)[e];
   if (ok) {
@@ -420,11 +441,18 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           if (!u.valid) continue;
           const C f = lds[l * PITCH + padx<PS>(x)];
           const int k = (int)m * a.km + x * a.kx;
-          fuse_store<T>(a.f, out, u.base + (long long)k * a.rs, sc * (f.x + sg * f.y));
+          const long long ib = u.base + (long long)k * a.rs;
+          const T hb = sc * (f.x + sg * f.y);
+          fuse_store<T>(a.f, out, ib, hb);
+          long long im = 0;
+          T hm = (T)0;
           if (u.mirror) {
             const int km = (k == 0) ? 0 : Nf - k;
-            fuse_store<T>(a.f, out, u.mbase + (long long)km * a.rs, sc * (f.x - sg * f.y));
+            im = u.mbase + (long long)km * a.rs;
+            hm = sc * (f.x - sg * f.y);
+            fuse_store<T>(a.f, out, im, hm);
           }
+          if (a.f.o2h) fuse_store_pair<T>(a.f, ib, hb, u.mirror != 0, im, hm);
         }
       } else {
         // one item per tile (los = 0): its step length from its CG scalars
@@ -444,11 +472,18 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           if (!u.valid) continue;
           const C f = lds[l * PITCH + padx<PS>(x)];
           const int k = (int)m * a.km + x * a.kx;
-          fuse_store_cg<T>(a.f, u.base + (long long)k * a.rs, sc * (f.x + sg * f.y), al, ok, shift, rr, xr);
+          const long long ib = u.base + (long long)k * a.rs;
+          const T hb = sc * (f.x + sg * f.y);
+          fuse_store_cg<T>(a.f, ib, hb, al, ok, shift, rr, xr);
+          long long im = 0;
+          T hm = (T)0;
           if (u.mirror) {
             const int km = (k == 0) ? 0 : Nf - k;
-            fuse_store_cg<T>(a.f, u.mbase + (long long)km * a.rs, sc * (f.x - sg * f.y), al, ok, shift, rr, xr);
+            im = u.mbase + (long long)km * a.rs;
+            hm = sc * (f.x - sg * f.y);
+            fuse_store_cg<T>(a.f, im, hm, al, ok, shift, rr, xr);
           }
+          if (a.f.o2h) fuse_store_pair<T>(a.f, ib, hb, u.mirror != 0, im, hm);
         }
         // fixed-order block sums (wave shuffles, then the waves in order)
         __shared__ double cgsh[2 * (NT / 64)];

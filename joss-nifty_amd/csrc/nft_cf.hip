@@ -186,6 +186,56 @@ struct FoldShape {
   long long nin, nout;  // elements per pre item
 };
 
+// fold from point-mirror pair sums on the half grid (last axis h = n/2+1):
+// the sign flips of the first d-1 axes only, in the order of bin_fold_kernel
+template <typename T>
+__global__ __launch_bounds__(256) void bin_fold_half_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                            FoldShape fs, long long pre, long long nhalf) {
+  const long long tot = pre * fs.nout;
+  const int D = fs.d;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    long long r = e % fs.nout;
+    const long long p = e / fs.nout;
+    long long q[FOLD_MAXD], m[FOLD_MAXD];
+    bool two[FOLD_MAXD];
+#pragma unroll
+    for (int a = FOLD_MAXD - 1; a >= 0; --a) {
+      if (a < D) {
+        q[a] = r % fs.h[a];
+        r /= fs.h[a];
+        m[a] = fs.n[a] - q[a];
+        two[a] = q[a] != 0 && m[a] != q[a];
+      } else {
+        q[a] = m[a] = 0;
+        two[a] = false;
+      }
+    }
+    const T* src = in + p * nhalf;
+    T acc = (T)0;
+#pragma unroll
+    for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s) {
+      bool ok = true;
+      long long idx = 0;
+#pragma unroll
+      for (int a = 0; a < FOLD_MAXD; ++a) {
+        if (a >= D) continue;
+        if (a == D - 1) {           // the half axis: no flip
+          idx = idx * fs.h[a] + q[a];
+          continue;
+        }
+        const bool hi = (s >> (FOLD_MAXD - 2 - a)) & 1;
+        ok = ok && (!hi || two[a]);
+        idx = idx * fs.n[a] + (hi ? m[a] : q[a]);
+      }
+      // patterns that flip axes beyond d-1 do not exist
+      for (int a = D - 1; a < FOLD_MAXD - 1; ++a) ok = ok && !((s >> (FOLD_MAXD - 2 - a)) & 1);
+      if (ok) acc += src[idx];
+    }
+    out[e] = acc;
+  }
+}
+
 // I: index type -- 32-bit when pre * nin < 2^31 (the usual case: cheaper
 // div/mod per element), 64-bit otherwise
 template <typename T, typename I>
@@ -325,6 +375,46 @@ int nft_bin_scatter_ordered(const void* in, const int* perm, const int* offsets,
                        (long long)nbins, (long long)post);
   else {
     set_last_error("nft_bin_scatter: bad dtype");
+    return NFT_ERR_ARG;
+  }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
+                      hipStream_t stream) {
+  if (ndim < 1 || ndim > FOLD_MAXD || pre < 0) {
+    set_last_error("nft_bin_fold_half: need 1 <= ndim <= 3 and pre >= 0");
+    return NFT_ERR_ARG;
+  }
+  FoldShape fs;
+  fs.d = ndim;
+  fs.nin = 1;
+  fs.nout = 1;
+  for (int a = 0; a < FOLD_MAXD; ++a) fs.n[a] = fs.h[a] = 1;
+  long long nhalf = 1;
+  for (int a = 0; a < ndim; ++a) {
+    if (shape[a] < 1) {
+      set_last_error("nft_bin_fold_half: bad shape");
+      return NFT_ERR_ARG;
+    }
+    fs.n[a] = shape[a];
+    fs.h[a] = shape[a] / 2 + 1;
+    fs.nin *= shape[a];
+    fs.nout *= fs.h[a];
+    nhalf *= (a == ndim - 1) ? fs.h[a] : shape[a];
+  }
+  const long long tot = pre * fs.nout;
+  if (tot <= 0) return NFT_OK;
+  prof_mark(stream, "bin_fold");
+  if (dtype == 0)
+    hipLaunchKernelGGL(bin_fold_half_kernel<double>, dim3(nblocks(tot)), dim3(256), 0, stream, (const double*)in,
+                       (double*)out, fs, (long long)pre, nhalf);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(bin_fold_half_kernel<float>, dim3(nblocks(tot)), dim3(256), 0, stream, (const float*)in,
+                       (float*)out, fs, (long long)pre, nhalf);
+  else {
+    set_last_error("nft_bin_fold_half: bad dtype");
     return NFT_ERR_ARG;
   }
   NFT_HIP_CHECK(hipGetLastError());

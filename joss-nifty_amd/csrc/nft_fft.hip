@@ -930,8 +930,8 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     int st = hartley_v2<T>(in, out, g, ax, sigma, scale, ws, ws_bytes, s, &f);
     if (st != NFT_FALLBACK) return st;
   }
-  if (f.cg) {
-    set_last_error("nft_hartley_fused: the CG-carrying epilogue needs the engine-v2 unpack pass "
+  if (f.cg || f.o2h) {
+    set_last_error("nft_hartley_fused: the CG-carrying epilogue / out2 pair sums need the engine-v2 unpack pass "
                    "(nft_hartley_cg_blocks == 0 for this geometry)");
     return NFT_ERR_UNSUPPORTED;
   }
@@ -1123,6 +1123,16 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     if ((f.pb && (!f.pc || !f.pidx)) || (f.out2 && !f.eb)) {
       set_last_error("nft_hartley_fused: incomplete fusion spec");
       return NFT_ERR_ARG;
+    }
+    f.o2h = 0;
+    if (fz->epi_out2_pairs) {
+      if (!f.out2 || !f.eb || ax.empty() || ax.back() != ndim - 1) {
+        set_last_error("nft_hartley_fused: epi_out2_pairs needs out2, epi_b and the last axis transformed");
+        return NFT_ERR_ARG;
+      }
+      f.o2h = 1;
+      f.nlast = shape[ndim - 1];
+      f.nh = shape[ndim - 1] / 2 + 1;
     }
     f.dr = nullptr;
     if (fz->dir_r) {

@@ -51,6 +51,10 @@ def _t(a):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=config.device())
 
 
+# xi0 * v of the Jacobian adjoint stored as point-mirror pair sums on the half
+# grid (NFT_O2_PAIRS=0: the full grid)
+_O2_PAIRS = os.environ.get("NFT_O2_PAIRS", "1") != "0"
+
 # amplitude forward + linearisation constants in native passes
 # (NFT_AMP_NATIVE_FWD=0: the torch formulation, for A/B comparisons)
 _AMP_NATIVE_FWD = os.environ.get("NFT_AMP_NATIVE_FWD", "1") != "0"
@@ -501,15 +505,29 @@ class CFJacobian(LinearOperator):
         A_full * v (+ shift * d_xi) and xi0 * v, v = c_h HT g."""
         m = self._m
         b = m.bins
-        w = torch.empty(self._afull.shape, dtype=self._afull.dtype, device=self.device)
-        oxi = out[m.k_xi] if out is not None else torch.empty_like(w)
-        epi = dict(a=self._afull, b=self._xi0, out2=w)
+        grid = tuple(self._afull.shape)
+        pairs = self._pairs(1)
+        # with pair sums: the batched adjoint's layout (a batch of one), so
+        # single and batched solves stay bitwise equal
+        w = torch.empty(self._half(grid) if pairs else grid, dtype=self._afull.dtype, device=self.device)
+        oxi = out[m.k_xi] if out is not None else torch.empty(grid, dtype=self._afull.dtype, device=self.device)
+        epi = dict(a=self._afull, b=self._xi0, out2=w, pairs=pairs)
         if out is not None and shift != 0.0:
             epi.update(d=d[m.k_xi], shift=shift)
-        _native.hartley_fused(oxi, range(w.ndim), m.c_h, x=g.contiguous(), epi=epi,
-                              convention=hartley_convention_code())
+        if pairs:
+            N = self._afull.numel()
+            _native.hartley_fused(oxi, tuple(range(1, 1 + len(grid))), m.c_h, x=g.contiguous(), epi=epi,
+                                  convention=hartley_convention_code(), shape=(1,) + grid,
+                                  batch=dict(period=N, out=N, out2=w.numel(), d=N))
+        else:
+            _native.hartley_fused(oxi, range(len(grid)), m.c_h, x=g.contiguous(), epi=epi,
+                                  convention=hartley_convention_code())
         ga = torch.empty(m.amp.B, dtype=w.dtype, device=w.device)
-        m.jbins.scatter(w, ga, 1)
+        if pairs:
+            wf = torch.empty((1, m.jbins.fold["nf"]), dtype=w.dtype, device=w.device)
+            m.jbins.scatter_from(m.jbins.fold_into(w, wf, 1, half=True), ga, 1)
+        else:
+            m.jbins.scatter(w, ga, 1)
         if out is None:
             if _AMP_TORCH:
                 res = m.amp.vjp(self._c, ga)
@@ -571,13 +589,25 @@ class CFJacobian(LinearOperator):
             dt = self._afull.dtype
             B = self._m.amp.B
             fold = self._m.jbins.fold
+            wshape = self._half(grid) if self._pairs(k) else grid
             bufs = self._mvb = dict(k=k, da=torch.empty((B, k), dtype=torch.float64, device=self.device),
                                     s=torch.empty((k,) + grid, dtype=dt, device=self.device),
-                                    w=torch.empty((k,) + grid, dtype=dt, device=self.device),
+                                    w=torch.empty((k,) + wshape, dtype=dt, device=self.device),
                                     wf=torch.empty((k, fold["nf"]) if fold else (1,), dtype=dt,
                                                    device=self.device),
                                     ga=torch.empty((k, B), dtype=dt, device=self.device))
         return bufs
+
+    @staticmethod
+    def _half(grid):
+        return tuple(grid[:-1]) + (grid[-1] // 2 + 1,)
+
+    def _pairs(self, k):
+        """the adjoint stores xi0 * v as point-mirror pair sums on the half
+        grid (nft_hartley_fuse.epi_out2_pairs): half the bytes of the second
+        epilogue output and of the mirror fold's input"""
+        return (_O2_PAIRS and self._m.jbins.fold is not None and len(self._afull.shape) >= 2
+                and self.cg_blocks(k) > 0)
 
     def mv_amp_jvp(self, D):
         """dA (B, k) of the k rows of D, bin-major interleaved: the
@@ -635,8 +665,9 @@ class CFJacobian(LinearOperator):
         if after_w is not None:
             after_w()
         w = bufs["w"]
-        epi = dict(a=self._afull, b=self._xi0, out2=w)
-        bt = dict(period=N, out=size, out2=N)
+        pairs = self._pairs(k)
+        epi = dict(a=self._afull, b=self._xi0, out2=w, pairs=pairs)
+        bt = dict(period=N, out=size, out2=w[0].numel())
         if shift != 0.0:
             epi.update(d=D[0, xo:], shift=shift)
             bt["d"] = size
@@ -647,7 +678,7 @@ class CFJacobian(LinearOperator):
     def mv_fold(self, w):
         """the mirror fold of w (the bandwidth-bound half of the bin sums)"""
         k = w.shape[0]
-        return self._m.jbins.fold_into(w, self._mv_bufs(k)["wf"], k)
+        return self._m.jbins.fold_into(w, self._mv_bufs(k)["wf"], k, half=self._pairs(k))
 
     def mv_amp_vjp(self, D, w, Q, shift=0.0, folded=None):
         """bin sums of w (folded: mv_fold's result, if already formed) and the

@@ -100,13 +100,17 @@ class BinIndex:
         return _native.bin_scatter(wf, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
                                    order=f["order"])
 
-    def fold_into(self, w, wf, pre):
+    def fold_into(self, w, wf, pre, half=False):
         """first half of scatter: the mirror fold of w into wf (pre, nf);
-        returns the operand of scatter_from (wf, or w without a fold)"""
+        returns the operand of scatter_from (wf, or w without a fold).
+        half: w holds point-mirror pair sums on the half grid
+        (nft_hartley_fuse.epi_out2_pairs)"""
         f = self.fold
         if f is None:
+            if half:
+                raise ValueError("pair sums need the folded bin index")
             return w
-        _native.bin_fold(w, wf, pre, f["shape"])
+        (_native.bin_fold_half if half else _native.bin_fold)(w, wf, pre, f["shape"])
         return wf
 
     def scatter_from(self, src, out, pre):

@@ -49,7 +49,7 @@ def main(reps=3, k=4):
     torch.cuda.synchronize()
     from nifty_amd.minimization import fused_cg
     dcar = bool(fused_cg._CARRY and fused_cg._CARRY_DIR and core.dir_blocks(k) > 0 and bench._CARRY_CACHE)
-    model = bench.byte_model(cf, R, k, n_lat, dir_carried=dcar)
+    model = bench.byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(core._pairs(k)))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "pmc_labels.json"), "w") as f:
         json.dump({"labels": [lab for lab, _ in p.records], "calibration_bytes": 8 * cal_n,
