@@ -91,7 +91,7 @@ def _pairdots(pairs):
 
 
 # ------------------------------------------------------------------ stages
-from ..library.correlated_fields_simple import _PRO_FOLD  # noqa: E402
+from ..library.correlated_fields_simple import _O2_PAIRS, _PRO_FOLD  # noqa: E402
 
 
 def _items(st, k):
@@ -191,9 +191,14 @@ class _CFStage:
         N = self.N
         shared = st["k"] == 1
         Xs = st["X"]
-        w = torch.empty((k,) + self.grid, dtype=G.dtype, device=G.device)
-        epi = dict(a=st["afull"], b=Xs[0, self.xo:], out2=w)
-        batch = dict(period=N, out=size, out2=N)
+        # xi0 * v as point-mirror pair sums on the half grid where the CF
+        # Jacobian's own adjoint uses them (CFJacobian._pairs)
+        jac_pairs = _O2_PAIRS and m.jbins.fold is not None and len(self.grid) >= 2 and \
+            _native.hartley_cg_blocks((k,) + self.grid, self.axes, G.dtype) > 0
+        wshape = self.grid[:-1] + (self.grid[-1] // 2 + 1,) if jac_pairs else self.grid
+        w = torch.empty((k,) + wshape, dtype=G.dtype, device=G.device)
+        epi = dict(a=st["afull"], b=Xs[0, self.xo:], out2=w, pairs=jac_pairs)
+        batch = dict(period=N, out=size, out2=w[0].numel())
         if not shared:
             batch.update(ea=N, eb=Xs.shape[1])
         if d is not None and shift != 0.0:
@@ -202,7 +207,11 @@ class _CFStage:
         _native.hartley_fused(Q[0, self.xo:], self.axes, m.c_h, x=G.contiguous(), epi=epi,
                               convention=hartley_convention_code(), shape=(k,) + self.grid, batch=batch)
         ga = torch.empty((k, m.amp.B), dtype=G.dtype, device=G.device)
-        m.jbins.scatter(w, ga, k)
+        if jac_pairs:
+            wf = torch.empty((k, m.jbins.fold["nf"]), dtype=G.dtype, device=G.device)
+            m.jbins.scatter_from(m.jbins.fold_into(w, wf, k, half=True), ga, k)
+        else:
+            m.jbins.scatter(w, ga, k)
         m.amp.native_vjp_batched(st["lin"], ga, Q, self.off, D=d, shift=shift if d is not None else 0.0,
                                  item_consts=_items(st, k))
         return Q
