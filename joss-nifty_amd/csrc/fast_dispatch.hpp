@@ -89,7 +89,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     const bool shared = (f.pro && ((f.pa && !f.sa) || (f.pb && !f.sb))) || (f.epi && ((f.ea && !f.sea) || (f.eb && !f.seb)));
     // measured slower at 2048^2 with 4 items (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us): opt-in
     static const bool on = getenv("NFT_BATCH_REMAP") != nullptr;
-    if (on && shared && !f.cg && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) b.bgroup = f.nb;
+    if (on && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) b.bgroup = f.nb;
   }
   // persistent grid (plain R2C rows): per_cu workgroups per CU
   static int ncu = 0;
