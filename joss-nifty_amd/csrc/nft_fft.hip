@@ -744,7 +744,10 @@ __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __r
 // of c (2^d pixels, fewer on self-mirror axes) -- each image's x, A, xi0 and
 // u accesses are contiguous across the wave (forward or reversed).  Same
 // arithmetic per element as pro_batch_kernel (bitwise).
-template <typename T>
+// D (the number of transform axes) is a template parameter so that the cell
+// coordinates and the per-item values stay in registers (a runtime D put
+// them in scratch).
+template <typename T, int D>
 __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __restrict__ u, long long P, int nb,
                                                        long long ncell) {
   const T* __restrict__ px = (const T*)f.px;
@@ -753,7 +756,6 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
   const T* __restrict__ pc = (const T*)f.pc;
   using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   const bool vec = f.ce == nb && f.sc == 1 && (nb & 1) == 0 && nb <= 8;
-  const int D = f.fnd;
   // the CG direction update carried here (f.dr): d = max(0, gamma/gprev) d + r
   // per item, written back to px, d.d accumulated per item (nb <= 8)
   const bool dirc = f.dr != nullptr;
@@ -775,10 +777,13 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
       bt[b] = (T)beta;
     }
   }
+  unsigned nn[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) nn[a] = (unsigned)f.fn[a];
   for (long long c = (long long)blockIdx.x * 256 + threadIdx.x; c < ncell; c += (long long)gridDim.x * 256) {
-    unsigned cc[3], nn[3], rest = (unsigned)c;
+    unsigned cc[D], rest = (unsigned)c;
+#pragma unroll
     for (int a = D - 1; a >= 0; --a) {
-      nn[a] = (unsigned)f.fn[a];
       const unsigned h = nn[a] / 2 + 1;
       const unsigned q = rest / h;
       cc[a] = rest - q * h;
@@ -786,6 +791,8 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
     }
     const long long ix = (long long)f.pidx[c] * f.ce;
     T cv[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) cv[b] = (T)0;
     if (vec) {
       const V2* q = (const V2*)(pc + ix);
 #pragma unroll
@@ -795,15 +802,21 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
           cv[2 * bp] = c2.x;
           cv[2 * bp + 1] = c2.y;
         }
+    } else if (nb <= 8) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        if (b < nb) cv[b] = pc[b * f.sc + ix];
     }
     // images: bit a of m flips axis a (skipped when that axis is self-mirror)
+#pragma unroll
     for (int m = 0; m < (1 << D); ++m) {
       unsigned j = 0;
       bool dup = false;
+#pragma unroll
       for (int a = 0; a < D; ++a) {
         unsigned k = cc[a];
         if ((m >> a) & 1) {
-          const unsigned km = (nn[a] - k) % nn[a];
+          const unsigned km = k == 0 ? 0 : nn[a] - k;
           if (km == k) dup = true;
           k = km;
         }
@@ -812,34 +825,27 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
       if (dup) continue;
       const T a = pa ? pa[j] : (T)1;
       const T bj = pb[j];
-      if (dirc) {
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          if (b >= nb) break;
-          T v = px[b * f.sx + j];
-          if (live[b]) {
-            v = bt[b] * v + pr[b * f.sx + j];
-            pd[b * f.sx + j] = v;
-            dd[b] += (double)v * (double)v;
-          }
-          if (pa) v *= a;
-          v += bj * (vec ? cv[b] : pc[b * f.sc + ix]);
-          u[b * P + j] = v;
-        }
-      } else if (vec) {
-        for (int b = 0; b < nb; ++b) {
-          T v = px[b * f.sx + j];
-          if (pa) v *= a;
-          v += bj * cv[b];
-          u[b * P + j] = v;
-        }
-      } else {
+      if (nb > 8) {  // large batches (no carried direction): items in a loop
         for (int b = 0; b < nb; ++b) {
           T v = px[b * f.sx + j];
           if (pa) v *= a;
           v += bj * pc[b * f.sc + ix];
           u[b * P + j] = v;
         }
+        continue;
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b >= nb) break;
+        T v = px[b * f.sx + j];
+        if (dirc && live[b]) {
+          v = bt[b] * v + pr[b * f.sx + j];
+          pd[b * f.sx + j] = v;
+          dd[b] += (double)v * (double)v;
+        }
+        if (pa) v *= a;
+        v += bj * cv[b];
+        u[b * P + j] = v;
       }
     }
   }
@@ -911,8 +917,13 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
       long long ncell = 1;
       for (int a = 0; a < f.fnd; ++a) ncell *= f.fn[a] / 2 + 1;
       prof_mark(s, f.dr ? "pro_fold+dir" : "pro_fold");
-      hipLaunchKernelGGL(pro_fold_kernel<T>, dim3((unsigned)((ncell + 255) / 256)), dim3(256), 0, s, f, u, f.P, f.nb,
-                         ncell);
+      const dim3 grid((unsigned)((ncell + 255) / 256));
+      if (f.fnd == 1)
+        hipLaunchKernelGGL((pro_fold_kernel<T, 1>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+      else if (f.fnd == 2)
+        hipLaunchKernelGGL((pro_fold_kernel<T, 2>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+      else
+        hipLaunchKernelGGL((pro_fold_kernel<T, 3>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
     } else {
       prof_mark(s, "pro_batch");
       hipLaunchKernelGGL(pro_batch_kernel<T>, dim3(nblk), dim3(256), 0, s, f, u, f.P, f.nb);
