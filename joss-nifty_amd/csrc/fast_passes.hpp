@@ -464,26 +464,79 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
                         scb[NFT_CG_DONE] == 0.0;
         const T al = (T)alpha, shift = (T)a.f.cshift;
         double rr = 0.0, xr = 0.0;
+        // two phases per group of CG_CH values: every operand load of the
+        // group first, then the arithmetic and the stores -- the loads of
+        // x and r cannot pass the previous stores to x and r otherwise
+        // (same arrays, runtime offsets), which serialised one memory
+        // round trip per element
+        constexpr int CG_CH = 2;
+        const T* __restrict__ ea = (const T*)a.f.ea;
+        const T* __restrict__ eb = (const T*)a.f.eb;
+        const T* __restrict__ cd = (const T*)a.f.cd;
+        T* __restrict__ cx = (T*)a.f.cx;
+        T* __restrict__ cr = (T*)a.f.cr;
 #pragma unroll
-        for (int r = 0; r < VPT; ++r) {
-          int l, x;
-          lx_of(r, l, x);
-          const UnpackLine u = lines[l];
-          if (!u.valid) continue;
-          const C f = lds[l * PITCH + padx<PS>(x)];
-          const int k = (int)m * a.km + x * a.kx;
-          const long long ib = u.base + (long long)k * a.rs;
-          const T hb = sc * (f.x + sg * f.y);
-          fuse_store_cg<T>(a.f, ib, hb, al, ok, shift, rr, xr);
-          long long im = 0;
-          T hm = (T)0;
-          if (u.mirror) {
+        for (int r0 = 0; r0 < VPT; r0 += CG_CH) {
+          long long ev[CG_CH][2], jv[CG_CH][2], bv[CG_CH][2];
+          bool use[CG_CH][2];
+          T hv[CG_CH][2], xv[CG_CH][2], rv_[CG_CH][2], dv[CG_CH][2], qv[CG_CH][2], wv[CG_CH][2];
+#pragma unroll
+          for (int c = 0; c < CG_CH; ++c) {
+            int l, x;
+            lx_of(r0 + c, l, x);
+            const UnpackLine u = lines[l];
+            const C fv = lds[l * PITCH + padx<PS>(x)];
+            const int k = (int)m * a.km + x * a.kx;
             const int km = (k == 0) ? 0 : Nf - k;
-            im = u.mbase + (long long)km * a.rs;
-            hm = sc * (f.x - sg * f.y);
-            fuse_store_cg<T>(a.f, im, hm, al, ok, shift, rr, xr);
+            use[c][0] = u.valid != 0;
+            use[c][1] = u.valid != 0 && u.mirror != 0;
+            hv[c][0] = sc * (fv.x + sg * fv.y);
+            hv[c][1] = sc * (fv.x - sg * fv.y);
+            const long long idx[2] = {u.base + (long long)k * a.rs, u.mbase + (long long)km * a.rs};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              long long b, j;
+              fuse_split(a.f, idx[h], b, j);
+              bv[c][h] = b;
+              jv[c][h] = j;
+              ev[c][h] = b * a.f.cst + j;
+              xv[c][h] = rv_[c][h] = dv[c][h] = qv[c][h] = wv[c][h] = (T)0;
+              if (use[c][h]) {
+                xv[c][h] = cx[ev[c][h]];
+                rv_[c][h] = cr[ev[c][h]];
+                if (ok) dv[c][h] = cd[ev[c][h]];
+                qv[c][h] = ea ? ea[b * a.f.sea + j] : (T)1;
+                if (a.f.out2) wv[c][h] = eb[b * a.f.seb + j];
+              }
+            }
           }
-          if (a.f.o2h) fuse_store_pair<T>(a.f, ib, hb, u.mirror != 0, im, hm);
+#pragma unroll
+          for (int c = 0; c < CG_CH; ++c) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              if (!use[c][h]) continue;
+              // the per-element arithmetic of fuse_store_cg
+              const T q = ea ? qv[c][h] * hv[c][h] : hv[c][h];
+              T xi = xv[c][h], ri = rv_[c][h];
+              if (ok) {
+                const T di = dv[c][h];
+                xi = xi - al * di;
+                ri = ri - al * (q + shift * di);
+                cx[ev[c][h]] = xi;
+                cr[ev[c][h]] = ri;
+              }
+              rr += (double)ri * (double)ri;
+              xr += (double)xi * (double)ri;
+              if (a.f.out2 && !a.f.o2h) ((T*)a.f.out2)[bv[c][h] * a.f.s2 + jv[c][h]] = wv[c][h] * hv[c][h];
+            }
+            if (a.f.o2h && use[c][0]) {
+              T w = wv[c][0] * hv[c][0];
+              if (use[c][1]) w += wv[c][1] * hv[c][1];
+              const long long j = jv[c][0];
+              const long long row = j / a.f.nlast, col = j - row * a.f.nlast;
+              ((T*)a.f.out2)[bv[c][0] * a.f.s2 + row * a.f.nh + col] = w;
+            }
+          }
         }
         // fixed-order block sums (wave shuffles, then the waves in order)
         __shared__ double cgsh[2 * (NT / 64)];
