@@ -249,7 +249,7 @@ typedef struct nft_hartley_fuse {
    * b * NFT_CG_NSCALARS of dir_sc; unchanged, partial 0, when its DONE is set)
    * before the prologue reads it, and dir_part[b * dir_pstride + dir_blk0 +
    * block] = dir_shift * (the block's sum of d^2), block <
-   * ceil(prod(n_a / 2 + 1) / 256) -- the d.d partials of
+   * nft_hartley_dir_blocks(item grid) -- the d.d partials of
    * nft_cg_direction_dd_batched for the grid segment. */
   const void* dir_r;
   const double* dir_sc;
@@ -270,6 +270,13 @@ typedef struct nft_hartley_fuse {
  * Hartley transform of this geometry (leading batch axis not among `axes`),
  * or 0 when its last pass cannot carry the update. */
 int nft_hartley_cg_blocks(int ndim, const int64_t* shape, int naxes, const int* axes, int dtype);
+
+/* Blocks of the folded prologue over an item grid of ndim (1..3) axes: the
+ * fundamental cell prod(n_a / 2 + 1) with its last axis padded to a multiple
+ * of 64 (every wave starts a row chunk aligned), 256 cells per block -- the
+ * number of dir_part entries per item of nft_hartley_fuse.dir_*; 0 for a bad
+ * shape. */
+int nft_hartley_dir_blocks(int ndim, const int64_t* shape);
 
 int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes,
                                 int dtype, size_t* bytes);

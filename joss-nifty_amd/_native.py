@@ -68,6 +68,7 @@ SIGNATURES = {
     "nft_amp_jvp_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _p]),
     "nft_amp_vjp_batched": (_i, [_p, _p, _p, _p, _p, _i, _i64, _i64, _p]),
     "nft_hartley_cg_blocks": (_i, [_i, _p, _i, _p, _i]),
+    "nft_hartley_dir_blocks": (_i, [_i, _p]),
     "nft_cg_update_seg_batched": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i, _i, _d, _p, _p, _i, _i, _p]),
     "nft_cg_finalize_batched": (_i, [_p, _i, _i, _p, _p]),
     "nft_amp_forward_buf": (_i64, [_i64]),
@@ -340,6 +341,12 @@ def hartley_cg_blocks(shape, axes, dtype):
     transform of `shape` (leading batch axis) over `axes`, 0 if unsupported"""
     nd, sh, na, ax = _shape_args(tuple(shape), tuple(axes))
     return int(load().nft_hartley_cg_blocks(nd, sh, na, ax, dtype_code(dtype)))
+
+
+def hartley_dir_blocks(grid):
+    """blocks (d.d partials per item) of the folded prologue over `grid`"""
+    sh = (ctypes.c_int64 * len(grid))(*[int(n) for n in grid])
+    return int(load().nft_hartley_dir_blocks(len(grid), sh))
 
 
 def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None, cg=None):

@@ -71,6 +71,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   FastArgs<T> b = a;
   b.ntiles = ntiles;
   b.bgroup = 0;
+  b.bmode = 0;
   if (a.f.o2h && (KIND != K_UNPACK || ROWS) && a.f.epi) {
     set_last_error("out2 pair sums: only the strided unpack pass stores them");
     return NFT_ERR_UNSUPPORTED;
@@ -87,9 +88,17 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     // batch items sharing prologue / epilogue operands: keep one tile's items on one XCD
     const FuseArgs& f = a.f;
     const bool shared = (f.pro && ((f.pa && !f.sa) || (f.pb && !f.sb))) || (f.epi && ((f.ea && !f.sea) || (f.eb && !f.seb)));
-    // measured slower at 2048^2 with 4 items (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us): opt-in
-    static const bool on = getenv("NFT_BATCH_REMAP") != nullptr;
-    if (on && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) b.bgroup = f.nb;
+    // measured slower at 2048^2 with 4 items for the r2c prologue and the
+    // plain epilogue (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us), faster
+    // for the CG-carrying epilogue, which is bound by its HBM traffic (the
+    // contiguous flavour, 231 -> 221 us): default there only; NFT_BATCH_REMAP
+    // = 0 / 1 / 2 sets it for every pass
+    static const int env_mode = getenv("NFT_BATCH_REMAP") ? atoi(getenv("NFT_BATCH_REMAP")) : -1;
+    const int mode = env_mode >= 0 ? env_mode : (f.cg ? 2 : 0);
+    if (mode > 0 && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) {
+      b.bgroup = f.nb;
+      b.bmode = mode;
+    }
   }
   // persistent grid (plain R2C rows): per_cu workgroups per CU
   static int ncu = 0;

@@ -171,6 +171,7 @@ template <typename T> struct FastArgs {
   FuseArgs f;         // R2C/H1D: prologue; UNPACK/H1D: epilogue
   long long ntiles;   // tiles of the pass (set by the launcher)
   int bgroup;         // > 1: batch-aware XCD tile remap over this many items (set by the launcher)
+  int bmode;          // remap flavour: 1 batch_tile, 2 batch_tile_contig
   int los;            // strided: log2 of the items (o) sharing one tile (their lines side by side)
 };
 
@@ -187,6 +188,16 @@ __device__ __forceinline__ long long batch_tile(long long w, long long ntiles, i
   const long long xg = w & 7, slot = w >> 3;
   const long long rl = slot / K, b = slot - rl * K;
   return b * TR + rl * 8 + xg;
+}
+// Contiguous variant: XCD group xg owns the tile range [xg TR/8, (xg+1) TR/8)
+// and walks it in order, the K items of a tile back to back, so adjacent
+// tiles (whose unaligned mirror-line runs share boundary cache lines) are
+// also on one XCD at about the same time.  A bijection when TR % 8 == 0.
+__device__ __forceinline__ long long batch_tile_contig(long long w, long long ntiles, int K) {
+  const long long TR = ntiles / K;
+  const long long xg = w & 7, slot = w >> 3;
+  const long long rl = slot / K, b = slot - rl * K;
+  return b * TR + xg * (TR >> 3) + rl;
 }
 
 // Persistent, prefetching tile loop: measured faster only for the plain
@@ -330,7 +341,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   C rv[VPT];
   long long t = blockIdx.x;
   if constexpr (!PERSIST) {
-    if (a.bgroup > 1) t = batch_tile(t, ntiles, a.bgroup);
+    if (a.bgroup > 1) t = a.bmode == 2 ? batch_tile_contig(t, ntiles, a.bgroup) : batch_tile(t, ntiles, a.bgroup);
   }
   if (prefetch && t < ntiles) load(t, rv);
   while (t < ntiles) {

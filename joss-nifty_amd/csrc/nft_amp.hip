@@ -146,6 +146,31 @@ __device__ __forceinline__ double carry_in(Q tot, int blk, int nb, double* sh) {
   return block_total(s, sh);
 }
 
+// Block -> (scan block bx, right-hand side by) of a batched launch.  nbx > 0:
+// a 1-D grid of roundup(nbx, 8) * nrhs workgroups in which the right-hand
+// sides of one bx are consecutive slots of one XCD group (workgroups are
+// dealt round-robin over the 8 XCDs: w and w + 8 share one), so the per-bin
+// constants the right-hand sides share are read from HBM once and from that
+// XCD's L2 after; padding workgroups (bx >= nbx) return at once.  nbx = 0:
+// the plain (bx, by) = (blockIdx.x, blockIdx.y) grid.  Placement only: the
+// arithmetic of every block is unchanged.
+__device__ __forceinline__ bool amp_block(int nbx, int& bx, int& by, int& gx) {
+  if (nbx <= 0) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    gx = gridDim.x;
+    return true;
+  }
+  const int nbp = (nbx + 7) & ~7;
+  const int ny = (int)(gridDim.x / (unsigned)nbp);
+  const int w = blockIdx.x, xg = w & 7, slot = w >> 3;
+  const int bl = slot / ny;
+  by = slot - bl * ny;
+  bx = bl * 8 + xg;
+  gx = nbx;
+  return bx < nbx;
+}
+
 // ------------------------------------------------------------------ JVP
 // J1: cs1 = local scan of t1*sf over j < B-2
 template <class P>
@@ -170,10 +195,12 @@ __device__ __forceinline__ void amp_jvp_1_body(int bx, int by, int gx, double* s
   if (threadIdx.x == 0) tot1[bx] = t;
 }
 
-__global__ __launch_bounds__(AT) void amp_jvp_1(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ tspec,
+__global__ __launch_bounds__(AT) void amp_jvp_1(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ tspec,
                                                 double* __restrict__ loc, double* __restrict__ tot1, long long ls, long long vs, long long wsd) {
   __shared__ double sh[2 * AT];
-  amp_jvp_1_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, tspec, const_cast<double*>(loc), const_cast<double*>(tot1), ls, vs, wsd);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_jvp_1_body<double*>(bx_, by_, gx_, sh, c_, dcs, tspec, const_cast<double*>(loc), const_cast<double*>(tot1), ls, vs, wsd);
 }
 
 // J3: c = loc + carry; t = (c + c_prev)/2*lv + t0*c0; local scan of t
@@ -210,11 +237,13 @@ __device__ __forceinline__ void amp_jvp_3_body(int bx, int by, int gx, double* s
   if (threadIdx.x == 0) tot2[bx] = t;
 }
 
-__global__ __launch_bounds__(AT) void amp_jvp_3(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ tspec,
+__global__ __launch_bounds__(AT) void amp_jvp_3(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ tspec,
                                                 const double* __restrict__ tot1, double* __restrict__ loc,
                                                 double* __restrict__ tot2, long long ls, long long vs, long long wsd) {
   __shared__ double sh[2 * AT];
-  amp_jvp_3_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, tspec, const_cast<double*>(tot1), const_cast<double*>(loc), const_cast<double*>(tot2), ls, vs, wsd);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_jvp_3_body<double*>(bx_, by_, gx_, sh, c_, dcs, tspec, const_cast<double*>(tot1), const_cast<double*>(loc), const_cast<double*>(tot2), ls, vs, wsd);
 }
 
 // J5: tl = [0,0, loc + carry]; dapre; partial sums of mspec*dapre
@@ -268,12 +297,14 @@ __device__ __forceinline__ void amp_jvp_5_body(int bx, int by, int gx, double* s
   if (threadIdx.x == 0) part[bx] = s;
 }
 
-__global__ __launch_bounds__(AT) void amp_jvp_5(AmpConst c_, const AmpConst* __restrict__ dcs, const double* tfl, const double* tsl,
+__global__ __launch_bounds__(AT) void amp_jvp_5(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, const double* tfl, const double* tsl,
                                                 const double* tflex, const double* tasp,
                                                 const double* __restrict__ loc, const double* __restrict__ tot2,
                                                 double* __restrict__ dapre, double* __restrict__ part, long long ls, long long vs, long long wsd) {
   __shared__ double sh[2 * AT];
-  amp_jvp_5_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, tfl, tsl, tflex, tasp, const_cast<double*>(loc), const_cast<double*>(tot2), const_cast<double*>(dapre), const_cast<double*>(part), ls, vs, wsd);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_jvp_5_body<double*>(bx_, by_, gx_, sh, c_, dcs, tfl, tsl, tflex, tasp, const_cast<double*>(loc), const_cast<double*>(tot2), const_cast<double*>(dapre), const_cast<double*>(part), ls, vs, wsd);
 }
 
 // J7: da from dapre and dS = sum(part)
@@ -305,12 +336,14 @@ __device__ __forceinline__ void amp_jvp_7_body(int bx, int by, int gx, double* s
   }
 }
 
-__global__ __launch_bounds__(AT) void amp_jvp_7(AmpConst c_, const AmpConst* __restrict__ dcs, const double* tfl, const double* tzm,
+__global__ __launch_bounds__(AT) void amp_jvp_7(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, const double* tfl, const double* tzm,
                                                 const double* __restrict__ dapre, const double* __restrict__ part,
                                                 int npart, double* __restrict__ da, long long ls, long long vs, long long wsd,
                                                 long long des) {
   __shared__ double sh[2 * AT];
-  amp_jvp_7_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, tfl, tzm, const_cast<double*>(dapre), const_cast<double*>(part), npart, da, ls, vs, wsd, des);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_jvp_7_body<double*>(bx_, by_, gx_, sh, c_, dcs, tfl, tzm, const_cast<double*>(dapre), const_cast<double*>(part), npart, da, ls, vs, wsd, des);
 }
 
 // ------------------------------------------------------------------ VJP
@@ -327,9 +360,11 @@ __device__ __forceinline__ void amp_vjp_1_body(int bx, int by, int gx, double* s
   if (threadIdx.x == 0) part[bx] = s;
 }
 
-__global__ __launch_bounds__(AT) void amp_vjp_1(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ g, double* __restrict__ part, long long ls, long long vs, long long wsd) {
+__global__ __launch_bounds__(AT) void amp_vjp_1(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ g, double* __restrict__ part, long long ls, long long vs, long long wsd) {
   __shared__ double sh[2 * AT];
-  amp_vjp_1_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, g, const_cast<double*>(part), ls, vs, wsd);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_vjp_1_body<double*>(bx_, by_, gx_, sh, c_, dcs, g, const_cast<double*>(part), ls, vs, wsd);
 }
 
 // V2: gapre; partials R2 = sum vslope*gapre, R3 = sum gapre*sc
@@ -363,11 +398,13 @@ __device__ __forceinline__ void amp_vjp_2_body(int bx, int by, int gx, double* s
   }
 }
 
-__global__ __launch_bounds__(AT) void amp_vjp_2(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ g,
+__global__ __launch_bounds__(AT) void amp_vjp_2(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ g,
                                                 const double* __restrict__ part1, int np1,
                                                 double* __restrict__ gapre, double* __restrict__ part23, long long ls, long long vs, long long wsd) {
   __shared__ double sh[2 * AT];
-  amp_vjp_2_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, g, const_cast<double*>(part1), np1, const_cast<double*>(gapre), const_cast<double*>(part23), ls, vs, wsd);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_vjp_2_body<double*>(bx_, by_, gx_, sh, c_, dcs, g, const_cast<double*>(part1), np1, const_cast<double*>(gapre), const_cast<double*>(part23), ls, vs, wsd);
 }
 
 // gtl[2+j] = gapre[2+j], minus R3 at the last bin
@@ -405,11 +442,13 @@ __device__ __forceinline__ void amp_vjp_3_body(int bx, int by, int gx, double* s
   if (threadIdx.x == 0) tot[bx] = t;
 }
 
-__global__ __launch_bounds__(AT) void amp_vjp_3(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ gapre,
+__global__ __launch_bounds__(AT) void amp_vjp_3(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ gapre,
                                                 const double* __restrict__ part23, int np,
                                                 double* __restrict__ loc, double* __restrict__ tot, long long ls, long long vs, long long wsd) {
   __shared__ double sh[2 * AT];
-  amp_vjp_3_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, const_cast<double*>(gapre), const_cast<double*>(part23), np, const_cast<double*>(loc), const_cast<double*>(tot), ls, vs, wsd);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_vjp_3_body<double*>(bx_, by_, gx_, sh, c_, dcs, const_cast<double*>(gapre), const_cast<double*>(part23), np, const_cast<double*>(loc), const_cast<double*>(tot), ls, vs, wsd);
 }
 
 // V4: y = loc + suffix carry (g0); z = y*lv/2; w = z_j + z_{j+1}; reverse local scan of w
@@ -453,12 +492,14 @@ __device__ __forceinline__ void amp_vjp_4_body(int bx, int by, int gx, double* s
   if (threadIdx.x == 0) tot4[bx] = t;
 }
 
-__global__ __launch_bounds__(AT) void amp_vjp_4(AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ gapre,
+__global__ __launch_bounds__(AT) void amp_vjp_4(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, const double* __restrict__ gapre,
                                                 const double* __restrict__ part23, int np,
                                                 const double* __restrict__ tot3, double* __restrict__ y,
                                                 double* __restrict__ loc, double* __restrict__ tot4, long long ls, long long vs, long long wsd) {
   __shared__ double sh[2 * AT];
-  amp_vjp_4_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, const_cast<double*>(gapre), const_cast<double*>(part23), np, const_cast<double*>(tot3), const_cast<double*>(y), const_cast<double*>(loc), const_cast<double*>(tot4), ls, vs, wsd);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_vjp_4_body<double*>(bx_, by_, gx_, sh, c_, dcs, const_cast<double*>(gapre), const_cast<double*>(part23), np, const_cast<double*>(tot3), const_cast<double*>(y), const_cast<double*>(loc), const_cast<double*>(tot4), ls, vs, wsd);
 }
 
 
@@ -504,11 +545,13 @@ __device__ __forceinline__ void amp_vjp_5_body(int bx, int by, int gx, double* s
   }
 }
 
-__global__ __launch_bounds__(AT) void amp_vjp_5(AmpConst c_, const AmpConst* __restrict__ dcs, AmpOut o, const double* __restrict__ y,
+__global__ __launch_bounds__(AT) void amp_vjp_5(int nbx_, AmpConst c_, const AmpConst* __restrict__ dcs, AmpOut o, const double* __restrict__ y,
                                                 const double* __restrict__ loc, const double* __restrict__ tot4,
                                                 double* __restrict__ part45, long long ls, long long vs, long long wsd) {
   __shared__ double sh[2 * AT];
-  amp_vjp_5_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, o, const_cast<double*>(y), const_cast<double*>(loc), const_cast<double*>(tot4), const_cast<double*>(part45), ls, vs, wsd);
+  int bx_, by_, gx_;
+  if (!amp_block(nbx_, bx_, by_, gx_)) return;
+  amp_vjp_5_body<double*>(bx_, by_, gx_, sh, c_, dcs, o, const_cast<double*>(y), const_cast<double*>(loc), const_cast<double*>(tot4), const_cast<double*>(part45), ls, vs, wsd);
 }
 
 // V6: scalar cotangents (one block)
@@ -625,6 +668,20 @@ __global__ __launch_bounds__(AT) void amp_barrier_probe(int nbar) {
 }
 
 static int nblk(long long n, int per) { return (int)std::max<long long>(1, (n + per - 1) / per); }
+
+// batched launches of the multi-kernel JVP / VJP: XCD-grouped right-hand
+// sides (amp_block) for the kernels it was measured to help (pref: the two
+// JVP scans, -3 us together at B = 313,847 with 4 RHS; the others measured
+// -0.5 to +1 us, within noise), never for a single right-hand side.
+// NFT_AMP_REMAP=0 / 2: off / on for every kernel.
+static bool amp_remap(unsigned ny, bool pref) {
+  static const int mode = getenv("NFT_AMP_REMAP") ? atoi(getenv("NFT_AMP_REMAP")) : 1;
+  return ny > 1 && (mode == 2 || (mode == 1 && pref));
+}
+static dim3 amp_grid(int nbx, unsigned ny, bool pref = false) {
+  return amp_remap(ny, pref) ? dim3((unsigned)(((nbx + 7) & ~7) * ny)) : dim3((unsigned)nbx, ny);
+}
+static int amp_nbx(int nbx, unsigned ny, bool pref = false) { return amp_remap(ny, pref) ? nbx : 0; }
 
 // Fused kernels: one launch per JVP / VJP.  Workgroup w owns scan tile
 // i = w % nbM (E*AT consecutive scan positions j = b - 2, striped) of
@@ -1284,15 +1341,15 @@ int nft_amp_jvp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
   const unsigned ny = (unsigned)nrhs;
   if (c.has_flex) {
     prof_mark(s, "amp_jvp_1");
-    hipLaunchKernelGGL(amp_jvp_1, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, tspec, loc, tot1, ls, vs, wsd);
+    hipLaunchKernelGGL(amp_jvp_1, amp_grid(nbM, ny, true), dim3(AT), 0, s, amp_nbx(nbM, ny, true), c, dcs, tspec, loc, tot1, ls, vs, wsd);
     prof_mark(s, "amp_jvp_3");
-    hipLaunchKernelGGL(amp_jvp_3, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, tspec, tot1, loc, tot2, ls, vs, wsd);
+    hipLaunchKernelGGL(amp_jvp_3, amp_grid(nbM, ny, true), dim3(AT), 0, s, amp_nbx(nbM, ny, true), c, dcs, tspec, tot1, loc, tot2, ls, vs, wsd);
   }
   prof_mark(s, "amp_jvp_5");
-  hipLaunchKernelGGL(amp_jvp_5, dim3(nbB, ny), dim3(AT), 0, s, c, dcs, tfl, tsl, tflex, tasp, loc, tot2, dapre, part, ls,
+  hipLaunchKernelGGL(amp_jvp_5, amp_grid(nbB, ny), dim3(AT), 0, s, amp_nbx(nbB, ny), c, dcs, tfl, tsl, tflex, tasp, loc, tot2, dapre, part, ls,
                      vs, wsd);
   prof_mark(s, "amp_jvp_7");
-  hipLaunchKernelGGL(amp_jvp_7, dim3(nblk(B, AT) < 1024 ? nblk(B, AT) : 1024, ny), dim3(AT), 0, s, c, dcs, tfl, tzm,
+  hipLaunchKernelGGL(amp_jvp_7, amp_grid(n7, ny), dim3(AT), 0, s, amp_nbx(n7, ny), c, dcs, tfl, tzm,
                      dapre, part, nbB, da, ls, vs, wsd, (long long)(da_elem_stride > 0 ? da_elem_stride : 1));
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
@@ -1327,17 +1384,17 @@ int nft_amp_vjp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
   }
   const unsigned ny = (unsigned)nrhs;
   prof_mark(s, "amp_vjp_1");
-  hipLaunchKernelGGL(amp_vjp_1, dim3(nr, ny), dim3(AT), 0, s, c, dcs, g, part1, ls, vs, wsd);
+  hipLaunchKernelGGL(amp_vjp_1, amp_grid(nr, ny), dim3(AT), 0, s, amp_nbx(nr, ny), c, dcs, g, part1, ls, vs, wsd);
   prof_mark(s, "amp_vjp_2");
-  hipLaunchKernelGGL(amp_vjp_2, dim3(nr, ny), dim3(AT), 0, s, c, dcs, g, part1, nr, gapre, part23, ls, vs, wsd);
+  hipLaunchKernelGGL(amp_vjp_2, amp_grid(nr, ny), dim3(AT), 0, s, amp_nbx(nr, ny), c, dcs, g, part1, nr, gapre, part23, ls, vs, wsd);
   if (c.has_flex) {
     prof_mark(s, "amp_vjp_3");
-    hipLaunchKernelGGL(amp_vjp_3, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, gapre, part23, nr, loc, tot3, ls, vs, wsd);
+    hipLaunchKernelGGL(amp_vjp_3, amp_grid(nbM, ny), dim3(AT), 0, s, amp_nbx(nbM, ny), c, dcs, gapre, part23, nr, loc, tot3, ls, vs, wsd);
     prof_mark(s, "amp_vjp_4");
-    hipLaunchKernelGGL(amp_vjp_4, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, gapre, part23, nr, tot3, y, loc, tot4, ls, vs,
+    hipLaunchKernelGGL(amp_vjp_4, amp_grid(nbM, ny), dim3(AT), 0, s, amp_nbx(nbM, ny), c, dcs, gapre, part23, nr, tot3, y, loc, tot4, ls, vs,
                        wsd);
     prof_mark(s, "amp_vjp_5");
-    hipLaunchKernelGGL(amp_vjp_5, dim3(nbM, ny), dim3(AT), 0, s, c, dcs, o, y, loc, tot4, part45, ls, vs, wsd);
+    hipLaunchKernelGGL(amp_vjp_5, amp_grid(nbM, ny), dim3(AT), 0, s, amp_nbx(nbM, ny), c, dcs, o, y, loc, tot4, part45, ls, vs, wsd);
   }
   prof_mark(s, "amp_vjp_6");
   hipLaunchKernelGGL(amp_vjp_6, dim3(1, ny), dim3(AT), 0, s, c, dcs, o, g, part1, nr, part23, nr, part45,

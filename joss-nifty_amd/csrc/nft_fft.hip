@@ -780,16 +780,30 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
   unsigned nn[D];
 #pragma unroll
   for (int a = 0; a < D; ++a) nn[a] = (unsigned)f.fn[a];
+  // threads walk the cell grid with its last axis padded to hp (a multiple
+  // of 64): each wave covers one aligned run of a cell row, so its direct
+  // images are whole cache lines and its mirrored ones share their one
+  // unaligned line with the neighbouring wave
+  const unsigned hl = nn[D - 1] / 2 + 1, hp = (hl + 63) & ~63u;
   for (long long c = (long long)blockIdx.x * 256 + threadIdx.x; c < ncell; c += (long long)gridDim.x * 256) {
     unsigned cc[D], rest = (unsigned)c;
+    {
+      const unsigned q = rest / hp;
+      cc[D - 1] = rest - q * hp;
+      rest = q;
+    }
+    if (cc[D - 1] >= hl) continue;
 #pragma unroll
-    for (int a = D - 1; a >= 0; --a) {
+    for (int a = D - 2; a >= 0; --a) {
       const unsigned h = nn[a] / 2 + 1;
       const unsigned q = rest / h;
       cc[a] = rest - q * h;
       rest = q;
     }
-    const long long ix = (long long)f.pidx[c] * f.ce;
+    unsigned cell = 0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) cell = cell * (nn[a] / 2 + 1) + cc[a];
+    const long long ix = (long long)f.pidx[cell] * f.ce;
     T cv[8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) cv[b] = (T)0;
@@ -914,8 +928,8 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     static const long long cap = getenv("NFT_PRO_NBLK") ? atoll(getenv("NFT_PRO_NBLK")) : (1LL << 30);
     const unsigned nblk = (unsigned)std::min<long long>((f.P + 255) / 256, cap);
     if (f.fnd > 0 && f.pb) {
-      long long ncell = 1;
-      for (int a = 0; a < f.fnd; ++a) ncell *= f.fn[a] / 2 + 1;
+      long long ncell = 1;  // padded cell grid (pro_fold_kernel)
+      for (int a = 0; a < f.fnd; ++a) ncell *= a == f.fnd - 1 ? ((f.fn[a] / 2 + 1 + 63) & ~63LL) : f.fn[a] / 2 + 1;
       prof_mark(s, f.dr ? "pro_fold+dir" : "pro_fold");
       const dim3 grid((unsigned)((ncell + 255) / 256));
       if (f.fnd == 1)
@@ -1148,7 +1162,7 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     f.dr = nullptr;
     if (fz->dir_r) {
       if (!fz->pro_folded || !f.pb || f.P <= 0 || f.nb < 1 || f.nb > 8 || !fz->dir_sc || !fz->dir_part ||
-          fz->dir_blk0 < 0 || fz->dir_pstride < fz->dir_blk0 + 1) {
+          fz->dir_blk0 < 0 || fz->dir_pstride < fz->dir_blk0 + nft_hartley_dir_blocks(f.fnd, (const int64_t*)f.fn)) {
         set_last_error("nft_hartley_fused: the direction carried by the prologue needs a folded, batched "
                        "prologue (<= 8 items) and its scalars / partials");
         return NFT_ERR_ARG;
@@ -1185,6 +1199,16 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
   if (dtype == 1) return hartley_fused_impl<float>(f, in, out, g, ax, sigma, scale, workspace, ws_bytes, hws, stream);
   set_last_error("bad dtype %d", dtype);
   return NFT_ERR_ARG;
+}
+
+int nft_hartley_dir_blocks(int ndim, const int64_t* shape) {
+  if (ndim < 1 || ndim > 3 || !shape) return 0;
+  long long ncell = 1;
+  for (int a = 0; a < ndim; ++a) {
+    if (shape[a] < 1) return 0;
+    ncell *= a == ndim - 1 ? ((shape[a] / 2 + 1 + 63) & ~63LL) : shape[a] / 2 + 1;
+  }
+  return (int)((ncell + 255) / 256);
 }
 
 int nft_hartley_cg_blocks(int ndim, const int64_t* shape, int naxes, const int* axes, int dtype) {

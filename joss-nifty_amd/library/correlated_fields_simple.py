@@ -634,8 +634,7 @@ class CFJacobian(LinearOperator):
         jb = self._m.jbins
         if not (_PRO_FOLD and jb.fold is not None) or not (1 <= k <= 8):
             return 0
-        ncell = int(np.prod([n // 2 + 1 for n in jb.fold["shape"]]))
-        return (ncell + 255) // 256
+        return _native.hartley_dir_blocks(jb.fold["shape"])
 
     def mv_grid(self, D, da, Q, W, shift=0.0, qpart=None, after_w=None, cg=None, pro_dir=None):
         """forward transform (with the prologue), W, adjoint transform: the

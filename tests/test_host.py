@@ -30,6 +30,17 @@ def test_library_exports_every_header_symbol():
     _native.load()
 
 
+def test_folded_prologue_block_count():
+    """nft_hartley_dir_blocks: cell grid prod(n/2+1), last axis padded to 64,
+    256 cells per block (pure host arithmetic)"""
+    from nifty_amd import _native
+    assert _native.hartley_dir_blocks((2048, 2048)) == (1025 * 1088 + 255) // 256
+    assert _native.hartley_dir_blocks((64, 30)) == (33 * 64 + 255) // 256
+    assert _native.hartley_dir_blocks((8, 8, 130)) == (5 * 5 * 128 + 255) // 256
+    assert _native.hartley_dir_blocks((100,)) == 1
+    assert _native.hartley_dir_blocks((0, 4)) == 0
+
+
 def test_no_cpu_fallback():
     import torch
     from nifty_amd import _native
