@@ -70,7 +70,9 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
   // (no FMA contraction): batched results are bitwise the K = 1 results
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CAP_F / 256;
-  __shared__ double u[K][256];
+  // pixel-major tile: the K values of one pixel are adjacent (one or two
+  // 16-byte LDS reads per entry instead of K 8-byte ones)
+  __shared__ __align__(16) double u[256][K];
   __shared__ float ew[K == 1 ? 1 : LOS_CAP_F];
   __shared__ unsigned char el[K == 1 ? 1 : LOS_CAP_F];
   __shared__ double prodbuf[K == 1 ? LOS_CAP_F : 1];
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       v = (double)x[b * xs + px];
       if (cs) v *= (double)cs[b * css + px];
     }
-    u[b][t] = v;
+    u[t][b] = v;
   }
   // four lanes per segment: thread t serves segments sq + 64 r
   constexpr int RND = LOS_SEG_ROUNDS;
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int k = t + i * 256;
-        if (k < n) prod[k] = (double)wv[i] * u[0][lv[i]];
+        if (k < n) prod[k] = (double)wv[i] * u[lv[i]][0];
       }
     }
     __syncthreads();
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
         for (int k = a + sub; k < e; k += 4) a0 += prod[k];
       } else {
         for (int k = a + sub; k < e; k += 4)
-          a0 = a0 + (double)p.ent_wf[e0 + k] * u[0][p.ent_loc[e0 + k]];
+          a0 = a0 + (double)p.ent_wf[e0 + k] * u[p.ent_loc[e0 + k]][0];
       }
       a0 += __shfl_xor(a0, 1, 64);
       a0 += __shfl_xor(a0, 2, 64);
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       const double w = staged ? (double)ew[k] : (double)p.ent_wf[e0 + k];
       const int l = staged ? el[k] : p.ent_loc[e0 + k];
 #pragma unroll
-      for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[b][l];
+      for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
     }
 #pragma unroll
     for (int b = 0; b < K; ++b) {
