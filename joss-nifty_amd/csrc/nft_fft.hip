@@ -920,7 +920,25 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     set_last_error("nft_hartley_fused: the direction carried by the prologue needs the folded batched prologue pass");
     return NFT_ERR_UNSUPPORTED;
   }
-  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && (f.nb > 1 || f.dr) &&
+  // a single folded item (P = 0) takes the split path too, as a batch of one:
+  // the in-pass prologue measured 116 us at 2048^2 against about 45 for the
+  // folded pass + the plain persistent R2C pass (NFT_PRO_SPLIT1=0: off)
+  static const bool split1 = !getenv("NFT_PRO_SPLIT1") || atoi(getenv("NFT_PRO_SPLIT1")) != 0;
+  if (split1 && !f.dr && f.P == 0 && f.fnd > 0 && f.pb && f.pro && !v1_only && !no_split &&
+      ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
+    fast::FuseArgs f1 = f;
+    f1.P = ntot;
+    f1.nb = 1;
+    f1.pshift = -1;
+    if ((ntot & (ntot - 1)) == 0) {
+      int sh = 0;
+      while ((1LL << sh) < ntot) ++sh;
+      f1.pshift = sh;
+    }
+    f1.sx = f1.so = f1.sd = f1.s2 = ntot;
+    return hartley_fused_impl<T>(f1, in, out, g, ax, sigma, scale, ws, ws_bytes, hws, s);
+  }
+  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && (f.nb > 1 || f.dr || f.fnd > 0) &&
       (long long)f.nb * f.P == ntot &&
       ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
     T* u = (T*)((char*)ws + align256(hws));
