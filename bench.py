@@ -244,6 +244,9 @@ def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False):
         # epilogue): two launches, the keys before and after the grid
         # segment; per launch the model carries half of their bytes
         "cg_update_seg": 3 * 8 * k * (n_lat - N),
+        # both amplitude segments in one launch (nft_cg_*2_batched)
+        "cg_update_seg2": 6 * 8 * k * (n_lat - N),
+        "cg_dir_dd2": 3 * 8 * k * (n_lat - N),
         # unpack + the grid segment's CG update: half spectrum (k), A, xi0;
         # x, r, d in (k), x, r and w = xi0*v out (k) -- q is not stored
         "fft_unpack+cg": 16 * k * Hh + 16 * N + 40 * k * N + 8 * k * (Hh if pairs else N),

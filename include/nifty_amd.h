@@ -378,6 +378,13 @@ int nft_cg_dd_blocks(int64_t n);
 int nft_cg_direction_dd_batched(void* d, const void* r, int64_t n, int64_t vstride, int nrhs, int dtype,
                                 const double* sc, double shift, double* part, int64_t pstride,
                                 hipStream_t stream);
+/* nft_cg_direction_dd_batched over two segments in one launch: [0, n1) with
+ * partials at part[rhs * pstride + b] and [o2, o2 + n2) (o2 >= n1) at
+ * part[rhs * pstride + poff2 + b] (poff2 >= nft_cg_dd_blocks(n1)); per
+ * block the work of two separate calls. */
+int nft_cg_direction_dd2_batched(void* d, const void* r, int64_t n1, int64_t o2, int64_t n2, int64_t vstride,
+                                 int nrhs, int dtype, const double* sc, double shift, double* part, int64_t poff2,
+                                 int64_t pstride, hipStream_t stream);
 int nft_fold_partials(const double* part, int nb, int nrhs, double* out, int64_t out_stride,
                       hipStream_t stream);
 /* The CG update split over segments of the packed vectors (pointers offset by
@@ -391,6 +398,14 @@ int nft_fold_partials(const double* part, int nb, int nrhs, double* out, int64_t
 int nft_cg_update_seg_batched(void* x, void* r, const void* d, const void* q, const void* b, int64_t n,
                               int64_t vstride, int nrhs, int dtype, double shift, const double* sc,
                               double* part, int nbtot, int blk0, hipStream_t stream);
+/* The same over two segments in one launch (the amplitude keys before and
+ * after the grid segment): elements [0, n1) with partial blocks at blk1 and
+ * [o2, o2 + n2) (o2 >= n1) at blk2, the block ranges disjoint; b = NULL.
+ * Per block the work (and so every partial) of two separate
+ * nft_cg_update_seg_batched calls. */
+int nft_cg_update_seg2_batched(void* x, void* r, const void* d, const void* q, int64_t n1, int blk1, int64_t o2,
+                               int64_t n2, int blk2, int64_t vstride, int nrhs, int dtype, double shift,
+                               const double* sc, double* part, int nbtot, hipStream_t stream);
 int nft_cg_finalize_batched(const double* part, int nbtot, int nrhs, double* sc, hipStream_t stream);
 
 /* ---- correlated-field amplitude Jacobian ------------------------------ */

@@ -70,6 +70,8 @@ SIGNATURES = {
     "nft_hartley_cg_blocks": (_i, [_i, _p, _i, _p, _i]),
     "nft_hartley_dir_blocks": (_i, [_i, _p]),
     "nft_cg_update_seg_batched": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i, _i, _d, _p, _p, _i, _i, _p]),
+    "nft_cg_update_seg2_batched": (_i, [_p, _p, _p, _p, _i64, _i, _i64, _i64, _i, _i64, _i, _i, _d, _p, _p, _i, _p]),
+    "nft_cg_direction_dd2_batched": (_i, [_p, _p, _i64, _i64, _i64, _i64, _i, _i, _p, _d, _p, _i64, _i64, _p]),
     "nft_cg_finalize_batched": (_i, [_p, _i, _i, _p, _p]),
     "nft_amp_forward_buf": (_i64, [_i64]),
     "nft_amp_forward_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _p, _i64, _p, _i64, _p, _p, _p]),

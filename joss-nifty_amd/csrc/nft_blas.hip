@@ -151,9 +151,26 @@ __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T*
                                                            const T* __restrict__ q,
                                                            const T* __restrict__ b, long long n, long long vs,
                                                            T shift, const double* __restrict__ sc,
-                                                           double* __restrict__ part, int nbtot, int blk0) {
+                                                           double* __restrict__ part, int nbtot, int blk0,
+                                                           int nb1 = 0, long long o2 = 0, long long n2 = 0,
+                                                           int blk2 = 0) {
+  // two ranges in one launch (nb1 > 0): blocks [0, nb1) serve [0, n) with
+  // partial slots blk0 + block, the rest serve [o2, o2 + n2) with slots
+  // blk2 + (block - nb1) -- per block exactly the work of separate launches
   __shared__ double sh[3 * (RED_NT / 64)];
-  const long long o = (long long)blockIdx.y * vs;
+  int bx = blockIdx.x, gx = gridDim.x;
+  long long o = (long long)blockIdx.y * vs;
+  if (nb1 > 0) {
+    if (bx < nb1) {
+      gx = nb1;
+    } else {
+      bx -= nb1;
+      gx -= nb1;
+      o += o2;
+      n = n2;
+      blk0 = blk2;
+    }
+  }
   sc += blockIdx.y * NFT_CG_NSCALARS;
   part += (long long)blockIdx.y * 3 * nbtot + blk0;
   x += o;
@@ -167,8 +184,8 @@ __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T*
                   sc[NFT_CG_DONE] == 0.0;
   const T al = (T)alpha;
   double v[3] = {0.0, 0.0, 0.0};
-  const long long stride = (long long)gridDim.x * RED_NT;
-  for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
+  const long long stride = (long long)gx * RED_NT;
+  for (long long i = (long long)bx * RED_NT + threadIdx.x; i < n; i += stride) {
     T xi = x[i], ri = r[i];
     if (ok) {
       const T di = d[i];
@@ -184,9 +201,9 @@ __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T*
   }
   block_sum<3>(v, sh);
   if (threadIdx.x == 0) {
-    part[0 * nbtot + blockIdx.x] = v[0];
-    part[1 * nbtot + blockIdx.x] = v[1];
-    part[2 * nbtot + blockIdx.x] = v[2];
+    part[0 * nbtot + bx] = v[0];
+    part[1 * nbtot + bx] = v[1];
+    part[2 * nbtot + bx] = v[2];
   }
 }
 
@@ -249,29 +266,45 @@ template <typename T>
 __global__ __launch_bounds__(RED_NT) void cg_dir_dd_kernel(T* __restrict__ d, const T* __restrict__ r, long long n,
                                                            long long vs, const double* __restrict__ sc,
                                                            double shift, double* __restrict__ part,
-                                                           long long pstride) {
+                                                           long long pstride, int nb1 = 0, long long o2 = 0,
+                                                           long long n2 = 0, long long poff2 = 0) {
+  // two ranges in one launch (nb1 > 0, as cg_update_kernel): the second
+  // range's partials start poff2 slots after the first's
   __shared__ double sh[RED_NT / 64];
+  int bx = blockIdx.x, gx = gridDim.x;
+  long long o = 0;
   sc += blockIdx.y * NFT_CG_NSCALARS;
   part += (long long)blockIdx.y * pstride;
+  if (nb1 > 0) {
+    if (bx < nb1) {
+      gx = nb1;
+    } else {
+      bx -= nb1;
+      gx -= nb1;
+      o = o2;
+      n = n2;
+      part += poff2;
+    }
+  }
   if (sc[NFT_CG_DONE] != 0.0) {
-    if (threadIdx.x == 0) part[blockIdx.x] = 0.0;
+    if (threadIdx.x == 0) part[bx] = 0.0;
     return;
   }
-  d += (long long)blockIdx.y * vs;
-  r += (long long)blockIdx.y * vs;
+  d += (long long)blockIdx.y * vs + o;
+  r += (long long)blockIdx.y * vs + o;
   double beta = sc[NFT_CG_GAMMA] / sc[NFT_CG_GPREV];
   if (!(beta > 0.0)) beta = 0.0;
   const T bt = (T)beta;
   double v[1] = {0.0};
-  const long long stride = (long long)gridDim.x * RED_NT;
+  const long long stride = (long long)gx * RED_NT;
 #pragma unroll 4
-  for (long long i = (long long)blockIdx.x * RED_NT + threadIdx.x; i < n; i += stride) {
+  for (long long i = (long long)bx * RED_NT + threadIdx.x; i < n; i += stride) {
     const T di = bt * d[i] + r[i];
     d[i] = di;
     v[0] += (double)di * (double)di;
   }
   block_sum<1>(v, sh);
-  if (threadIdx.x == 0) part[blockIdx.x] = shift * v[0];
+  if (threadIdx.x == 0) part[bx] = shift * v[0];
 }
 
 // r = (ax + shift x) - b (exact residual refresh, conjugate_gradient.py:103-105
@@ -474,6 +507,33 @@ int nft_cg_update_seg_batched(void* x, void* r, const void* d, const void* q, co
   return NFT_OK;
 }
 
+int nft_cg_update_seg2_batched(void* x, void* r, const void* d, const void* q, int64_t n1, int blk1, int64_t o2,
+                               int64_t n2, int blk2, int64_t vstride, int nrhs, int dtype, double shift,
+                               const double* sc, double* part, int nbtot, hipStream_t stream) {
+  const int nb1 = red_blocks(n1), nb2 = red_blocks(n2);
+  if (n1 < 1 || n2 < 1 || o2 < n1 || blk1 < 0 || blk2 < 0 || blk1 + nb1 > nbtot || blk2 + nb2 > nbtot || !part ||
+      (blk1 < blk2 + nb2 && blk2 < blk1 + nb1)) {
+    set_last_error("nft_cg_update_seg2: bad ranges or partial blocks");
+    return NFT_ERR_ARG;
+  }
+  const dim3 grid(nb1 + nb2, nrhs);
+  prof_mark(stream, "cg_update_seg2");
+  if (dtype == 0)
+    hipLaunchKernelGGL(cg_update_kernel<double>, grid, dim3(RED_NT), 0, stream, (double*)x, (double*)r,
+                       (const double*)d, (const double*)q, (const double*)nullptr, (long long)n1,
+                       (long long)vstride, shift, sc, part, nbtot, blk1, nb1, (long long)o2, (long long)n2, blk2);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(cg_update_kernel<float>, grid, dim3(RED_NT), 0, stream, (float*)x, (float*)r,
+                       (const float*)d, (const float*)q, (const float*)nullptr, (long long)n1, (long long)vstride,
+                       (float)shift, sc, part, nbtot, blk1, nb1, (long long)o2, (long long)n2, blk2);
+  else {
+    set_last_error("nft_cg_update_seg2: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
 int nft_cg_finalize_batched(const double* part, int nbtot, int nrhs, double* sc, hipStream_t stream) {
   prof_mark(stream, "cg_finalize_kernel");
   hipLaunchKernelGGL(cg_finalize_kernel, dim3(nrhs), dim3(RED_NT), 0, stream, part, nbtot, sc);
@@ -525,6 +585,32 @@ int nft_cg_direction_dd_batched(void* d, const void* r, int64_t n, int64_t vstri
                        (long long)n, (long long)vstride, sc, shift, part, (long long)pstride);
   else {
     set_last_error("nft_cg_direction_dd: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_direction_dd2_batched(void* d, const void* r, int64_t n1, int64_t o2, int64_t n2, int64_t vstride,
+                                 int nrhs, int dtype, const double* sc, double shift, double* part, int64_t poff2,
+                                 int64_t pstride, hipStream_t stream) {
+  const int nb1 = red_blocks(n1), nb2 = red_blocks(n2);
+  if (!part || n1 < 1 || n2 < 1 || o2 < n1 || nrhs < 1 || poff2 < nb1 || pstride < poff2 + nb2) {
+    set_last_error("nft_cg_direction_dd2: bad ranges or partial slots");
+    return NFT_ERR_ARG;
+  }
+  const dim3 grid(nb1 + nb2, nrhs);
+  prof_mark(stream, "cg_dir_dd2");
+  if (dtype == 0)
+    hipLaunchKernelGGL(cg_dir_dd_kernel<double>, grid, dim3(RED_NT), 0, stream, (double*)d, (const double*)r,
+                       (long long)n1, (long long)vstride, sc, shift, part, (long long)pstride, nb1, (long long)o2,
+                       (long long)n2, (long long)poff2);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(cg_dir_dd_kernel<float>, grid, dim3(RED_NT), 0, stream, (float*)d, (const float*)r,
+                       (long long)n1, (long long)vstride, sc, shift, part, (long long)pstride, nb1, (long long)o2,
+                       (long long)n2, (long long)poff2);
+  else {
+    set_last_error("nft_cg_direction_dd2: bad dtype %d", dtype);
     return NFT_ERR_ARG;
   }
   NFT_HIP_CHECK(hipGetLastError());

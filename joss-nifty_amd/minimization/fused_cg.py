@@ -492,6 +492,9 @@ _CARRY = os.environ.get("NFT_CG_CARRY", "1") != "0"
 # ... and the grid segment's direction update inside the folded prologue
 # (NFT_CG_CARRY_DIR=0: a separate direction pass)
 _CARRY_DIR = os.environ.get("NFT_CG_CARRY_DIR", "1") != "0"
+# the amplitude keys before and after the grid segment in one launch each for
+# the direction and the update (nft_cg_*2_batched; NFT_CG_SEG2=0: two each)
+_SEG2 = os.environ.get("NFT_CG_SEG2", "1") != "0"
 
 
 class _CarryIteration:
@@ -549,11 +552,16 @@ class _CarryIteration:
         if self.dirs is None:
             _native._check(lib.nft_cg_direction_dd_batched(P(D), P(Rr), n, n, k, 0, P(SC), self.shift, P(self.PQ),
                                                            pstride, s_))
+        elif _SEG2 and len(self.dirs) == 2 and self.dirs[0][0] == 0:
+            (_, n1, _), (o2, n2, blk2) = self.dirs
+            _native._check(lib.nft_cg_direction_dd2_batched(P(D), P(Rr), n1, o2, n2, n, k, 0, P(SC), self.shift,
+                                                            P(self.PQ), blk2, pstride, s_))
         else:
             for o, ln, blk in self.dirs:
                 _native._check(lib.nft_cg_direction_dd_batched(
                     Pv(D.data_ptr() + 8 * o), Pv(Rr.data_ptr() + 8 * o), ln, n, k, 0, P(SC), self.shift,
                     Pv(self.PQ.data_ptr() + 8 * blk), pstride, s_))
+        if self.dirs is not None:
             pro_dir = dict(r=Rr[0, self.g0:], sc=SC, part=self.PQ, pstride=pstride, shift=self.shift,
                            blk0=self.pro_blk0)
         da = core.mv_amp_jvp(D)
@@ -567,11 +575,16 @@ class _CarryIteration:
                   nbtot=self.nbtot, blk0=self.tiles_blk0)
         w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbd:], after_w=fold, cg=cg, pro_dir=pro_dir)
         core.mv_amp_vjp(D, w, Q, 0.0)
-        for o, ln, blk in self.amp:
-            e = 8 * o
-            _native._check(lib.nft_cg_update_seg_batched(
-                Pv(X.data_ptr() + e), Pv(Rr.data_ptr() + e), Pv(D.data_ptr() + e), Pv(Q.data_ptr() + e), Pv(0),
-                ln, n, k, 0, self.shift, P(SC), P(self.UP), self.nbtot, blk, s_))
+        if _SEG2 and len(self.amp) == 2 and self.amp[0][0] == 0:
+            (_, n1, blk1), (o2, n2, blk2) = self.amp
+            _native._check(lib.nft_cg_update_seg2_batched(P(X), P(Rr), P(D), P(Q), n1, blk1, o2, n2, blk2, n, k, 0,
+                                                          self.shift, P(SC), P(self.UP), self.nbtot, s_))
+        else:
+            for o, ln, blk in self.amp:
+                e = 8 * o
+                _native._check(lib.nft_cg_update_seg_batched(
+                    Pv(X.data_ptr() + e), Pv(Rr.data_ptr() + e), Pv(D.data_ptr() + e), Pv(Q.data_ptr() + e),
+                    Pv(0), ln, n, k, 0, self.shift, P(SC), P(self.UP), self.nbtot, blk, s_))
         _native._check(lib.nft_cg_finalize_batched(P(self.UP), self.nbtot, k, P(SC), s_))
 
 
