@@ -215,17 +215,31 @@ __device__ __forceinline__ void amp_jvp_3_body(int bx, int by, int gx, double* s
   tot2 += by * wsd;
     const long long M = c.B - 2;
   const int nb = (int)((M + ABLK - 1) / ABLK);
-  const double carry = carry_in<false>(tot1, bx, nb, sh);
   const long long j0 = (long long)bx * ABLK + threadIdx.x;
+  // operands in flight before the carry's barriers (same expressions after)
+  double lo[AE], t1[AE], sfv[AE], lvv[AE], t0[AE], c0v[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long j = j0 + (long long)k * AT;
+    if (j < M) {
+      lo[k] = loc[j];
+      t1[k] = tspec[M + j];
+      sfv[k] = c.sf[j];
+      lvv[k] = c.lv[j];
+      t0[k] = tspec[j];
+      c0v[k] = c.c0[j];
+    }
+  }
+  const double carry = carry_in<false>(tot1, bx, nb, sh);
   double v[AE];
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
     long long j = j0 + (long long)k * AT;
     if (j < M) {
-      const double cj = loc[j] + carry;
-      const double u1 = tspec[M + j] * c.sf[j];
+      const double cj = lo[k] + carry;
+      const double u1 = t1[k] * sfv[k];
       const double cp = cj - u1;
-      v[k] = (cj + cp) / 2 * c.lv[j] + tspec[j] * c.c0[j];
+      v[k] = (cj + cp) / 2 * lvv[k] + t0[k] * c0v[k];
     } else {
       v[k] = 0.0;
     }
@@ -263,12 +277,26 @@ __device__ __forceinline__ void amp_jvp_5_body(int bx, int by, int gx, double* s
   part += by * wsd;
     const long long B = c.B, M = B - 2;
   const int nbM = c.has_flex ? (int)((M + ABLK - 1) / ABLK) : 0;
+  const long long b0 = (long long)bx * ABLK;
+  // operands in flight before the carries' barriers (same expressions after)
+  double lo[AE], vsl[AE], scv[AE], qf[AE], qa[AE], ms[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long b = b0 + threadIdx.x + (long long)k * AT;
+    if (b < B) {
+      if (c.has_flex && b >= 2) lo[k] = loc[b - 2];
+      vsl[k] = c.vslope[b];
+      scv[k] = c.sc[b];
+      if (c.has_flex) qf[k] = c.Qf[b];
+      if (c.has_asp) qa[k] = c.Qa[b];
+      ms[k] = c.mspec[b];
+    }
+  }
   double T = 0;  // tl[B-1] = total of the second scan
   if (c.has_flex) T = carry_in<false>(tot2, nbM, nbM, sh);
   const double ssl = c.sig_s * tsl[0];
   const double sf_ = c.has_flex ? tflex[0] : 0.0;
   const double sa_ = c.has_asp ? tasp[0] : 0.0;
-  const long long b0 = (long long)bx * ABLK;
   // tl_b needs scan position j = b-2; this block's j-range spans at most the
   // scan blocks blk0 and blk0+1
   const int blk0 = b0 >= 2 ? (int)((b0 - 2) / ABLK) : 0;
@@ -284,13 +312,13 @@ __device__ __forceinline__ void amp_jvp_5_body(int bx, int by, int gx, double* s
     double tl = 0;
     if (c.has_flex && b >= 2) {
       const long long j = b - 2;
-      tl = loc[j] + ((int)(j / ABLK) == blk0 ? cr0 : cr1);
+      tl = lo[k] + ((int)(j / ABLK) == blk0 ? cr0 : cr1);
     }
-    double d = c.vslope[b] * ssl + tl - T * c.sc[b];
-    if (c.has_flex) d += sf_ * c.Qf[b];
-    if (c.has_asp) d += sa_ * c.Qa[b];
+    double d = vsl[k] * ssl + tl - T * scv[k];
+    if (c.has_flex) d += sf_ * qf[k];
+    if (c.has_asp) d += sa_ * qa[k];
     dapre[b] = d;
-    acc += c.mspec[b] * d;
+    acc += ms[k] * d;
   }
   (void)tfl;
   const double s = block_total(acc, sh);
@@ -319,18 +347,27 @@ __device__ __forceinline__ void amp_jvp_7_body(int bx, int by, int gx, double* s
   dapre += by * wsd;
   part += by * wsd;
   da += by * vs;
-    double s = 0;
+  const long long B = c.B;
+  // the first element's operands in flight before the sum's barriers
+  const long long bf = (long long)bx * AT + threadIdx.x;
+  double anf = 0.0, dpf = 0.0;
+  if (bf < B && bf > 0) {
+    anf = c.An[bf];
+    dpf = dapre[bf];
+  }
+  const double tf0 = tfl[0];
+  double s = 0;
   for (int i = threadIdx.x; i < npart; i += AT) s += part[i];
   const double dS = block_total(s, sh);
-  const double dfl = c.fl * c.ls_f * tfl[0];
-  const long long B = c.B;
-  for (long long b = (long long)bx * AT + threadIdx.x; b < B; b += (long long)gx * AT) {
+  const double dfl = c.fl * c.ls_f * tf0;
+  for (long long b = bf; b < B; b += (long long)gx * AT) {
     double v;
     if (b == 0) {
       v = c.has_zm ? c.zm * c.ls_o * tzm[0] : 0.0;
     } else {
-      const double An = c.An[b];
-      v = dfl * An + c.fl * An * (dapre[b] / 2. - dS / (2. * c.S));
+      const bool first = b == bf;
+      const double An = first ? anf : c.An[b];
+      v = dfl * An + c.fl * An * ((first ? dpf : (double)dapre[b]) / 2. - dS / (2. * c.S));
     }
     da[b * des] = v * c.total_volume;
   }
@@ -377,18 +414,32 @@ __device__ __forceinline__ void amp_vjp_2_body(int bx, int by, int gx, double* s
   part1 += by * wsd;
   gapre += by * wsd;
   part23 += by * wsd;
-    double s = 0;
+  // the first element's operands in flight before the sum's barriers
+  const long long bf = (long long)bx * AT + threadIdx.x;
+  double gf = 0.0, anf = 0.0, msf = 0.0, vsf = 0.0, scf = 0.0;
+  if (bf < c.B) {
+    gf = bf > 0 ? g[bf] : 0.0;
+    anf = c.An[bf];
+    msf = c.mspec[bf];
+    vsf = c.vslope[bf];
+    scf = c.sc[bf];
+  }
+  double s = 0;
   for (int i = threadIdx.x; i < np1; i += AT) s += part1[i];
   const double R1 = block_total(s, sh);
   const double k = c.fl * R1 / (2. * c.S);
   double r2 = 0, r3 = 0;
-  for (long long b = (long long)bx * AT + threadIdx.x; b < c.B; b += (long long)gx * AT) {
-    const double gm = b > 0 ? c.total_volume * g[b] : 0.0;
+  for (long long b = bf; b < c.B; b += (long long)gx * AT) {
+    const bool first = b == bf;
+    const double gb = first ? gf : (b > 0 ? g[b] : 0.0);
+    const double an = first ? anf : c.An[b], ms = first ? msf : c.mspec[b];
+    const double vsl = first ? vsf : c.vslope[b], scb = first ? scf : c.sc[b];
+    const double gm = b > 0 ? c.total_volume * gb : 0.0;
     const double gAn = c.fl * gm;
-    const double ga = c.An[b] * gAn / 2. - c.mspec[b] * k;
+    const double ga = an * gAn / 2. - ms * k;
     gapre[b] = ga;
-    r2 += c.vslope[b] * ga;
-    r3 += ga * c.sc[b];
+    r2 += vsl * ga;
+    r3 += ga * scb;
   }
   r2 = block_total(r2, sh);
   r3 = block_total(r3, sh);
@@ -424,16 +475,23 @@ __device__ __forceinline__ void amp_vjp_3_body(int bx, int by, int gx, double* s
   part23 += by * wsd;
   loc += by * wsd;
   tot += by * wsd;
-    double s = 0;
+    const long long M = c.B - 2;
+  const long long j0 = (long long)bx * ABLK + threadIdx.x;
+  // operands in flight before the sum's barriers
+  double ga[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long j = j0 + (long long)k * AT;
+    if (j < M) ga[k] = gapre[j + 2];
+  }
+  double s = 0;
   for (int i = threadIdx.x; i < np; i += AT) s += part23[2 * i + 1];
   const double R3 = block_total(s, sh);
-  const long long M = c.B - 2;
-  const long long j0 = (long long)bx * ABLK + threadIdx.x;
   double v[AE];
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
     long long j = j0 + (long long)k * AT;
-    v[k] = j < M ? gtl_at(c, gapre, j, R3) : 0.0;
+    v[k] = j < M ? ga[k] - (j + 2 == c.B - 1 ? R3 : 0.0) : 0.0;
   }
   double t = block_scan<true>(v, sh);
 #pragma unroll
@@ -464,22 +522,36 @@ __device__ __forceinline__ void amp_vjp_4_body(int bx, int by, int gx, double* s
   y += by * wsd;
   loc += by * wsd;
   tot4 += by * wsd;
-    double s = 0;
+    const long long M = c.B - 2;
+  const int nb = (int)((M + ABLK - 1) / ABLK);
+  const long long j0 = (long long)bx * ABLK + threadIdx.x;
+  // operands in flight before the sums' barriers (same expressions after)
+  double lo[AE], lvv[AE], lvn[AE], ga[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long j = j0 + (long long)k * AT;
+    if (j < M) {
+      lo[k] = loc[j];
+      lvv[k] = c.lv[j];
+      if (j + 1 < M) {
+        lvn[k] = c.lv[j + 1];
+        ga[k] = gapre[j + 2];
+      }
+    }
+  }
+  double s = 0;
   for (int i = threadIdx.x; i < np; i += AT) s += part23[2 * i + 1];
   const double R3 = block_total(s, sh);
-  const long long M = c.B - 2;
-  const int nb = (int)((M + ABLK - 1) / ABLK);
   const double carry = carry_in<true>(tot3, bx, nb, sh);
-  const long long j0 = (long long)bx * ABLK + threadIdx.x;
   double v[AE];
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
     long long j = j0 + (long long)k * AT;
     if (j < M) {
-      const double yj = y[j] = loc[j] + carry;
-      const double zj = yj * c.lv[j] / 2.;
+      const double yj = y[j] = lo[k] + carry;
+      const double zj = yj * lvv[k] / 2.;
       double zn = 0.0;
-      if (j + 1 < M) zn = (yj - gtl_at(c, gapre, j, R3)) * c.lv[j + 1] / 2.;
+      if (j + 1 < M) zn = (yj - (ga[k] - (j + 2 == c.B - 1 ? R3 : 0.0))) * lvn[k] / 2.;
       v[k] = zj + zn;
     } else {
       v[k] = 0.0;
@@ -517,15 +589,25 @@ __device__ __forceinline__ void amp_vjp_5_body(int bx, int by, int gx, double* s
   part45 += by * wsd;
     const long long M = c.B - 2;
   const int nb = (int)((M + ABLK - 1) / ABLK);
-  const double carry = carry_in<true>(tot4, bx, nb, sh);
   const long long j0 = (long long)bx * ABLK + threadIdx.x;
+  // operands in flight before the carry's barriers
+  double yv[AE], lo[AE];
+#pragma unroll
+  for (int k = 0; k < AE; ++k) {
+    const long long j = j0 + (long long)k * AT;
+    if (j < M) {
+      yv[k] = y[j];
+      lo[k] = loc[j];
+    }
+  }
+  const double carry = carry_in<true>(tot4, bx, nb, sh);
   double r4 = 0, r5 = 0;
 #pragma unroll
   for (int k = 0; k < AE; ++k) {
     long long j = j0 + (long long)k * AT;
     if (j < M) {
-      const double g0 = y[j];
-      const double g1 = loc[j] + carry;
+      const double g0 = yv[k];
+      const double g1 = lo[k] + carry;
       double s0 = g0 * c.c0[j], s1 = g1 * c.sf[j];
       if (o.dspec) {
         s0 += o.shift * o.dspec[j];
@@ -567,8 +649,12 @@ __device__ __forceinline__ void amp_vjp_6_body(int bx, int by, int gx, double* s
   part23 += by * wsd;
   part45 += by * wsd;
     double a = 0, b2 = 0, b4 = 0, b5 = 0;
+  // unrolled so that the loads of a thread issue together (order unchanged)
+#pragma unroll 4
   for (int i = threadIdx.x; i < np1; i += AT) a += part1[i];
+#pragma unroll 4
   for (int i = threadIdx.x; i < np23; i += AT) b2 += part23[2 * i];
+#pragma unroll 4
   for (int i = threadIdx.x; i < np45; i += AT) {
     b4 += part45[2 * i];
     b5 += part45[2 * i + 1];

@@ -103,9 +103,13 @@ __global__ __launch_bounds__(RED_NT) void fold_partials(const double* __restrict
   out += (long long)blockIdx.x * ostride;
   double v[W];
 #pragma unroll
-  for (int k = 0; k < W; ++k) {
-    v[k] = 0.0;
-    for (int b = threadIdx.x; b < nb; b += RED_NT) v[k] += part[k * nb + b];
+  for (int k = 0; k < W; ++k) v[k] = 0.0;
+  // the rows interleaved and 8 strides unrolled: the loads issue together,
+  // each row's sum keeps its order (bitwise the plain loops)
+#pragma unroll 8
+  for (int b = threadIdx.x; b < nb; b += RED_NT) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) v[k] += part[k * nb + b];
   }
   block_sum<W>(v, sh);
   if (threadIdx.x == 0) {
@@ -186,11 +190,13 @@ __global__ __launch_bounds__(RED_NT) void cg_update_kernel(T* __restrict__ x, T*
   double v[3] = {0.0, 0.0, 0.0};
   const long long stride = (long long)gx * RED_NT;
   for (long long i = (long long)bx * RED_NT + threadIdx.x; i < n; i += stride) {
+    // d and q are read whether or not the step applies, so that their loads
+    // need not wait for the scalars that decide it (same arithmetic)
     T xi = x[i], ri = r[i];
+    const T di = d[i], qi = q[i];
     if (ok) {
-      const T di = d[i];
       xi = xi - al * di;
-      ri = ri - al * (q[i] + shift * di);
+      ri = ri - al * (qi + shift * di);
       x[i] = xi;
       r[i] = ri;
     }
@@ -213,11 +219,12 @@ __global__ __launch_bounds__(RED_NT) void cg_finalize_kernel(const double* __res
   __shared__ double sh[3 * (RED_NT / 64)];
   sc += blockIdx.x * NFT_CG_NSCALARS;
   part += (long long)blockIdx.x * 3 * nb;
-  double v[3];
+  double v[3] = {0.0, 0.0, 0.0};
+  // rows interleaved, 8 strides unrolled (each row's order unchanged)
+#pragma unroll 8
+  for (int b = threadIdx.x; b < nb; b += RED_NT) {
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    v[k] = 0.0;
-    for (int b = threadIdx.x; b < nb; b += RED_NT) v[k] += part[k * nb + b];
+    for (int k = 0; k < 3; ++k) v[k] += part[k * nb + b];
   }
   block_sum<3>(v, sh);
   if (threadIdx.x == 0 && sc[NFT_CG_DONE] == 0.0) {
@@ -286,19 +293,31 @@ __global__ __launch_bounds__(RED_NT) void cg_dir_dd_kernel(T* __restrict__ d, co
       part += poff2;
     }
   }
+  d += (long long)blockIdx.y * vs + o;
+  r += (long long)blockIdx.y * vs + o;
+  // the first element's operands in flight before the scalars are read
+  const long long i0 = (long long)bx * RED_NT + threadIdx.x;
+  T d0 = (T)0, r0 = (T)0;
+  if (i0 < n) {
+    d0 = d[i0];
+    r0 = r[i0];
+  }
   if (sc[NFT_CG_DONE] != 0.0) {
     if (threadIdx.x == 0) part[bx] = 0.0;
     return;
   }
-  d += (long long)blockIdx.y * vs + o;
-  r += (long long)blockIdx.y * vs + o;
   double beta = sc[NFT_CG_GAMMA] / sc[NFT_CG_GPREV];
   if (!(beta > 0.0)) beta = 0.0;
   const T bt = (T)beta;
   double v[1] = {0.0};
   const long long stride = (long long)gx * RED_NT;
+  if (i0 < n) {
+    const T di = bt * d0 + r0;
+    d[i0] = di;
+    v[0] += (double)di * (double)di;
+  }
 #pragma unroll 4
-  for (long long i = (long long)bx * RED_NT + threadIdx.x; i < n; i += stride) {
+  for (long long i = i0 + stride; i < n; i += stride) {
     const T di = bt * d[i] + r[i];
     d[i] = di;
     v[0] += (double)di * (double)di;
@@ -354,11 +373,12 @@ __global__ void cg_residual_finalize(const double* __restrict__ part, int nb, do
   __shared__ double sh[3 * (RED_NT / 64)];
   sc += blockIdx.x * NFT_CG_NSCALARS;
   part += (long long)blockIdx.x * 3 * nb;
-  double v[3];
+  double v[3] = {0.0, 0.0, 0.0};
+  // rows interleaved, 8 strides unrolled (each row's order unchanged)
+#pragma unroll 8
+  for (int b = threadIdx.x; b < nb; b += RED_NT) {
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    v[k] = 0.0;
-    for (int b = threadIdx.x; b < nb; b += RED_NT) v[k] += part[k * nb + b];
+    for (int k = 0; k < 3; ++k) v[k] += part[k * nb + b];
   }
   block_sum<3>(v, sh);
   if (threadIdx.x == 0 && sc[NFT_CG_DONE] == 0.0) {
