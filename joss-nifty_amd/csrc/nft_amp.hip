@@ -92,6 +92,30 @@ __device__ __forceinline__ double block_total(double v, double* sh) {
   return t;
 }
 
+// NV block-wide sums at once (one barrier pair instead of NV): per value the
+// wave tree and the fixed-order sum over waves of block_total (bitwise)
+template <int NV>
+__device__ __forceinline__ void block_totals(double (&v)[NV], double* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int NW = AT / 64;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wsum(v[k]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) sh[k * NW + w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double t = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) t += sh[k * NW + i];
+    v[k] = t;
+  }
+  __syncthreads();
+}
+
 // inclusive block scan of AE values per thread in STRIPED layout: v[k] is
 // element k*AT + threadIdx.x of the block (so every global access of a block
 // is a coalesced 2 KB run per k).  REV scans from the end.  Wave scans by
@@ -441,11 +465,11 @@ __device__ __forceinline__ void amp_vjp_2_body(int bx, int by, int gx, double* s
     r2 += vsl * ga;
     r3 += ga * scb;
   }
-  r2 = block_total(r2, sh);
-  r3 = block_total(r3, sh);
+  double rr[2] = {r2, r3};
+  block_totals<2>(rr, sh);
   if (threadIdx.x == 0) {
-    part23[2 * bx] = r2;
-    part23[2 * bx + 1] = r3;
+    part23[2 * bx] = rr[0];
+    part23[2 * bx + 1] = rr[1];
   }
 }
 
@@ -619,11 +643,11 @@ __device__ __forceinline__ void amp_vjp_5_body(int bx, int by, int gx, double* s
       if (c.has_asp) r5 += g0 * c.p1[j];
     }
   }
-  r4 = block_total(r4, sh);
-  r5 = block_total(r5, sh);
+  double rr[2] = {r4, r5};
+  block_totals<2>(rr, sh);
   if (threadIdx.x == 0) {
-    part45[2 * bx] = r4;
-    part45[2 * bx + 1] = r5;
+    part45[2 * bx] = rr[0];
+    part45[2 * bx + 1] = rr[1];
   }
 }
 
@@ -659,10 +683,9 @@ __device__ __forceinline__ void amp_vjp_6_body(int bx, int by, int gx, double* s
     b4 += part45[2 * i];
     b5 += part45[2 * i + 1];
   }
-  const double R1 = block_total(a, sh);
-  const double R2 = block_total(b2, sh);
-  const double R4 = block_total(b4, sh);
-  const double R5 = block_total(b5, sh);
+  double rr[4] = {a, b2, b4, b5};
+  block_totals<4>(rr, sh);
+  const double R1 = rr[0], R2 = rr[1], R4 = rr[2], R5 = rr[3];
   if (threadIdx.x == 0) {
     const double sh_ = o.shift;
     o.fl[0] = c.fl * c.ls_f * R1 + (o.dfl ? sh_ * o.dfl[0] : 0.0);
