@@ -454,6 +454,53 @@ int nft_amp_vjp_batched(const nft_amp_const* c, const nft_amp_const* item_consts
                         const nft_amp_out* out, double* ws, int nrhs, int64_t lat_stride,
                         int64_t g_stride, hipStream_t stream);
 
+/* Two-phase amplitude JVP / VJP (csrc/nft_amp2.hip: two launches each; the
+ * first forms tile-local scans and per-tile sums, the second combines them
+ * over the tiles in a fixed order); the batched forms above take this path
+ * when it applies.  Key arrays are indexed fl, sl, flex, asp, zm, spec (NULL:
+ * absent key), pointing at right-hand side 0, rows lat_stride elements apart.
+ * item_mode: 0 = every RHS uses *c; 1 = item_consts is a DEVICE array of nrhs
+ * constant sets (one per RHS); 2 = item_consts is ONE device constant set
+ * shared by every RHS (read once per workgroup for up to 4 RHS).  *c gives B
+ * and the flags in every mode.  Returns NFT_AMP2_FALLBACK (nothing launched)
+ * when NFT_AMP2=0 or B is too small / large; the caller then uses the
+ * multi-kernel path.  Workspace: nrhs * nft_amp_workspace(B) bytes.
+ *
+ * nft_amp2_jvp: da[r * da_stride + b * da_elem_stride] = J_amp t_r.  With
+ * r != NULL (residual keys) the tangent t is the CG direction and is first
+ * updated in place, d = max(0, gamma/gprev) d + r (per RHS scalars in sc,
+ * unchanged when sc[NFT_CG_DONE] != 0), and part[r * pstride + tile] =
+ * shift * d.d of the amplitude keys per tile (nft_amp2_tiles tiles; tile 0
+ * includes the scalar keys; 0 for a finished RHS) -- the identity part of the
+ * data-space curvature.
+ *
+ * nft_amp2_vjp: out[key] = shift * d[key] + J_amp^T g_r (d may be NULL), or,
+ * with out2 != NULL, the CG update of the amplitude keys carried instead:
+ * out = x keys, out2 = r keys, d = direction keys, x -= alpha d,
+ * r -= alpha (J_amp^T g + shift d) with alpha = sc[GAMMA] / sc[CURV] and the
+ * guards of nft_cg_update_batched; then the iteration's finalize
+ * (nft_cg_finalize_batched semantics, x.b = 0) over the r.r / x.r partials of
+ * the amplitude keys (part: 2 * nft_amp2_tiles per RHS, pstride apart) and of
+ * the grid segment (gpart: ngp r.r partials at gpart[r * gp_stride + t], the
+ * x.r ones gp_row after them), folded in a fixed order. */
+#define NFT_AMP2_FALLBACK 1
+int nft_amp2_enabled(void);
+/* on = 0 / 1: force the two-phase path off / on for later calls (A/B and
+ * tests); on < 0: back to the environment (NFT_AMP2) */
+void nft_amp2_set_enabled(int on);
+int nft_amp2_tiles(int64_t B, int nrhs, int item_mode);
+int nft_amp2_jvp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, double* const* t,
+                 const double* const* r, int64_t lat_stride, double* da, int64_t da_stride, int64_t da_elem_stride,
+                 double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift,
+                 hipStream_t stream);
+int nft_amp2_vjp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, const double* g,
+                 int64_t g_stride,
+                 double* const* out, double* const* out2, const double* const* d, int64_t lat_stride, double shift,
+                 double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
+                 int64_t gp_stride, int64_t gp_row, int ngp, hipStream_t stream);
+
+
+
 /* Amplitude model (device pointers, fp64; M = B - 2): the operator chain of
  * src/library/correlated_fields_simple.py:85-127 (_Normalization, _SlopeRemover,
  * _TwoLogIntegrations, the LognormalTransform / NormalTransform scalings) with

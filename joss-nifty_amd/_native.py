@@ -73,6 +73,11 @@ SIGNATURES = {
     "nft_cg_update_seg2_batched": (_i, [_p, _p, _p, _p, _i64, _i, _i64, _i64, _i, _i64, _i, _i, _d, _p, _p, _i, _p]),
     "nft_cg_direction_dd2_batched": (_i, [_p, _p, _i64, _i64, _i64, _i64, _i, _i, _p, _d, _p, _i64, _i64, _p]),
     "nft_cg_finalize_batched": (_i, [_p, _i, _i, _p, _p]),
+    "nft_amp2_enabled": (_i, []),
+    "nft_amp2_set_enabled": (None, [_i]),
+    "nft_amp2_tiles": (_i, [_i64, _i, _i]),
+    "nft_amp2_jvp": (_i, [_p, _p, _i, _p, _p, _i64, _p, _i64, _i64, _p, _i, _p, _p, _i64, _d, _p]),
+    "nft_amp2_vjp": (_i, [_p, _p, _i, _p, _i64, _p, _p, _p, _i64, _d, _p, _i, _p, _p, _i64, _p, _i64, _i64, _i, _p]),
     "nft_amp_forward_buf": (_i64, [_i64]),
     "nft_amp_forward_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _p, _i64, _p, _i64, _p, _p, _p]),
 }
@@ -124,6 +129,7 @@ class AmpOut(ctypes.Structure):
 
 CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD, CG_DONE, CG_ITER, CG_AUTO = range(11)
 CG_NSCALARS = 16
+AMP2_FALLBACK = 1  # NFT_AMP2_FALLBACK
 
 _lib = None
 _load_error = None

@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "nft_api_internal.hpp"
+#include "../../include/nifty_amd.h"
 
 namespace nft {
 
@@ -1440,6 +1441,14 @@ int nft_amp_jvp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
   const int nbB = nblk(B, ABLK);
   double* part = tot2 + nbM + 1;
   const int n7 = nblk(B, AT) < 1024 ? nblk(B, AT) : 1024;
+  {
+    // two-phase tiles (nft_amp2.hip) where they apply
+    double* t[6] = {const_cast<double*>(tfl), const_cast<double*>(tsl), const_cast<double*>(tflex),
+                    const_cast<double*>(tasp), const_cast<double*>(tzm), const_cast<double*>(tspec)};
+    const int st = nft_amp2_jvp(cst, dcs, dcs ? 1 : 0, t, nullptr, ls, da, vs, da_elem_stride, ws, nrhs, nullptr, nullptr, 0, 0.0,
+                                s);
+    if (st != NFT_AMP2_FALLBACK) return st;
+  }
   if (fused_enabled() && M >= 1) {
     const long long des = da_elem_stride > 0 ? da_elem_stride : 1;
     int st = jvp_fused_try<4>(c, dcs, nrhs, tfl, tsl, tflex, tasp, tzm, tspec, da, ws, ls, vs, wsd, des, s);
@@ -1486,6 +1495,13 @@ int nft_amp_vjp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
   double* tot3 = part23 + 2 * nr + 2;
   double* tot4 = tot3 + nbM + 1;
   double* part45 = tot4 + nbM + 1;
+  {
+    double* out[6] = {o.fl, o.sl, o.flex, o.asp, o.zm, o.spec};
+    const double* d[6] = {o.dfl, o.dsl, o.dflex, o.dasp, o.dzm, o.dspec};
+    const int st = nft_amp2_vjp(cst, dcs, dcs ? 1 : 0, g, vs, out, nullptr, d, ls, o.shift, ws, nrhs, nullptr, nullptr, 0,
+                                nullptr, 0, 0, 0, s);
+    if (st != NFT_AMP2_FALLBACK) return st;
+  }
   if (fused_enabled() && M >= 1) {
     int st = vjp_fused_try<4>(c, dcs, nrhs, o, g, ws, ls, vs, wsd, s);
     if (st == NFT_FALLBACK) st = vjp_fused_try<8>(c, dcs, nrhs, o, g, ws, ls, vs, wsd, s);

@@ -320,21 +320,48 @@ class _AmplitudeModel:
             return D[0, off[key]:].data_ptr()
         return at
 
+    def _keys6(self):
+        return (self.k_fl, self.k_sl, self.k_flex, self.k_asp, self.k_zm, self.k_spec)
+
+    def _key_ptrs(self, T, off):
+        """ctypes array of the 6 key pointers (fl, sl, flex, asp, zm, spec) of
+        packed row 0 of T (NULL for absent keys), or NULL if T is None"""
+        import ctypes
+        if T is None:
+            return None
+        return (ctypes.c_void_p * 6)(*[T[0, off[kk]:].data_ptr() if kk in off else None for kk in self._keys6()])
+
+    @staticmethod
+    def _item_mode(const, item_consts):
+        """(host AmpConst, item pointer, nft_amp2 item_mode): an AmpLin
+        without per-item constants is ONE device constant set shared by every
+        right-hand side (mode 2)"""
+        if isinstance(const, AmpLin):
+            if item_consts is None:
+                return const.host, const.items(1), 2
+            return const.host, item_consts, 1
+        return const, item_consts, (1 if item_consts else 0)
+
     def native_jvp_batched(self, const, D, off, da, interleave=False, item_consts=None):
         """da[b] = J_amp D[b] for the k rows of a packed batch D (k, size);
         interleave: da is (B, k), bin-major (one contiguous run per bin)."""
         import ctypes
-        at = self._ptrs(D, off)
         k, size = D.shape
-        if isinstance(const, AmpLin):
-            if item_consts is None:
-                item_consts = const.items(k)
-            const = const.host
         lib = _native.load()
         ws = _native.workspace(k * lib.nft_amp_workspace(self.B), D.device, "amp")
         P = ctypes.c_void_p
+        host, ic, mode = self._item_mode(const, item_consts)
+        st = lib.nft_amp2_jvp(ctypes.byref(host), P(ic), mode, self._key_ptrs(D, off), None, size, P(da.data_ptr()),
+                              1 if interleave else self.B, k if interleave else 1, P(ws.data_ptr()), k, None, None,
+                              0, 0.0, _native.stream_ptr())
+        if st != _native.AMP2_FALLBACK:
+            _native._check(st)
+            return da
+        at = self._ptrs(D, off)
+        if mode == 2:
+            ic = const.items(k)
         _native._check(lib.nft_amp_jvp_batched(
-            ctypes.byref(const), P(item_consts), P(at(self.k_fl)), P(at(self.k_sl)), P(at(self.k_flex)), P(at(self.k_asp)),
+            ctypes.byref(host), P(ic), P(at(self.k_fl)), P(at(self.k_sl)), P(at(self.k_flex)), P(at(self.k_asp)),
             P(at(self.k_zm)), P(at(self.k_spec)), P(da.data_ptr()), P(ws.data_ptr()), k, size,
             1 if interleave else self.B, k if interleave else 1, _native.stream_ptr()))
         return da
@@ -343,12 +370,19 @@ class _AmplitudeModel:
         """Q[b] amplitude keys = shift * D[b] + J_amp^T g[b]."""
         import ctypes
         k, size = Q.shape
-        if isinstance(const, AmpLin):
-            if item_consts is None:
-                item_consts = const.items(k)
-            const = const.host
         lib = _native.load()
         ws = _native.workspace(k * lib.nft_amp_workspace(self.B), Q.device, "amp")
+        P = ctypes.c_void_p
+        host, ic, mode = self._item_mode(const, item_consts)
+        dk = self._key_ptrs(D, off) if (D is not None and shift != 0.0) else None
+        st = lib.nft_amp2_vjp(ctypes.byref(host), P(ic), mode, P(g.data_ptr()), self.B, self._key_ptrs(Q, off), None,
+                              dk, size, float(shift), P(ws.data_ptr()), k, None, None, 0, None, 0, 0, 0,
+                              _native.stream_ptr())
+        if st != _native.AMP2_FALLBACK:
+            _native._check(st)
+            return Q
+        if mode == 2:
+            ic = const.items(k)
         atq = self._ptrs(Q, off)
         atd = self._ptrs(D, off) if (D is not None and shift != 0.0) else (lambda key: None)
         o = _native.AmpOut()
@@ -357,11 +391,49 @@ class _AmplitudeModel:
             setattr(o, short, atq(key))
             setattr(o, "d" + short, atd(key))
         o.shift = float(shift)
-        _native._check(lib.nft_amp_vjp_batched(ctypes.byref(const), ctypes.c_void_p(item_consts),
+        _native._check(lib.nft_amp_vjp_batched(ctypes.byref(host), ctypes.c_void_p(ic),
                                                ctypes.c_void_p(g.data_ptr()), ctypes.byref(o),
                                                ctypes.c_void_p(ws.data_ptr()), k, size, self.B,
                                                _native.stream_ptr()))
         return Q
+
+    # ----- the amplitude keys' CG work carried by the two-phase kernels
+    def amp2_tiles(self, const, k):
+        """tile count of the two-phase JVP / VJP for k RHS (0: not applicable)"""
+        _, _, mode = self._item_mode(const, None)
+        return int(_native.load().nft_amp2_tiles(self.B, k, mode))
+
+    def native_jvp_dir(self, const, D, R, off, da, SC, part, pstride, shift):
+        """d = max(0, gamma/gprev) d + r on the amplitude keys of the k rows of
+        D (in place), d.d partials per tile (times shift) into part, and
+        da (B, k) = J_amp d, bin-major (nft_amp2_jvp with residual keys)."""
+        import ctypes
+        k, size = D.shape
+        lib = _native.load()
+        ws = _native.workspace(k * lib.nft_amp_workspace(self.B), D.device, "amp")
+        P = ctypes.c_void_p
+        host, ic, mode = self._item_mode(const, None)
+        _native._check(lib.nft_amp2_jvp(ctypes.byref(host), P(ic), mode, self._key_ptrs(D, off),
+                                        self._key_ptrs(R, off), size, P(da.data_ptr()), 1, k, P(ws.data_ptr()), k,
+                                        P(SC.data_ptr()), P(part.data_ptr()), int(pstride), float(shift),
+                                        _native.stream_ptr()))
+        return da
+
+    def native_vjp_cg(self, const, g, X, R, D, off, SC, part, pstride, gpart, gp_stride, gp_row, ngp, shift):
+        """the amplitude keys' CG update x -= alpha d, r -= alpha (J_amp^T g +
+        shift d) and the iteration's finalize over their r.r / x.r partials
+        and the grid segment's (nft_amp2_vjp with out2)"""
+        import ctypes
+        k, size = X.shape
+        lib = _native.load()
+        ws = _native.workspace(k * lib.nft_amp_workspace(self.B), X.device, "amp")
+        P = ctypes.c_void_p
+        host, ic, mode = self._item_mode(const, None)
+        _native._check(lib.nft_amp2_vjp(ctypes.byref(host), P(ic), mode, P(g.data_ptr()), self.B,
+                                        self._key_ptrs(X, off), self._key_ptrs(R, off), self._key_ptrs(D, off), size,
+                                        float(shift), P(ws.data_ptr()), k, P(SC.data_ptr()), P(part.data_ptr()),
+                                        int(pstride), P(gpart.data_ptr()), int(gp_stride), int(gp_row), int(ngp),
+                                        _native.stream_ptr()))
 
     def native_jvp(self, const, t, da):
         if isinstance(const, AmpLin):
@@ -618,6 +690,30 @@ class CFJacobian(LinearOperator):
         m.amp.native_jvp_batched(self._const(), D, dict(zip(self.layout.keys, self.layout.offsets)), da,
                                  interleave=True)
         return da
+
+    def amp2_tiles(self, k):
+        """tile count of the two-phase amplitude kernels (carried direction /
+        update of the amplitude keys), 0 if they do not apply"""
+        return self._m.amp.amp2_tiles(self._const(), k)
+
+    def mv_amp_jvp_dir(self, D, R, SC, part, pstride, shift):
+        """the amplitude keys' CG direction update (in place, d.d partials per
+        tile) and dA (B, k) of the updated D, bin-major interleaved"""
+        m = self._m
+        k = D.shape[0]
+        da = self._mv_bufs(k)["da"]
+        return m.amp.native_jvp_dir(self._const(), D, R, dict(zip(self.layout.keys, self.layout.offsets)), da, SC,
+                                    part, pstride, shift)
+
+    def mv_amp_vjp_cg(self, X, R, D, w, SC, part, pstride, gpart, gp_stride, gp_row, ngp, shift):
+        """bin sums of w, then the amplitude keys' CG update with J_amp^T and
+        the iteration's finalize (no q is stored)"""
+        m = self._m
+        k = X.shape[0]
+        ga = self._mv_bufs(k)["ga"]
+        m.jbins.scatter_from(self.mv_fold(w), ga, k)
+        m.amp.native_vjp_cg(self._const(), ga, X, R, D, dict(zip(self.layout.keys, self.layout.offsets)), SC, part,
+                            pstride, gpart, gp_stride, gp_row, ngp, shift)
 
     def cg_blocks(self, k):
         """partial blocks per item of the CG-carrying adjoint epilogue at

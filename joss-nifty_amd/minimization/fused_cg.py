@@ -495,6 +495,10 @@ _CARRY_DIR = os.environ.get("NFT_CG_CARRY_DIR", "1") != "0"
 # the amplitude keys before and after the grid segment in one launch each for
 # the direction and the update (nft_cg_*2_batched; NFT_CG_SEG2=0: two each)
 _SEG2 = os.environ.get("NFT_CG_SEG2", "1") != "0"
+# the amplitude keys' direction with the JVP and their update + the finalize
+# with the VJP in the two-phase amplitude kernels (NFT_CG_AMP2=0: the
+# separate direction / update / finalize launches)
+_AMP2 = os.environ.get("NFT_CG_AMP2", "1") != "0"
 
 
 class _CarryIteration:
@@ -517,6 +521,22 @@ class _CarryIteration:
         g0, g1 = core.grid_segment()
         self.g0 = g0
         tiles = core.cg_blocks(k)
+        # the amplitude keys' direction / update carried by the two-phase
+        # amplitude kernels (nft_amp2_*): partials [amplitude tiles][prologue
+        # blocks] for d.d, [amplitude tiles] for r.r / x.r (each tile also
+        # folds a slice of the grid epilogue's partials, GP)
+        self.na = int(core.amp2_tiles(k)) if (_AMP2 and hasattr(core, "amp2_tiles")) else 0
+        pb = core.dir_blocks(k) if (_CARRY_DIR and hasattr(core, "dir_blocks")) else 0
+        if self.na and pb:
+            dev = core.device
+            self.tiles = tiles
+            self.nbd = self.na + pb
+            self.pro_blk0 = self.na
+            self.PQ = torch.empty((k, self.nbd + nq), dtype=torch.float64, device=dev)
+            self.UP = torch.empty((k, 2 * self.na), dtype=torch.float64, device=dev)
+            self.GP = torch.empty((k, 3 * tiles), dtype=torch.float64, device=dev)
+            return
+        self.na = 0
         nb0 = int(lib.nft_cg_dd_blocks(g0)) if g0 > 0 else 0
         nb1 = int(lib.nft_cg_dd_blocks(n - g1)) if n > g1 else 0
         self.amp = [(o, e - o, blk) for (o, e), blk in (((0, g0), 0), ((g1, n), nb0 + tiles)) if e > o]
@@ -541,7 +561,27 @@ class _CarryIteration:
     def supported(core, k):
         return _CARRY and hasattr(core, "cg_blocks") and core.cg_blocks(k) > 0
 
+    def _call_amp2(self, X, Rr, D, Q, SC):
+        core, lib = self.core, self.lib
+        n, k, g0 = self.n, self.k, self.g0
+        pstride = self.nbd + self.nq
+        da = core.mv_amp_jvp_dir(D, Rr, SC, self.PQ, pstride, self.shift)
+        pro_dir = dict(r=Rr[0, g0:], sc=SC, part=self.PQ, pstride=pstride, shift=self.shift, blk0=self.pro_blk0)
+
+        def fold():
+            _native._check(lib.nft_fold_partials(_native.ptr(self.PQ), pstride, k,
+                                                 ctypes.c_void_p(SC.data_ptr() + _native.CG_CURV * 8),
+                                                 _native.CG_NSCALARS, _native.stream_ptr()))
+        cg = dict(x=X[0, g0:], r=Rr[0, g0:], d=D[0, g0:], sc=SC, part=self.GP, stride=n, shift=self.shift,
+                  nbtot=self.tiles, blk0=0)
+        w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbd:], after_w=fold, cg=cg,
+                         pro_dir=pro_dir)
+        core.mv_amp_vjp_cg(X, Rr, D, w, SC, self.UP, 2 * self.na, self.GP, 3 * self.tiles, self.tiles, self.tiles,
+                           self.shift)
+
     def __call__(self, X, Rr, D, Q, SC):
+        if self.na:
+            return self._call_amp2(X, Rr, D, Q, SC)
         core, lib = self.core, self.lib
         P = _native.ptr
         s_ = _native.stream_ptr()
