@@ -48,10 +48,32 @@ def parse():
     p.add_argument("--cpu-pairs", type=int, default=1, help="mirrored pairs in the timed CPU oracle draw")
     p.add_argument("--no-demo", action="store_true", help="skip the demo-controller line")
     p.add_argument("--deterministic-allreduce", action="store_true")
+    p.add_argument("--backend", choices=["nccl", "gloo"], default=None,
+                   help="process-group backend (default: nccl = RCCL on a GPU, gloo on CPU)")
     return p.parse_args()
 
 
-def setup_dist():
+def launch_workers(n):
+    """`--gpus N` without a launcher: start N ranks of this script (one per
+    GPU, LOCAL_RANK = RANK) as child processes -- this process never touches
+    the GPU -- forward rank 0's line and exit with the worst status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def setup_dist(backend=None):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     lrank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -59,7 +81,7 @@ def setup_dist():
         torch.cuda.set_device(lrank % torch.cuda.device_count())
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend or ("nccl" if torch.cuda.is_available() else "gloo"))
     return ws, rank, lrank
 
 
@@ -403,11 +425,37 @@ def demo_step(ift, lh, pos, nsamp, comm):
             "controllers": "sampling AbsDelta(0.05, 100); NewtonCG(AbsDelta(0.5, convergence_level=2, 15))"}
 
 
+class _TimedComm:
+    """the communicator with its collectives timed (device-synchronised
+    before and after each): the KL-mean all-reduce of one extra, untimed step"""
+
+    def __init__(self, comm):
+        self._c = comm
+        self.calls = []
+
+    def __getattr__(self, name):
+        return getattr(self._c, name)
+
+    def allreduce_tensor_(self, t):
+        torch.cuda.synchronize() if t.is_cuda else None
+        t0 = time.perf_counter()
+        self._c.allreduce_tensor_(t)
+        torch.cuda.synchronize() if t.is_cuda else None
+        self.calls.append((time.perf_counter() - t0, t.numel() * t.element_size()))
+        return t
+
+
 def main():
     args = parse()
-    ws, rank, lrank = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_workers(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE is {os.environ.get('WORLD_SIZE')}",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    ws, rank, lrank = setup_dist(args.backend)
     import nifty_amd as ift
-    ift.config.set_device(f"cuda:{lrank}" if torch.cuda.is_available() else "cpu")
+    ift.config.set_device(f"cuda:{lrank % torch.cuda.device_count()}" if torch.cuda.is_available() else "cpu")
     if args.deterministic_allreduce:
         ift.utilities.DETERMINISTIC_ALLREDUCE = True
     comm = ift.TorchComm() if ws > 1 else None
@@ -438,12 +486,38 @@ def main():
     barrier_sync(ws)
     el = time.perf_counter() - t0
     iters = ift.ConjugateGradient.iterations_total - it0
+    dist_info = None
     if ws > 1:
         import torch.distributed as dist
-        t = torch.tensor([el, float(iters)], dtype=torch.float64, device="cuda")
+        dev = "cuda" if torch.cuda.is_available() and dist.get_backend() != "gloo" else "cpu"
+        t = torch.tensor([el, float(iters)], dtype=torch.float64, device=dev)
         dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
         el, iters = float(t[0]), float(t[1])
+        # every rank drew its share and holds the same KL: a rank that
+        # disagrees fails the run (non-zero exit on every rank)
+        per_rank = [int(c) for c in comm.allgather(kl.samples.n_local_samples)]
+        vals = comm.allgather(float(kl.value))
+        # the KL-mean all-reduce of one extra, untimed step, timed on its own
+        tc = _TimedComm(comm)
+        sl = ift.draw_samples(pos, H, mini, nsamp, True, comm=tc)
+        ift.SampledKLEnergyClass(sl, H, [], None, True)
+        ar = tc.calls
+        ar_ms = comm.allgather(sum(c[0] for c in ar) * 1e3)
+        dist_info = {"backend": dist.get_backend(), "samples_per_rank": per_rank,
+                     "kl_allreduce": {"calls": len(ar), "bytes": sum(c[1] for c in ar),
+                                      "ms_max_over_ranks": round(max(ar_ms), 4),
+                                      "timing": "one extra untimed step, device-synchronised around each call"}}
+        bad = []
+        if sum(per_rank) != 2 * nsamp:
+            bad.append(f"samples per rank {per_rank} do not add up to {2 * nsamp}")
+        if any(v != vals[0] for v in vals):
+            bad.append(f"KL values differ over ranks: {vals}")
+        if bad:
+            if rank == 0:
+                print("bench.py: rank mismatch: " + "; ".join(bad), file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            sys.exit(3)
     samples = 2 * nsamp * args.steps
     sps = samples / el
     cgps = iters / el
@@ -476,7 +550,7 @@ def main():
                            "global_batch": samples // args.steps, "parallelism": f"sample-dp{ws}"},
                 "cg_iter_per_s": round(cgps, 3), "cg_iters": int(iters),
                 "roofline": roof, "cpu_baseline": cpu, "demo_controllers": demo,
-                "cg_iteration": cgit, "kernels": kp}
+                "cg_iteration": cgit, "kernels": kp, "distributed": dist_info}
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist

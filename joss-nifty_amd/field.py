@@ -81,6 +81,14 @@ class Field:
         arr = gen(dtype=dtype, shape=domain.shape, **kwargs)
         return Field(domain, arr)
 
+    def __reduce__(self):
+        # host values on the wire, the receiving process's device on arrival
+        # (a MAP mean broadcast to ranks that each own a GPU)
+        return (Field.from_raw, (self._domain, self.val_np()))
+
+    def __deepcopy__(self, memo):
+        return Field(self._domain, self._val.clone())
+
     # ------------------------------------------------------------ properties
     @property
     def val(self):

@@ -96,6 +96,22 @@ def load_field(fname, domain=None):
     return MultiField.from_dict({k: Field.from_raw(md[k], arrs[k]) for k in meta["keys"]}, md), meta["extra"]
 
 
+def load_domain(fname, domain=None):
+    """the domain of the field stored in `fname` from its descriptor alone
+    (no array is read); keys of `domain` take that domain, as in load_field"""
+    with np.load(fname, allow_pickle=False) as z:
+        meta = json.loads(bytes(z["__meta__"]).decode())
+    if meta["kind"] == "Field":
+        return DomainTuple.make(domain if domain is not None else _dom_from_desc(meta["domains"][""]))
+    doms = {}
+    for k in meta["keys"]:
+        if isinstance(domain, MultiDomain) and k in domain.keys():
+            doms[k] = domain[k]
+        else:
+            doms[k] = _dom_from_desc(meta["domains"][k])
+    return MultiDomain.make(doms)
+
+
 def save_json(fname, obj):
     tmp = fname + ".tmp"
     with open(tmp, "w") as f:

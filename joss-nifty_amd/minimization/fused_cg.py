@@ -144,8 +144,10 @@ def _count_only(ctl):
 
 
 def _count_silent(ctl):
-    """a count-only controller that logs nothing: its checks read no energy"""
-    return _count_only(ctl) and ctl._name is None and ctl._iteration_limit is not None
+    """a count-only controller that logs nothing and keeps no energy history:
+    its checks read no energy"""
+    return (_count_only(ctl) and ctl._name is None and ctl._iteration_limit is not None
+            and getattr(ctl, "_history", None) is None)
 
 
 class _CountOnlyState:

@@ -697,7 +697,9 @@ def kl_batch(hamiltonian, positions):
     covariance) or PoissonianEnergy applied to a supported model chain.
 
     Returns ([value_i], [gradient_i MultiField])."""
-    if not ENABLED or len(positions) < 2:
+    # one position too: per row the batched pass does not depend on the
+    # batch, so a rank holding one sample computes the 1-rank run's terms
+    if not ENABLED or len(positions) < 1:
         return None
     parsed = _likelihood(hamiltonian, positions)
     if parsed is None:

@@ -63,6 +63,7 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
         sseq = reduce(lambda a, b: a + b, [[ss] * 2 for ss in sseq]) if n_samples > 0 else []
     local_samples, local_neg = [], []
     utilities.check_MPI_synced_random_state(comm)
+    utilities.check_MPI_equality(sseq, comm)
     y = None
     ntask, rank, _ = get_MPI_params_from_comm(comm)
     lo, hi = shareRange(len(sseq), ntask, rank)
@@ -92,7 +93,10 @@ def draw_samples(position, H, minimizer, n_samples, mirror_samples, napprox=0, w
         prepared = dict(zip(drawing, sols))
     y = None
     gb = None
-    if geometric and hi - lo > 1 and isinstance(sam_position, MultiField):
+    # a rank holding one sample refines it as a batch of one: per sample the
+    # batched refinement's arithmetic does not depend on the batch, so a
+    # sharded run draws the 1-rank run's samples bit for bit
+    if geometric and hi - lo >= 1 and isinstance(sam_position, MultiField):
         from . import geovi_batch
         gb = geovi_batch.plan(minimizer, f_lh, None, sam_position)
     if gb is not None:

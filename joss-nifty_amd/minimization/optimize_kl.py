@@ -29,7 +29,8 @@ from ..multi_field import MultiField
 from ..operators.energy_operators import StandardHamiltonian
 from ..operators.operator import Operator
 from ..sugar import from_random, full, makeDomain
-from ..utilities import get_MPI_params_from_comm, myassert
+from ..utilities import (check_MPI_equality, check_MPI_synced_random_state, get_MPI_params_from_comm,
+                         myassert)
 from . import checkpoint
 from .descent_minimizers import DescentMinimizer
 from .energy_adapter import EnergyAdapter
@@ -138,8 +139,14 @@ def optimize_kl(likelihood_energy, total_iterations, n_samples, kl_minimizer, sa
         if dry_run:
             logger.info(f"Iteration {it} checked")
             continue
-        sl = None
         cm = comm(it)
+        # every rank runs the same iteration (optimize_kl.py:342-345); the
+        # mean by a device checksum of each key, one allgather of tokens
+        check_MPI_synced_random_state(cm)
+        check_MPI_equality(lh.domain, cm)
+        check_MPI_equality(mean.domain, cm)
+        check_MPI_equality(mean, cm, hash_=True)
+        sl = None
         if n_samples(it) == 0:
             e = EnergyAdapter(mean_iter, ham, constants=constants(it), want_metric=True)
             if cm is None:

@@ -188,9 +188,18 @@ class SampleList:
     def local_iterator(self):
         return iter(self._s)
 
+    def _template(self, op):
+        """a zero object of op's result layout, for a rank without samples"""
+        def template():
+            from ..sugar import full
+            z = full(self._domain, 0.)
+            return 0 * (op(z) if op is not None else z)
+        return template
+
     def average(self, op=None):
         res = [op(s) if op is not None else s for s in self._s]
-        return utilities.allreduce_sum(res, self._comm, counts=self._counts) / self.n_samples
+        return utilities.allreduce_sum(res, self._comm, counts=self._counts,
+                                       template=self._template(op)) / self.n_samples
 
     def sample_stat(self, op=None):
         mean = self.average(op)
@@ -205,9 +214,17 @@ class SampleList:
 
     @classmethod
     def load(cls, file_name_base, comm=None, domain=None):
-        from .checkpoint import load_field
+        """``domain``: the samples' domain; a rank whose share of the files is
+        empty (e.g. the one sample of a MAP iteration on two ranks) takes it
+        from sample 0's file, so that every rank joins the constructor's
+        collective"""
+        from .checkpoint import load_domain, load_field
         _barrier(comm)
-        return cls([load_field(f, domain)[0] for f in _local_sample_files(file_name_base, comm)], comm=comm)
+        files = _local_sample_files(file_name_base, comm)
+        samples = [load_field(f, domain)[0] for f in files]
+        if domain is None and not samples:
+            domain = load_domain(f"{file_name_base}.0.npz")
+        return cls(samples, comm=comm, domain=domain)
 
 
 def _barrier(comm):

@@ -17,6 +17,7 @@ continues from the generator: results are bit-identical either way; a wrong
 prediction only costs background CPU time.
 """
 import threading
+import weakref
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -196,10 +197,21 @@ last_script = None
 # pinned tensor up by address).  The served array is a view of that memory:
 # the same values, only where they live differs.
 _PIN_BYTES = 1 << 20
-_pinned = {}
+_PIN_CAP = 1 << 31          # page-locked bytes held for served draws at most
+_pinned = {}                # address -> (pinned tensor, weakref of the served array)
+_pinned_bytes = 0
+
+
+def _unpin(key):
+    global _pinned_bytes
+    ent = _pinned.pop(key, None)
+    if ent is not None:
+        _pinned_bytes -= ent[0].numel() * ent[0].element_size()
+    return ent
 
 
 def _pin(a):
+    global _pinned_bytes
     if not isinstance(a, np.ndarray) or a.nbytes < _PIN_BYTES or a.dtype.kind not in "fc":
         return a
     try:
@@ -211,19 +223,29 @@ def _pin(a):
         return a
     v = t.numpy()
     with _lock:
-        _pinned[v.ctypes.data] = t
-        while len(_pinned) > 64:
-            _pinned.pop(next(iter(_pinned)))
+        _unpin(v.ctypes.data)
+        _pinned[v.ctypes.data] = (t, weakref.ref(v))
+        _pinned_bytes += t.numel() * t.element_size()
+        # draws converted before their upload (fp32 casts, complex assembly,
+        # arithmetic) never come back: the oldest go first, by count and bytes
+        while _pinned and (len(_pinned) > 64 or _pinned_bytes > _PIN_CAP):
+            _unpin(next(iter(_pinned)))
     return v
 
 
 def take_pinned(arr):
-    """the page-locked tensor behind a served prefetched draw, or None"""
+    """the page-locked tensor behind a served prefetched draw, or None: only
+    for the served array object itself (a view of it -- transposed, sliced --
+    shares its address but not its layout)"""
     if not _pinned or not isinstance(arr, np.ndarray):
         return None
     with _lock:
-        t = _pinned.pop(arr.ctypes.data, None)
-    if t is None or tuple(t.shape) != arr.shape or t.numpy().dtype != arr.dtype:
+        ent = _pinned.get(arr.ctypes.data)
+        if ent is None or ent[1]() is not arr:
+            return None
+        _unpin(arr.ctypes.data)
+    t = ent[0]
+    if tuple(t.shape) != arr.shape or t.numpy().dtype != arr.dtype or not arr.flags.c_contiguous:
         return None
     return t
 

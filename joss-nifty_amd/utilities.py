@@ -67,24 +67,50 @@ class TorchComm:
     def backend(self):
         return self._dist.get_backend(self._group)
 
+    def _staged(self, t):
+        """gloo moves host memory only: a device tensor goes through a host
+        copy (RCCL takes it in place)"""
+        return t.is_cuda and self.backend == "gloo"
+
     def allreduce_tensor_(self, t):
         """In-place SUM all-reduce of a tensor (one RCCL call on GPU)."""
-        self._dist.all_reduce(t, group=self._group)
+        if self._staged(t):
+            h = t.cpu()
+            self._dist.all_reduce(h, group=self._group)
+            t.copy_(h)
+        else:
+            self._dist.all_reduce(t, group=self._group)
         return t
 
     def _global(self, r):
         return r if self._group is None else self._dist.get_global_rank(self._group, r)
 
     def send_tensor(self, t, dest):
-        self._dist.send(t.contiguous(), self._global(dest), group=self._group)
+        t = t.cpu() if self._staged(t) else t.contiguous()
+        self._dist.send(t, self._global(dest), group=self._group)
 
     def recv_tensor_(self, t, source):
-        self._dist.recv(t, self._global(source), group=self._group)
+        if self._staged(t):
+            h = torch_empty_like_host(t)
+            self._dist.recv(h, self._global(source), group=self._group)
+            t.copy_(h)
+        else:
+            self._dist.recv(t, self._global(source), group=self._group)
         return t
 
     def broadcast_tensor_(self, t, root):
-        self._dist.broadcast(t, self._global(root), group=self._group)
+        if self._staged(t):
+            h = t.cpu()
+            self._dist.broadcast(h, self._global(root), group=self._group)
+            t.copy_(h)
+        else:
+            self._dist.broadcast(t, self._global(root), group=self._group)
         return t
+
+
+def torch_empty_like_host(t):
+    import torch
+    return torch.empty(t.shape, dtype=t.dtype)
 
 
 def pairwise_sum(vals):
@@ -137,23 +163,38 @@ def _flatten(obj):
 
 
 class _Packed:
-    """one object (Field / MultiField / scalar / tuple of them) as ONE flat
-    fp64 buffer on the collective's device, and back"""
+    """one object (Field / MultiField / scalar / tuple of them) as flat
+    buffers on the collective's device, ONE per element dtype (usually just
+    fp64): every element is summed in its own dtype, as the serial pairwise
+    sum does, and complex tensors travel as (re, im) pairs of their real
+    dtype"""
 
     def __init__(self, obj, comm):
         self.ts, self.rebuild = _flatten(obj)
         self.dev = _comm_device(comm, self.ts[0].device)
-        self.buf = torch.cat([t.reshape(-1).to(self.dev, torch.float64) for t in self.ts])
+        groups = {}
+        for i, t in enumerate(self.ts):
+            r = torch.view_as_real(t) if t.is_complex() else t
+            if not r.is_floating_point():
+                r = r.to(torch.float64)
+            groups.setdefault(r.dtype, []).append((i, r))
+        self.dtypes = sorted(groups, key=str)
+        self.layout = [groups[d] for d in self.dtypes]
+        self.bufs = [torch.cat([r.reshape(-1).to(self.dev) for _, r in grp]) for grp in self.layout]
 
     def zeros(self):
-        return torch.zeros_like(self.buf)
+        return [torch.zeros_like(b) for b in self.bufs]
 
-    def unpack(self, buf):
-        out, off = [], 0
-        for t in self.ts:
-            n = t.numel()
-            out.append(buf[off:off + n].reshape(t.shape).to(t.device, t.dtype))
-            off += n
+    def unpack(self, bufs):
+        out = [None] * len(self.ts)
+        for grp, buf in zip(self.layout, bufs):
+            off = 0
+            for i, r in grp:
+                n = r.numel()
+                v = buf[off:off + n].reshape(r.shape).to(self.ts[i].device)
+                t = self.ts[i]
+                out[i] = torch.view_as_complex(v.contiguous()) if t.is_complex() else v.to(t.dtype)
+                off += n
         return self.rebuild(out)
 
 
@@ -199,14 +240,15 @@ def allreduce_sum(obj, comm, deterministic=None, counts=None, template=None):
         return _tree_sum(vals, comm, counts, template)
     if vals:
         pk = _Packed(pairwise_sum(vals), comm)
-        buf = pk.buf
+        bufs = pk.bufs
     else:
         if template is None:
             raise RuntimeError("a rank without items needs a template of the result layout")
         pk = _Packed(template(), comm)
-        buf = pk.zeros()
-    comm.allreduce_tensor_(buf)
-    return pk.unpack(buf)
+        bufs = pk.zeros()
+    for b in bufs:
+        comm.allreduce_tensor_(b)
+    return pk.unpack(bufs)
 
 
 def _tree_sum(vals, comm, counts, template):
@@ -221,36 +263,85 @@ def _tree_sum(vals, comm, counts, template):
     who = [t for t, (a, b) in enumerate(zip(lo, hi)) for _ in range(b - a)]
     mine = [_Packed(v, comm) for v in vals]
     like = mine[0] if mine else _Packed(template(), comm)
-    bufs = [None] * nobj
+    bufs = [None] * nobj   # per item: its list of per-dtype buffers
     for i, p in enumerate(mine):
-        bufs[lo[rank] + i] = p.buf
+        bufs[lo[rank] + i] = p.bufs
     step = 1
     while step < nobj:
         for j in range(0, nobj, 2 * step):
             if j + step < nobj:
                 if rank == who[j]:
                     if who[j] == who[j + step]:
-                        bufs[j] = bufs[j] + bufs[j + step]
+                        bufs[j] = [a + b for a, b in zip(bufs[j], bufs[j + step])]
                     else:
                         other = like.zeros()
-                        comm.recv_tensor_(other, who[j + step])
-                        bufs[j] = bufs[j] + other
+                        for o in other:
+                            comm.recv_tensor_(o, who[j + step])
+                        bufs[j] = [a + b for a, b in zip(bufs[j], other)]
                     bufs[j + step] = None
                 elif rank == who[j + step]:
-                    comm.send_tensor(bufs[j + step], who[j])
+                    for b in bufs[j + step]:
+                        comm.send_tensor(b, who[j])
                     bufs[j + step] = None
         step *= 2
     out = bufs[0] if rank == who[0] else like.zeros()
-    comm.broadcast_tensor_(out, who[0])
+    for o in out:
+        comm.broadcast_tensor_(o, who[0])
     return like.unpack(out)
 
 
+def device_checksum(t):
+    """An order- and bit-sensitive 64-bit checksum of a tensor's values,
+    computed where the tensor lives (one int64 back to the host): each word's
+    bits are mixed and weighted by an odd multiplier of its position, summed
+    with wraparound.  Equal tensors give equal checksums on every rank; any
+    bit flip or permutation changes it with overwhelming probability.  (The
+    reference pickles the whole field and hashes the bytes,
+    src/utilities.py:453-458.)"""
+    import torch
+    t = t.detach().contiguous()
+    if t.is_complex():
+        t = torch.view_as_real(t).contiguous()
+    flat = t.reshape(-1)
+    if flat.numel() == 0:
+        return 0
+    ints = {8: torch.int64, 4: torch.int32, 2: torch.int16, 1: torch.uint8}[flat.element_size()]
+    w = (flat.view(ints) if flat.dtype != ints else flat).to(torch.int64)
+    w = w ^ (w >> 29)
+    idx = torch.arange(1, w.numel() + 1, dtype=torch.int64, device=w.device)
+    mult = (idx * -7046029254386353131) | 1       # 0x9E3779B97F4A7C15 (golden ratio), odd
+    return int(((w * mult) ^ (w >> 17)).sum())
+
+
+def _sync_token(obj, hash_):
+    """what check_MPI_equality gathers for obj: fields by (domain, dtype,
+    device checksum) per key, domains by value (compared with ==; their
+    pickles carry per-process cached hashes), anything else by its pickle
+    (bytes as they are, e.g. getState()'s), blake2b-hashed on request"""
+    import pickle
+    from hashlib import blake2b
+    from .domain_tuple import DomainTuple
+    from .domains import Domain
+    from .field import Field
+    from .multi_domain import MultiDomain
+    from .multi_field import MultiField
+    if isinstance(obj, Field):
+        return ("field", obj.domain, str(obj.dtype), device_checksum(obj.val))
+    if isinstance(obj, MultiField):
+        return ("multifield", obj.domain,
+                tuple((k, str(obj[k].dtype), device_checksum(obj[k].val)) for k in obj.domain.keys()))
+    if isinstance(obj, (DomainTuple, MultiDomain, Domain)):
+        return ("domain", obj)
+    b = obj if isinstance(obj, bytes) else pickle.dumps(obj)
+    return ("bytes", blake2b(b).hexdigest() if hash_ else b)
+
+
 def check_MPI_equality(obj, comm, hash_=False):
+    """RuntimeError unless obj is the same on every task of comm
+    (src/utilities.py:434-458)"""
     if comm is None:
         return
-    import pickle
-    h = hash(pickle.dumps(obj)) if hash_ else obj
-    lst = comm.allgather(h)
+    lst = comm.allgather(_sync_token(obj, hash_))
     if not all(x == lst[0] for x in lst):
         raise RuntimeError("MPI tasks are not in sync")
 

@@ -202,3 +202,198 @@ def test_deterministic_tree_any_split(results):
         for n0, d in results[r]["dets"].items():
             for k in dom.keys():
                 np.testing.assert_array_equal(d[k], np.asarray(serial[k]), err_msg=f"split {n0}")
+
+
+def _worker_lists(rank, world, port, q, tmp):
+    """a MAP SampleList (one sample on two ranks) saved, resumed and averaged;
+    the deterministic tree over fp32 and complex fields"""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import nifty_amd as ift
+        from nifty_amd import utilities
+        comm = ift.TorchComm()
+        res = {}
+        dom, vals = _values(3)
+        # MAP: rank 0 holds the single sample, rank 1 none (optimize_kl's
+        # SampleList of one position)
+        mine = vals[:1] if rank == 0 else []
+        sl = ift.SampleList(mine, comm=comm, domain=dom)
+        base = os.path.join(tmp, "map")
+        sl.save(base)
+        back = ift.SampleList.load(base, comm=comm)   # no domain: read from sample 0's file
+        res["n"] = (back.n_samples, back.n_local_samples)
+        res["dom"] = back.domain == dom
+        avg = back.average()
+        res["avg"] = {k: np.asarray(avg[k]) for k in dom.keys()}
+        op = lambda s: 2. * s["a"]  # noqa: E731  (op changes the layout)
+        res["avg_op"] = np.asarray(back.average(op).val)
+        m, v = back.sample_stat()
+        res["stat"] = {k: np.asarray(m[k]) for k in dom.keys()}
+        # the deterministic tree for fp32 and complex: bitwise the serial sum
+        d2 = ift.makeDomain({"f": ift.RGSpace(9), "c": ift.RGSpace((3, 4))})
+        rng = np.random.default_rng(3)
+        items = []
+        for i in range(7):
+            f = (rng.standard_normal(9) * 10.0 ** rng.integers(-4, 4, 9)).astype(np.float32)
+            c = rng.standard_normal((3, 4)) * 10.0 ** rng.integers(-6, 6, (3, 4)) \
+                + 1j * rng.standard_normal((3, 4))
+            items.append(ift.MultiField.from_dict({"f": ift.makeField(d2["f"], f),
+                                                   "c": ift.makeField(d2["c"], c)}, d2))
+        lo, hi = utilities.shareRange(7, world, rank)
+        t = utilities.allreduce_sum(items[lo:hi], comm, deterministic=True)
+        res["det32c"] = {k: np.asarray(t[k]) for k in d2.keys()}
+        comm.Barrier()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception as e:
+        import traceback
+        q.put((rank, "ERROR " + repr(e) + "\n" + traceback.format_exc()))
+
+
+@pytest.fixture(scope="module")
+def list_results(tmp_path_factory):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    tmp = str(tmp_path_factory.mktemp("lists"))
+    procs = [ctx.Process(target=_worker_lists, args=(r, world, port, q, tmp)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, res = q.get(timeout=240)
+        out[r] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r, res in out.items():
+        assert not isinstance(res, str), res
+    return out
+
+
+def test_map_sample_list_resume(list_results):
+    """SampleList.load on a rank whose share of the files is empty takes the
+    domain from sample 0's file and joins the constructor's allgather (no hang);
+    average / sample_stat on that rank match the owner's"""
+    _, vals = _values(3)
+    assert list_results[0]["n"] == (1, 1) and list_results[1]["n"] == (1, 0)
+    for r in list_results:
+        assert list_results[r]["dom"]
+        for k, v in list_results[r]["avg"].items():
+            np.testing.assert_array_equal(v, np.asarray(vals[0][k]))
+            np.testing.assert_array_equal(list_results[r]["stat"][k], np.asarray(vals[0][k]))
+        np.testing.assert_array_equal(list_results[r]["avg_op"], 2. * np.asarray(vals[0]["a"]))
+
+
+def test_deterministic_tree_fp32_complex(list_results):
+    """fp32 stays fp32 and complex stays complex through the packed buffers:
+    bitwise the serial pairwise sum on every rank"""
+    sys.path.insert(0, ROOT)
+    import nifty_amd as ift
+    from nifty_amd import utilities
+    d2 = ift.makeDomain({"f": ift.RGSpace(9), "c": ift.RGSpace((3, 4))})
+    rng = np.random.default_rng(3)
+    items = []
+    for i in range(7):
+        f = (rng.standard_normal(9) * 10.0 ** rng.integers(-4, 4, 9)).astype(np.float32)
+        c = rng.standard_normal((3, 4)) * 10.0 ** rng.integers(-6, 6, (3, 4)) + 1j * rng.standard_normal((3, 4))
+        items.append(ift.MultiField.from_dict({"f": ift.makeField(d2["f"], f),
+                                               "c": ift.makeField(d2["c"], c)}, d2))
+    serial = utilities.pairwise_sum(items)
+    for r in list_results:
+        for k in ("f", "c"):
+            got = list_results[r]["det32c"][k]
+            want = np.asarray(serial[k])
+            assert got.dtype == want.dtype, (k, got.dtype)
+            np.testing.assert_array_equal(got, want)
+
+
+def _worker_desync(rank, world, port, q):
+    """the reference's MPI consistency guards (utilities.py:434-478,
+    kl_energies.py:136-137, optimize_kl.py:342-345) firing on ranks that
+    disagree -- and staying quiet on ranks that agree"""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import nifty_amd as ift
+        from nifty_amd import utilities
+        comm = ift.TorchComm()
+        res = {}
+
+        def raises(fn):
+            try:
+                fn()
+            except RuntimeError as e:
+                return "not in sync" in str(e)
+            return False
+        dom, vals = _values(2)
+        f = vals[0]
+        # equal objects pass
+        utilities.check_MPI_synced_random_state(comm)
+        utilities.check_MPI_equality(f, comm, hash_=True)
+        utilities.check_MPI_equality(dom, comm)
+        utilities.check_MPI_equality(np.random.SeedSequence(4).spawn(3), comm)
+        # one ulp on one rank, one key
+        a = np.asarray(f["a"]).copy()
+        if rank == 1:
+            a[3] = np.nextafter(a[3], np.inf)
+        g = ift.MultiField.from_dict({"a": ift.makeField(dom["a"], a), "b": f["b"], "xi": f["xi"]}, dom)
+        res["field"] = raises(lambda: utilities.check_MPI_equality(g, comm, hash_=True))
+        # a permutation of the same values
+        a2 = np.asarray(f["a"]).copy()
+        if rank == 1:
+            a2[[0, 1]] = a2[[1, 0]]
+        g2 = ift.MultiField.from_dict({"a": ift.makeField(dom["a"], a2), "b": f["b"], "xi": f["xi"]}, dom)
+        res["perm"] = raises(lambda: utilities.check_MPI_equality(g2, comm, hash_=True))
+        d2 = ift.makeDomain({"a": ift.RGSpace(7, distances=1. + rank)})
+        res["domain"] = raises(lambda: utilities.check_MPI_equality(d2, comm))
+        res["sseq"] = raises(lambda: utilities.check_MPI_equality(
+            np.random.SeedSequence(4 + rank).spawn(3), comm))
+        # the random state: one extra draw on rank 1
+        ift.random.push_sseq_from_seed(5)
+        if rank == 1:
+            ift.random.current_rng().standard_normal(1)
+        res["state"] = raises(lambda: utilities.check_MPI_synced_random_state(comm))
+        ift.random.pop_sseq()
+        # optimize_kl refuses to start an iteration from means that differ
+        sp = ift.RGSpace(8)
+        lh = ift.GaussianEnergy(ift.full(sp, 1.)) @ ift.ScalingOperator(sp, 2.).ducktape("x")
+        pos = ift.MultiField.from_dict({"x": ift.full(sp, 0.5 + 1e-3 * rank)})
+        ift.random.push_sseq_from_seed(6)
+        res["optkl"] = raises(lambda: ift.optimize_kl(
+            lh, 1, 0, ift.NewtonCG(ift.GradientNormController(iteration_limit=1)), None, None,
+            initial_position=pos, comm=comm))
+        ift.random.pop_sseq()
+        comm.Barrier()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception as e:
+        import traceback
+        q.put((rank, "ERROR " + repr(e) + "\n" + traceback.format_exc()))
+
+
+def test_mpi_guards_fire_on_desync():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_desync, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, res = q.get(timeout=240)
+        out[r] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r, res in out.items():
+        assert not isinstance(res, str), res
+        for k, v in res.items():
+            assert v, (r, k)

@@ -36,7 +36,8 @@ def _run(ift, lh, pos, total, **kw):
     means = []
 
     def inspect(sl, i):
-        m = sl._m if hasattr(sl, "_m") else sl.local_item(0)
+        # a MAP iteration's SampleList holds its one position on rank 0 only
+        m = sl._m if hasattr(sl, "_m") else sl.average()
         means.append({k: m[k].val.cpu().numpy() for k in m.keys()})
     ift.random.push_sseq_from_seed(61)
     try:
