@@ -30,27 +30,55 @@ CF_ARGS = dict(offset_mean=0, offset_std=(1e-3, 1e-6), fluctuations=(1., 0.8),
                loglogavgslope=(-3., 1), flexibility=(2, 1.), asperity=(0.5, 0.4))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
+# BASELINE.json configs (SURVEY.md §8(d) synthetic inputs); `pairs`: mirrored
+# pairs per GPU = the config's n_samples over its GPU count, per-GPU share
+# measured on one GPU (C2 4, C4 2, C5 4 pairs)
+CONFIGS = {
+    "C2": dict(shape=(1024, 1024), lik="poisson", pairs=4, cg="fp64",
+               desc="1024^2 SimpleCorrelatedField, exp, Poisson counts, geoVI mirrored"),
+    "C3": dict(shape=(2048, 2048), lik="los", pairs=4, cg="fp64",
+               desc="2048^2 SimpleCorrelatedField, sigmoid, LOSResponse, Gaussian 1e-3, geoVI mirrored"),
+    "C4": dict(shape=(512, 512, 512), lik="gauss", pairs=2, cg="fp64",
+               desc="512^3 SimpleCorrelatedField (no asperity), GeometryRemover, Gaussian 0.01, geoVI mirrored"),
+    "C5": dict(shape=(4096, 4096), lik="gauss", pairs=4, cg="fp32",
+               desc="4096^2 SimpleCorrelatedField, GeometryRemover, Gaussian 0.01, geoVI mirrored, "
+                    "fp32-storage / fp64-accumulated CG"),
+}
+
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--size", type=int, default=2048)
+    p.add_argument("--config", choices=sorted(CONFIGS), default="C3",
+                   help="BASELINE.json workload (the headline is C3; C2 / C4 / C5 are the other GPU configs' "
+                        "per-GPU shares)")
+    p.add_argument("--size", type=int, default=None, help="grid edge (default: the config's)")
     p.add_argument("--nlos", type=int, default=16384)
     # C3 (BASELINE.json configs[2]): geoVI n_samples=8 mirrored pairs across 2
     # GPUs -> 4 pairs (8 samples) per GPU, held fixed per GPU (weak scaling)
-    p.add_argument("--samples-per-gpu", type=int, default=4, help="mirrored pairs per GPU")
+    p.add_argument("--samples-per-gpu", type=int, default=None, help="mirrored pairs per GPU (default: the config's)")
     p.add_argument("--lin-iters", type=int, default=100)
     p.add_argument("--newton-iters", type=int, default=2)
     p.add_argument("--newton-cg-max", type=int, default=50)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-pairs", type=int, default=1, help="mirrored pairs in the timed CPU oracle draw")
+    p.add_argument("--cpu-lin-iters", type=int, default=None,
+                   help="C2/C4/C5: linear-CG iterations of the bounded CPU oracle sample (default 3; C4 1)")
     p.add_argument("--no-demo", action="store_true", help="skip the demo-controller line")
     p.add_argument("--deterministic-allreduce", action="store_true")
     p.add_argument("--backend", choices=["nccl", "gloo"], default=None,
                    help="process-group backend (default: nccl = RCCL on a GPU, gloo on CPU)")
-    return p.parse_args()
+    a = p.parse_args()
+    cfg = CONFIGS[a.config]
+    if a.size is None:
+        a.size = cfg["shape"][0]
+    if a.samples_per_gpu is None:
+        a.samples_per_gpu = cfg["pairs"]
+    if a.cpu_lin_iters is None:
+        a.cpu_lin_iters = 1 if len(cfg["shape"]) == 3 else 3
+    return a
 
 
 def launch_workers(n):
@@ -95,7 +123,30 @@ def barrier_sync(ws):
         torch.cuda.synchronize()
 
 
-def build_problem(ift, n, nlos):
+def build_problem(ift, n, nlos, config="C3"):
+    """(cf, R or None, likelihood energy, expansion point, LOS geometry or
+    None) of a BASELINE config, synthetic mock data from seed 27"""
+    cfg = CONFIGS[config]
+    if cfg["lik"] != "los":
+        shape = (n,) * len(cfg["shape"])
+        sp = ift.RGSpace(shape)
+        cf = ift.SimpleCorrelatedField(sp, **(dict(CF_ARGS, asperity=None) if len(shape) == 3 else CF_ARGS))
+        ift.random.push_sseq_from_seed(27)
+        mock = ift.from_random(cf.domain, "normal")
+        if cfg["lik"] == "poisson":
+            sig = cf.exp()
+            lam = sig(mock).val.cpu().numpy()
+            counts = ift.random.current_rng().poisson(lam).astype(np.int64)
+            pos = 0.1 * ift.from_random(cf.domain, "normal")
+            lh = ift.PoissonianEnergy(ift.makeField(sp, counts)) @ sig
+        else:
+            R = ift.GeometryRemover(sp)
+            N = ift.ScalingOperator(R.target, 0.01, np.float64)
+            data = R(cf(mock)) + N.draw_sample()
+            pos = 0.1 * ift.from_random(cf.domain, "normal")
+            lh = ift.GaussianEnergy(data, inverse_covariance=N.inverse) @ (R @ cf)
+        ift.random.pop_sseq()
+        return cf, None, lh, pos, None
     sp = ift.RGSpace((n, n))
     cf = ift.SimpleCorrelatedField(sp, **CF_ARGS)
     signal = ift.sigmoid(cf)
@@ -119,7 +170,7 @@ def probe_setup(ift, lh, pos, k):
     (kl_energies.py:147-153, 1 + J^T J of the likelihood's transformation),
     its fused core, and k random right-hand-side buffers laid out like
     FusedCGBatch's (k, latent) blocks."""
-    from nifty_amd.minimization.fused_cg import fusable_metric
+    from nifty_amd.minimization.fused_cg import fusable_metric, mixed_precision
     dtype, f_lh = lh.get_transformation()
     fl = f_lh(ift.Linearization.make_var(pos))
     met = (ift.SandwichOperator.make(fl.jac, ift.ScalingOperator(f_lh.target, 1., dtype))
@@ -130,11 +181,13 @@ def probe_setup(ift, lh, pos, k):
     lay = core.layout
     # probe vectors: device normals in the packed layout (padding zero); the
     # values do not matter for timing, so the host PCG64 stream is not used
-    X = torch.zeros((3 * k, lay.size), dtype=torch.float64, device=lay.device)
+    # (C5: fp32 storage, as FusedCGBatch.run allocates them)
+    dt = torch.float32 if mixed_precision(core, W) else torch.float64
+    X = torch.zeros((3 * k, lay.size), dtype=dt, device=lay.device)
     g = torch.Generator(device=lay.device)
     g.manual_seed(1234)
     for key, o, n in zip(lay.keys, lay.offsets, lay.sizes):
-        X[:, o:o + n] = torch.randn((3 * k, n), dtype=torch.float64, device=lay.device, generator=g)
+        X[:, o:o + n] = torch.randn((3 * k, n), dtype=torch.float64, device=lay.device, generator=g).to(dt)
     return core, W, shift, X
 
 
@@ -151,6 +204,7 @@ def cg_iteration(lib, core, W, shift, bufs, k):
     n = X.shape[1]
     P = _native.ptr
     s_ = _native.stream_ptr()
+    dt = _native.dtype_code(X.dtype)
     nq = _quad_blocks(core, W, X.dtype)
     from nifty_amd.minimization.fused_cg import _CarryIteration
     if nq and X.dtype == torch.float64 and _CarryIteration.supported(core, k):
@@ -165,15 +219,15 @@ def cg_iteration(lib, core, W, shift, bufs, k):
     if nq:
         nbd = int(lib.nft_cg_dd_blocks(n))
         PQ = torch.empty((k, nbd + nq), dtype=torch.float64, device=X.device)
-        _native._check(lib.nft_cg_direction_dd_batched(P(D), P(R), n, n, k, 0, P(SC), shift, P(PQ), nbd + nq, s_))
+        _native._check(lib.nft_cg_direction_dd_batched(P(D), P(R), n, n, k, dt, P(SC), shift, P(PQ), nbd + nq, s_))
         core.metric_flat_batch(D, Q, W, 0.0, qpart=PQ[:, nbd:])
         _native._check(lib.nft_fold_partials(P(PQ), nbd + nq, k, P(SC[:, _native.CG_CURV:]), _native.CG_NSCALARS,
                                              s_))
     else:
-        _native._check(lib.nft_cg_direction_batched(P(D), P(R), n, n, k, 0, P(SC), s_))
+        _native._check(lib.nft_cg_direction_batched(P(D), P(R), n, n, k, dt, P(SC), s_))
         core.metric_flat_batch(D, Q, W, 0.0)
-        _native._check(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, 0, shift, P(SC), P(ws), s_))
-    _native._check(lib.nft_cg_update_batched(P(X), P(R), P(D), P(Q), 0, n, n, k, 0, shift, P(SC), P(ws), s_))
+        _native._check(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, shift, P(SC), P(ws), s_))
+    _native._check(lib.nft_cg_update_batched(P(X), P(R), P(D), P(Q), 0, n, n, k, dt, shift, P(SC), P(ws), s_))
 
 
 def cg_iteration_wall(lib, core, W, shift, bufs, k, reps=20):
@@ -219,15 +273,18 @@ def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False):
     """Algorithmic bytes per launch (fp64, every operand array counted once per
     launch; arrays shared by the k right-hand sides -- amplitude, xi0, pindex,
     the LOS matrix and its scales -- once).  DESIGN.md §3."""
-    n = cf.target.shape[0]
-    N = n * n
-    Hh = n * (n // 2 + 1)
+    shape = cf.target.shape
+    N = int(np.prod(shape))
+    Hh = N // shape[-1] * (shape[-1] // 2 + 1)
     B = cf.amp.B
-    P = R._plan_np
-    nnz = int(P["box_ent"][-1])
-    nseg = int(P["nseg"])
-    nbox = int(P["nbox"])
-    nlos = R.target.shape[0]
+    if R is not None:
+        P = R._plan_np
+        nnz = int(P["box_ent"][-1])
+        nseg = int(P["nseg"])
+        nbox = int(P["nbox"])
+        nlos = R.target.shape[0]
+    else:   # no LOS pair (C2, C4, C5): its rows are not used
+        nnz = nseg = nbox = nlos = 0
     # the Jacobian adjoint's bin sums run over the mirror-folded cell (N_f)
     fold = getattr(getattr(cf, "jbins", None), "fold", None)
     Nf = fold["nf"] if fold else N
@@ -346,17 +403,31 @@ def load_pmc(label):
     return None if e is None else e.get("traffic_bytes")
 
 
-def survey_bytes_per_iteration(cf, R):
+def survey_bytes_per_iteration(cf, R, config="C3"):
     """SURVEY.md §8(d)'s algorithmic bytes of one linear-CG iteration of one
-    right-hand side: N [(4d + 13) s + 8] for the CF metric + CG update, plus
-    2 s N + 16 nnz for the LOS pair (s = 8, d = 2)."""
+    right-hand side: N [(4d + 13) s + 8] for the CF metric + CG update (s = 8
+    fp64, 4 for C5's fp32 storage), + 2 s N for Poisson's per-pixel weights,
+    + 2 s N + 16 nnz for the LOS pair."""
+    cfg = CONFIGS[config]
     N = int(np.prod(cf.target.shape))
     d = len(cf.target.shape)
-    nnz = int(R._plan_np["box_ent"][-1])
-    return N * ((4 * d + 13) * 8 + 8) + 2 * 8 * N + 16 * nnz
+    s = 4 if cfg["cg"] == "fp32" else 8
+    by = N * ((4 * d + 13) * s + 8)
+    if cfg["lik"] == "poisson":
+        by += 2 * s * N
+    if R is not None:
+        by += 2 * s * N + 16 * int(R._plan_np["box_ent"][-1])
+    return by
 
 
-def roofline_of(kp, cgit, cf, R):
+def bytes_model_text(config):
+    cfg = CONFIGS[config]
+    s = "4" if cfg["cg"] == "fp32" else "8"
+    extra = {"poisson": " + 2sN (Poisson weights)", "los": " + 2sN + 16 nnz (LOS pair)"}.get(cfg["lik"], "")
+    return f"SURVEY §8(d): k x (N[(4d+13)s+8]{extra}), s = {s}, d = {len(cfg['shape'])}"
+
+
+def roofline_of(kp, cgit, cf, R, config="C3"):
     """roofline of the FFT+CG matvec the north star targets: one batched CG
     iteration (k right-hand sides) as a unit -- §8(d) bytes x k over the
     measured iteration time (HIP-graph replay of the iteration body, timed
@@ -365,12 +436,12 @@ def roofline_of(kp, cgit, cf, R):
     traffic: PMC HBM bytes of the same launches (profiles/pmc_traffic.json),
     when every kernel of the iteration has an entry."""
     k = cgit["rhs"]
-    by = survey_bytes_per_iteration(cf, R) * k
+    by = survey_bytes_per_iteration(cf, R, config) * k
     us = cgit["us_per_iteration"]
     ach = by / (us * 1e-6) / 1e9
     traffic = 0
     for lab, e in kp.items():
-        t = load_pmc(lab)
+        t = load_pmc(lab) if config == "C3" else None   # the PMC passes cover C3 only
         if t is None:
             traffic = None
             break
@@ -379,7 +450,7 @@ def roofline_of(kp, cgit, cf, R):
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "cg_iteration",
             "rhs": k, "avg_launch_us": us, "algorithmic_bytes_per_launch": by,
-            "bytes_model": "SURVEY §8(d): k x (N[(4d+13)s+8] + 2sN + 16 nnz)",
+            "bytes_model": bytes_model_text(config),
             "largest_kernel": {"label": dom, "avg_us": kp[dom]["avg_us"], "launches": kp[dom]["launches"],
                                "gbs": kp[dom]["gbs"]}}
 
@@ -403,6 +474,38 @@ def cpu_baseline(args, lat0, R, n, pairs):
                                 max_cg=args.newton_cg_max)
         el = time.perf_counter() - t
     return 2 * pairs / el, iters / el, ncores, el, iters
+
+
+def cpu_baseline_config(args, lat0, n, gpu_iters, gpu_samples):
+    """C2 / C4 / C5: the oracle's geoVI draw (oracle/geovi.py, numpy +
+    scipy.fft on all host cores) of one mirrored pair, bounded to
+    `args.cpu_lin_iters` linear-CG iterations and no Newton step (the full
+    draw would take minutes to hours on the host); the CPU rate is its CG
+    iterations per second, and `value` the samples per second the CPU would
+    reach running the GPU run's CG iterations per sample at that rate."""
+    import scipy.fft
+    from oracle.cf import CFOracle
+    from oracle.geovi import GaussWhitened, PoissonWhitened, draw_geovi
+    from oracle.sampling import GradNormCtl
+    cfg = CONFIGS[args.config]
+    shape = (n,) * len(cfg["shape"])
+    ncores = os.cpu_count() or 1
+    o = CFOracle(shape, **(dict(CF_ARGS, asperity=None) if len(shape) == 3 else CF_ARGS))
+    lh = PoissonWhitened(o) if cfg["lik"] == "poisson" else GaussWhitened(o, 0.01)
+    with scipy.fft.set_workers(ncores):
+        t = time.perf_counter()
+        _, iters = draw_geovi(lh, lat0, 1, True, np.random.SeedSequence(1000),
+                              lambda: GradNormCtl(iteration_limit=args.cpu_lin_iters), 0)
+        el = time.perf_counter() - t
+    cgps = iters / el
+    value = gpu_samples / (gpu_iters / cgps)
+    return {"value": round(value, 6), "unit": "samples/s", "cores": ncores, "kind": "port",
+            "cg_iter_per_s": round(cgps, 4),
+            "sample": (f"oracle geoVI draw (oracle/geovi.py: numpy, scipy.fft workers={ncores}) of 1 mirrored "
+                       f"pair on the same {'x'.join(map(str, shape))} problem, bounded to {args.cpu_lin_iters} "
+                       f"linear-CG iteration(s) and no Newton step: {iters} CG iterations in {el:.1f} s (setup "
+                       f"included); value = the GPU run's {gpu_iters} CG iterations for {gpu_samples} samples "
+                       f"at this CPU rate")}
 
 
 def demo_step(ift, lh, pos, nsamp, comm):
@@ -460,7 +563,10 @@ def main():
         ift.utilities.DETERMINISTIC_ALLREDUCE = True
     comm = ift.TorchComm() if ws > 1 else None
     n = args.size
-    cf, R, lh, pos, _ = build_problem(ift, n, args.nlos)
+    cfg = CONFIGS[args.config]
+    if cfg["cg"] == "fp32":
+        ift.config.set_cg_precision("fp32")
+    cf, R, lh, pos, _ = build_problem(ift, n, args.nlos, args.config)
     H = ift.StandardHamiltonian(lh, ift.GradientNormController(iteration_limit=args.lin_iters))
     mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=args.newton_iters),
                         max_cg_iterations=args.newton_cg_max)
@@ -523,12 +629,15 @@ def main():
     cgps = iters / el
     kp, cgit = kernel_probe(ift, cf, R, lh, pos, args.samples_per_gpu) if torch.cuda.is_available() \
         else (None, None)
-    roof = roofline_of(kp, cgit, cf, R) if kp else None
+    roof = roofline_of(kp, cgit, cf, R, args.config) if kp else None
     demo = None
-    if not args.no_demo and torch.cuda.is_available():
+    if not args.no_demo and torch.cuda.is_available() and args.config == "C3":
         demo = demo_step(ift, lh, pos, nsamp, comm)
     cpu = None
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.config != "C3":
+        lat0 = {k: pos[k].val.cpu().numpy() for k in cf.domain.keys()}
+        cpu = cpu_baseline_config(args, lat0, n, int(iters), samples)
+    elif rank == 0 and ws == 1 and not args.no_cpu_baseline:
         lat0 = {k: pos[k].val.cpu().numpy() for k in cf.domain.keys()}
         sps_c, cgps_c, ncores, cel, citers = cpu_baseline(args, lat0, R, n, args.cpu_pairs)
         cpu = {"value": round(sps_c, 6), "unit": "samples/s", "cores": ncores, "kind": "port",
@@ -538,16 +647,25 @@ def main():
                           f"problem with the bench's controllers: {2 * args.cpu_pairs} samples, {citers} CG "
                           f"iterations in {cel:.1f} s")}
     if rank == 0:
-        line = {"metric": "geoVI samples-drawn/sec (+ CG-iter/sec), 2048^2 CorrelatedField",
+        if args.config == "C3":
+            wl = (f"C3: {n}x{n} SimpleCorrelatedField, sigmoid, LOSResponse({args.nlos}), "
+                  f"Gaussian 1e-3, geoVI mirrored, {args.samples_per_gpu} pair(s)/GPU, "
+                  f"lin CG {args.lin_iters} it, NewtonCG {args.newton_iters} it "
+                  f"(inner CG <= {args.newton_cg_max})")
+            metric = "geoVI samples-drawn/sec (+ CG-iter/sec), 2048^2 CorrelatedField"
+        else:
+            shp = "x".join([str(n)] * len(cfg["shape"]))
+            wl = (f"{args.config}: {cfg['desc'].replace(str(cfg['shape'][0]), str(n), 1)} "
+                  f"({shp}), {args.samples_per_gpu} pair(s)/GPU, lin CG {args.lin_iters} it, "
+                  f"NewtonCG {args.newton_iters} it (inner CG <= {args.newton_cg_max})")
+            metric = f"geoVI samples-drawn/sec (+ CG-iter/sec), {args.config} per-GPU share"
+        line = {"metric": metric,
                 "value": round(sps, 6), "unit": "samples/s", "n_gpus": ws, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "f32 (fp64-accumulated CG)" if cfg["cg"] == "fp32" else "f64",
                 "data": "synthetic",
-                "config": {"workload": f"C3: {n}x{n} SimpleCorrelatedField, sigmoid, LOSResponse({args.nlos}), "
-                                       f"Gaussian 1e-3, geoVI mirrored, {args.samples_per_gpu} pair(s)/GPU, "
-                                       f"lin CG {args.lin_iters} it, NewtonCG {args.newton_iters} it "
-                                       f"(inner CG <= {args.newton_cg_max})",
-                           "global_batch": samples // args.steps, "parallelism": f"sample-dp{ws}"},
+                "config": {"workload": wl, "global_batch": samples // args.steps, "parallelism": f"sample-dp{ws}"},
                 "cg_iter_per_s": round(cgps, 3), "cg_iters": int(iters),
                 "roofline": roof, "cpu_baseline": cpu, "demo_controllers": demo,
                 "cg_iteration": cgit, "kernels": kp, "distributed": dist_info}

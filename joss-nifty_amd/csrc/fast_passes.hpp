@@ -212,6 +212,10 @@ constexpr bool persist_ok() {
 
 // in-line LDS padding of a pass (fft_fast.hpp padx): every 8 elements for
 // the strided passes; NFT_PAD_ROWS / NFT_PAD_COLS override at build time
+// values per load group of the CG-carrying unpack epilogue (build-time knob)
+#ifndef NFT_CG_CH
+#define NFT_CG_CH 1
+#endif
 #ifndef NFT_PAD_ROWS
 #define NFT_PAD_ROWS -1
 #endif
@@ -480,7 +484,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         // x and r cannot pass the previous stores to x and r otherwise
         // (same arrays, runtime offsets), which serialised one memory
         // round trip per element
-        constexpr int CG_CH = 2;
+        constexpr int CG_CH = NFT_CG_CH;
         const T* __restrict__ ea = (const T*)a.f.ea;
         const T* __restrict__ eb = (const T*)a.f.eb;
         const T* __restrict__ cd = (const T*)a.f.cd;

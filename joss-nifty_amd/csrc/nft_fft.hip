@@ -747,25 +747,31 @@ __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __r
 // D (the number of transform axes) is a template parameter so that the cell
 // coordinates and the per-item values stay in registers (a runtime D put
 // them in scratch).
-template <typename T, int D>
+// images per load group of the folded prologue (build-time knob; 0: 16 / NBM)
+#ifndef NFT_PRO_G
+#define NFT_PRO_G 2
+#endif
+template <typename T, int D, int NBM>
 __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __restrict__ u, long long P, int nb,
                                                        long long ncell) {
+  // NBM: register capacity for the items (nb <= NBM; nb > 8 runs the item
+  // loop of the last branch with NBM = 8)
   const T* __restrict__ px = (const T*)f.px;
   const T* __restrict__ pa = (const T*)f.pa;
   const T* __restrict__ pb = (const T*)f.pb;
   const T* __restrict__ pc = (const T*)f.pc;
   using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
-  const bool vec = f.ce == nb && f.sc == 1 && (nb & 1) == 0 && nb <= 8;
+  const bool vec = f.ce == nb && f.sc == 1 && (nb & 1) == 0 && nb <= NBM;
   // the CG direction update carried here (f.dr): d = max(0, gamma/gprev) d + r
   // per item, written back to px, d.d accumulated per item (nb <= 8)
   const bool dirc = f.dr != nullptr;
-  T* __restrict__ pd = const_cast<T*>(px);
+  T* pd = const_cast<T*>(px);
   const T* __restrict__ pr = (const T*)f.dr;
-  T bt[8];
-  bool live[8];
-  double dd[8];
+  T bt[NBM];
+  bool live[NBM];
+  double dd[NBM];
 #pragma unroll
-  for (int b = 0; b < 8; ++b) {
+  for (int b = 0; b < NBM; ++b) {
     dd[b] = 0.0;
     bt[b] = (T)0;
     live[b] = false;
@@ -785,6 +791,14 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
   // images are whole cache lines and its mirrored ones share their one
   // unaligned line with the neighbouring wave
   const unsigned hl = nn[D - 1] / 2 + 1, hp = (hl + 63) & ~63u;
+  // images in groups of G: every load of a group (x, r, A, xi0 of all its
+  // images and items) is issued before its first store -- d is stored back
+  // into the array x is read from, so a load cannot pass an earlier store
+  // and per-image load / store pairs would serialise one memory round trip
+  // per image and item
+  constexpr int NIMG = 1 << D;
+  constexpr int G0 = NFT_PRO_G > 0 ? NFT_PRO_G : (16 / NBM > 0 ? 16 / NBM : 1);
+  constexpr int G = G0 < NIMG ? G0 : NIMG;
   for (long long c = (long long)blockIdx.x * 256 + threadIdx.x; c < ncell; c += (long long)gridDim.x * 256) {
     unsigned cc[D], rest = (unsigned)c;
     {
@@ -804,27 +818,26 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
 #pragma unroll
     for (int a = 0; a < D; ++a) cell = cell * (nn[a] / 2 + 1) + cc[a];
     const long long ix = (long long)f.pidx[cell] * f.ce;
-    T cv[8];
+    T cv[NBM];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) cv[b] = (T)0;
+    for (int b = 0; b < NBM; ++b) cv[b] = (T)0;
     if (vec) {
       const V2* q = (const V2*)(pc + ix);
 #pragma unroll
-      for (int bp = 0; bp < 4; ++bp)
+      for (int bp = 0; bp < NBM / 2; ++bp)
         if (2 * bp < nb) {
           const V2 c2 = q[bp];
           cv[2 * bp] = c2.x;
           cv[2 * bp + 1] = c2.y;
         }
-    } else if (nb <= 8) {
+    } else if (nb <= NBM) {
 #pragma unroll
-      for (int b = 0; b < 8; ++b)
+      for (int b = 0; b < NBM; ++b)
         if (b < nb) cv[b] = pc[b * f.sc + ix];
     }
     // images: bit a of m flips axis a (skipped when that axis is self-mirror)
-#pragma unroll
-    for (int m = 0; m < (1 << D); ++m) {
-      unsigned j = 0;
+    auto image = [&](int m, unsigned& j) {
+      j = 0;
       bool dup = false;
 #pragma unroll
       for (int a = 0; a < D; ++a) {
@@ -836,50 +849,95 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
         }
         j = j * nn[a] + k;
       }
-      if (dup) continue;
-      const T a = pa ? pa[j] : (T)1;
-      const T bj = pb[j];
-      if (nb > 8) {  // large batches (no carried direction): items in a loop
+      return !dup;
+    };
+    if (nb > NBM) {  // large batches (no carried direction): items in a loop
+#pragma unroll
+      for (int m = 0; m < NIMG; ++m) {
+        unsigned j;
+        if (!image(m, j)) continue;
+        const T a = pa ? pa[j] : (T)1;
+        const T bj = pb[j];
         for (int b = 0; b < nb; ++b) {
           T v = px[b * f.sx + j];
           if (pa) v *= a;
           v += bj * pc[b * f.sc + ix];
           u[b * P + j] = v;
         }
-        continue;
+      }
+      continue;
+    }
+#pragma unroll
+    for (int g0 = 0; g0 < NIMG; g0 += G) {
+      unsigned jj[G];
+      bool ok[G];
+      T av[G], bv[G], xv[G][NBM], rv[G][NBM];
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        ok[i] = image(g0 + i, jj[i]);
+        const unsigned j = jj[i];
+        av[i] = (T)1;
+        bv[i] = (T)0;
+#pragma unroll
+        for (int b = 0; b < NBM; ++b) xv[i][b] = rv[i][b] = (T)0;
+        if (!ok[i]) continue;
+        if (pa) av[i] = pa[j];
+        bv[i] = pb[j];
+#pragma unroll
+        for (int b = 0; b < NBM; ++b) {
+          if (b >= nb) break;
+          xv[i][b] = px[b * f.sx + j];
+          if (dirc && live[b]) rv[i][b] = pr[b * f.sx + j];
+        }
       }
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        if (b >= nb) break;
-        T v = px[b * f.sx + j];
-        if (dirc && live[b]) {
-          v = bt[b] * v + pr[b * f.sx + j];
-          pd[b * f.sx + j] = v;
-          dd[b] += (double)v * (double)v;
+      for (int i = 0; i < G; ++i) {
+        if (!ok[i]) continue;
+        const unsigned j = jj[i];
+#pragma unroll
+        for (int b = 0; b < NBM; ++b) {
+          if (b >= nb) break;
+          T v = xv[i][b];
+          if (dirc && live[b]) {
+            v = bt[b] * v + rv[i][b];
+            pd[b * f.sx + j] = v;
+            dd[b] += (double)v * (double)v;
+          }
+          if (pa) v *= av[i];
+          v += bv[i] * cv[b];
+          u[b * P + j] = v;
         }
-        if (pa) v *= a;
-        v += bj * cv[b];
-        u[b * P + j] = v;
       }
     }
   }
   if (dirc) {
     // per item: wave shuffles, then the four waves in order (fixed order)
-    __shared__ double dsh[4][8];
+    __shared__ double dsh[4][NBM];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < NBM; ++b) {
       double v = dd[b];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
       if ((threadIdx.x & 63) == 0) dsh[threadIdx.x >> 6][b] = v;
     }
     __syncthreads();
-    if (threadIdx.x < (unsigned)nb) {
+    if (threadIdx.x < (unsigned)nb && threadIdx.x < (unsigned)NBM) {
       const int b = threadIdx.x;
       const double t = ((dsh[0][b] + dsh[1][b]) + dsh[2][b]) + dsh[3][b];
       f.dpart[b * f.dps + f.dblk0 + blockIdx.x] = live[b] ? f.dshift * t : 0.0;
     }
   }
+}
+
+template <typename T, int D>
+static void launch_pro_fold(const fast::FuseArgs& f, T* u, long long ncell, hipStream_t s) {
+  const dim3 grid((unsigned)((ncell + 255) / 256));
+  if (f.nb <= 2)
+    hipLaunchKernelGGL((pro_fold_kernel<T, D, 2>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+  else if (f.nb <= 4)
+    hipLaunchKernelGGL((pro_fold_kernel<T, D, 4>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+  else
+    hipLaunchKernelGGL((pro_fold_kernel<T, D, 8>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
 }
 
 template <typename T>
@@ -949,13 +1007,12 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
       long long ncell = 1;  // padded cell grid (pro_fold_kernel)
       for (int a = 0; a < f.fnd; ++a) ncell *= a == f.fnd - 1 ? ((f.fn[a] / 2 + 1 + 63) & ~63LL) : f.fn[a] / 2 + 1;
       prof_mark(s, f.dr ? "pro_fold+dir" : "pro_fold");
-      const dim3 grid((unsigned)((ncell + 255) / 256));
       if (f.fnd == 1)
-        hipLaunchKernelGGL((pro_fold_kernel<T, 1>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+        launch_pro_fold<T, 1>(f, u, ncell, s);
       else if (f.fnd == 2)
-        hipLaunchKernelGGL((pro_fold_kernel<T, 2>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+        launch_pro_fold<T, 2>(f, u, ncell, s);
       else
-        hipLaunchKernelGGL((pro_fold_kernel<T, 3>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+        launch_pro_fold<T, 3>(f, u, ncell, s);
     } else {
       prof_mark(s, "pro_batch");
       hipLaunchKernelGGL(pro_batch_kernel<T>, dim3(nblk), dim3(256), 0, s, f, u, f.P, f.nb);

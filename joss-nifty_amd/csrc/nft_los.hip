@@ -34,7 +34,10 @@ constexpr int LOS_CAP_F = 2048;  // entries per forward work item (host-guarante
 constexpr int LOS_CH_A = 2048;   // adjoint: entries staged in LDS per chunk
 constexpr int LOS_YL = 2048;     // adjoint: LDS slots for the line values of a box (all batch vectors)
 constexpr int LOS_KMAX = 8;      // vectors per batched launch
-constexpr int LOS_SEG_ROUNDS = 4;  // forward: <= 256 segments per item = 4 rounds of 64 quads (host-guaranteed)
+constexpr int LOS_SEG_ROUNDS = 4;
+#ifndef NFT_LOS_UT
+#define NFT_LOS_UT 0
+#endif  // forward: <= 256 segments per item = 4 rounds of 64 quads (host-guaranteed)
 
 struct BoxGeom {
   long long H, W;
@@ -62,22 +65,42 @@ struct BoxGeom {
 // the reduce reads each line's slots contiguously.  The bounds and slots of
 // all of a thread's segments (LOS_SEG_ROUNDS rounds of 64) are loaded before
 // the barrier, off the critical path of the segment loop.
+// XCD-contiguous work order: workgroups are dealt to the 8 XCDs round-robin,
+// so workgroup w takes unit (w % 8) * ceil(n / 8) + w / 8 -- each XCD walks
+// one contiguous range of boxes, and neighbouring boxes (which share lines
+// of sight: adjacent partial slots forward, the same line values adjoint)
+// meet in that XCD's L2.  A bijection onto [0, n) for a grid of 8 ceil(n/8)
+// workgroups (the surplus ones return).
+__device__ __forceinline__ int xcd_unit(int w, int n) {
+  const int per = (n + 7) >> 3;
+  return (w & 7) * per + (w >> 3);
+}
+
 template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __restrict__ x,
                                                      const T* __restrict__ cs, double* __restrict__ part,
-                                                     long long xs, int pk, long long css) {
+                                                     long long xs, int pk, long long css, int dbg) {
   // every product is rounded before it is summed, in all K variants alike
   // (no FMA contraction): batched results are bitwise the K = 1 results
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CAP_F / 256;
   // pixel-major tile: the K values of one pixel are adjacent (one or two
   // 16-byte LDS reads per entry instead of K 8-byte ones)
+#if NFT_LOS_UT
+  // vector-major tile: 8-byte reads of pixel l at bank 2 l mod 64 (the
+  // pixel-major 32-byte rows put every pixel on one of 8 bank groups)
+  __shared__ __align__(16) double ut[K][256];
+#define UAT(l, b) ut[b][l]
+#else
   __shared__ __align__(16) double u[256][K];
+#define UAT(l, b) u[l][b]
+#endif
   __shared__ float ew[K == 1 ? 1 : LOS_CAP_F];
   __shared__ unsigned char el[K == 1 ? 1 : LOS_CAP_F];
   __shared__ double prodbuf[K == 1 ? LOS_CAP_F : 1];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
-  const int it = blockIdx.x, t = threadIdx.x;
+  const int it = (dbg & 16) ? xcd_unit(blockIdx.x, p.nitems) : (int)blockIdx.x, t = threadIdx.x;
+  if (it >= p.nitems) return;
   const int box = p.item_box[it];
   bool ok;
   const long long px = g.pixel(box, t, ok);
@@ -91,19 +114,19 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int k = t + i * 256;
-      wv[i] = k < n ? p.ent_wf[e0 + k] : 0.f;
-      lv[i] = k < n ? p.ent_loc[e0 + k] : 0;
+      wv[i] = k < n ? ((dbg & 8) ? 1.f : p.ent_wf[e0 + k]) : 0.f;
+      lv[i] = k < n ? ((dbg & 8) ? (unsigned char)k : p.ent_loc[e0 + k]) : 0;
     }
   }
   // column (pixel-side) scale: shared by the vectors (css = 0) or one per vector
 #pragma unroll
   for (int b = 0; b < K; ++b) {
     double v = 0.0;
-    if (ok) {
+    if (ok && !(dbg & 4)) {
       v = (double)x[b * xs + px];
       if (cs) v *= (double)cs[b * css + px];
     }
-    u[t][b] = v;
+    UAT(t, b) = v;
   }
   // four lanes per segment: thread t serves segments sq + 64 r
   constexpr int RND = LOS_SEG_ROUNDS;
@@ -135,7 +158,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int k = t + i * 256;
-        if (k < n) prod[k] = (double)wv[i] * u[lv[i]][0];
+        if (k < n) prod[k] = (double)wv[i] * UAT(lv[i], 0);
       }
     }
     __syncthreads();
@@ -145,7 +168,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
         for (int k = a + sub; k < e; k += 4) a0 += prod[k];
       } else {
         for (int k = a + sub; k < e; k += 4)
-          a0 = a0 + (double)p.ent_wf[e0 + k] * u[p.ent_loc[e0 + k]][0];
+          a0 = a0 + (double)p.ent_wf[e0 + k] * UAT(p.ent_loc[e0 + k], 0);
       }
       a0 += __shfl_xor(a0, 1, 64);
       a0 += __shfl_xor(a0, 2, 64);
@@ -165,7 +188,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       const double w = staged ? (double)ew[k] : (double)p.ent_wf[e0 + k];
       const int l = staged ? el[k] : p.ent_loc[e0 + k];
 #pragma unroll
-      for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
+      for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * UAT(l, b);
     }
 #pragma unroll
     for (int b = 0; b < K; ++b) {
@@ -173,14 +196,16 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       v += __shfl_xor(v, 1, 64);
       v += __shfl_xor(v, 2, 64);
       // every lane of the quad holds the sum: lane sub stores vectors sub, sub + 4
-      if ((b & 3) == sub) part[(long long)slot * pk + b] = v;
+      if ((b & 3) == sub && (!(dbg & 1) || v == 12345.678)) part[(long long)slot * pk + b] = v;
     }
   };
+  if (dbg & 2) return;
 #pragma unroll
   for (int r = 0; r < RND; ++r)
     if (sq + 64 * r < s1) segk(so[r], sa[r], sb[r]);
   for (int s = sq + 64 * RND; s < s1; s += 64) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
 }
+#undef UAT
 
 // one wave per line of sight, all K vectors: the line's slots (boxes
 // ascending) hold K adjacent partials each; per vector a fixed-order sum
@@ -243,7 +268,7 @@ template <typename T, typename IDX, int K>
 __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* __restrict__ lidx,
                                                      const T* __restrict__ yv, const T* __restrict__ cs,
                                                      const T* __restrict__ rs, T* __restrict__ out, double scale,
-                                                     long long ys, long long os, long long rss) {
+                                                     long long ys, long long os, long long rss, int remap) {
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CH_A / 256;
   // line table: 256 lines per vector cover every box of an 8-bit-index plan
@@ -255,7 +280,8 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   __shared__ __align__(16) float ew[K == 1 ? 2 * LOS_CH_A : LOS_CH_A];
   __shared__ IDX el[K == 1 ? 1 : LOS_CH_A];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
-  const int box = blockIdx.x, t = threadIdx.x;
+  const int box = remap ? xcd_unit(blockIdx.x, p.nbox) : (int)blockIdx.x, t = threadIdx.x;
+  if (box >= p.nbox) return;
   const int l0 = p.box_lptr[box], nl = p.box_lptr[box + 1] - l0;
   const int e0 = p.box_ent[box], n = p.box_ent[box + 1] - e0;
   const unsigned short* off = p.pix_off + (size_t)box * 257;
@@ -500,15 +526,23 @@ static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* 
       return;
     }
   }
-  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, pk,
-                     css);
+  // NFT_LOS_DBG (read per launch; tuning probe only): ablation bits of the
+  // items kernel -- 1 no partial stores, 2 no segment sums, 4 no pixel loads,
+  // 8 no entry loads
+  const char* dbs = getenv("NFT_LOS_DBG");
+  const int dbg = dbs ? atoi(dbs) : 0;
+  const unsigned grid = (dbg & 16) ? (unsigned)(8 * ((p->nitems + 7) / 8)) : (unsigned)p->nitems;
+  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3(grid), dim3(256), 0, s, *p, x, cs, part, xs, pk, css, dbg);
 }
 
 template <typename T, typename IDX, int K>
 static void adj_boxes_k(const nft_los_plan* p, const IDX* li, const T* y, const T* cs, const T* rs, T* out,
                         double scale, long long ys, long long os, long long rss, hipStream_t s) {
-  hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), dim3((unsigned)p->nbox), dim3(256), 0, s, *p, li, y, cs, rs, out,
-                     scale, ys, os, rss);
+  const char* ab = getenv("NFT_LOS_ADJ_XCD");   // tuning probe (read per launch)
+  const int remap = ab ? atoi(ab) : 0;
+  const unsigned grid = remap ? (unsigned)(8 * ((p->nbox + 7) / 8)) : (unsigned)p->nbox;
+  hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), dim3(grid), dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys,
+                     os, rss, remap);
 }
 
 // vectors are processed in groups of 8 / 4 / 2 / 1 (template sizes)

@@ -12,7 +12,8 @@ Restates
 on latent dicts {key: ndarray} in sorted-key order.  The whitened likelihood
 map f (GaussianEnergy(data, 1/var).get_transformation composed with the
 response, energy_operators.py:186-195,578-579) is `LOSWhitened` (sigmoid o
-LOSResponse, config C3) or `GaussWhitened` (GeometryRemover).  The geoVI
+LOSResponse, config C3), `GaussWhitened` (GeometryRemover) or
+`PoissonWhitened` (exp signal, Poisson counts, config C2).  The geoVI
 energy of a sample is 0.5 |T(x) - m|^2 with T = 1 + J0^T f (kl_energies.py:
 117-118,147-151); its gradient is (1 + J(x)^T J0) (T(x) - m) and its metric
 (1 + J(x)^T J0)(1 + J0^T J(x)).
@@ -41,6 +42,31 @@ class GaussWhitened:
 
     def vjp(self, x, g):
         return _shape_like(self.cf.vjp(x, self.sq * g), x)
+
+
+class PoissonWhitened:
+    """f(x) = 2 sqrt(lambda), lambda = exp(cf(x)) (PoissonianEnergy
+    .get_transformation, energy_operators.py:624-625, composed with the exp
+    signal): f = 2 exp(cf / 2), f' = exp(cf / 2)"""
+
+    def __init__(self, cf):
+        self.cf = cf
+        self.data_shape = cf.shape
+        self._cache = (None, None)
+
+    def _h(self, x):
+        if self._cache[0] is not x:
+            self._cache = (x, np.exp(0.5 * self.cf.value(x)))
+        return self._cache[1]
+
+    def f(self, x):
+        return 2. * self._h(x)
+
+    def jvp(self, x, t):
+        return self._h(x) * self.cf.jvp(x, t)
+
+    def vjp(self, x, g):
+        return _shape_like(self.cf.vjp(x, self._h(x) * g), x)
 
 
 class LOSWhitened:

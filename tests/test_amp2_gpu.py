@@ -204,8 +204,9 @@ def test_carried_amplitude_cg(ift, iters):
 def test_logging_controller_sees_every_energy(ift):
     """A count-only controller with an energy history (enable_logging) is not
     silent: every check reads the energy, so the CG runs unchunked; the
-    iterates equal the silent controller's to rounding and the history holds one
-    energy per check, the last one the final energy's value"""
+    iterates equal the silent controller's to rounding and the history holds the
+    start energy (twice, as the reference's start + first check record it) and
+    one energy per check, the last one the final energy's value"""
     from nifty_amd.minimization import fused_cg
     cf, lh, pos = _los_problem(ift, golden("losmetric64.npz"))
     dtype, f_lh = lh.get_transformation()
@@ -214,8 +215,8 @@ def test_logging_controller_sees_every_energy(ift):
          + ift.ScalingOperator(fl.domain, 1., float))
     core, W, shift = fused_cg.fusable_metric(A)
     e = ift.QuadraticEnergy(0.1 * ift.from_random(cf.domain, "normal"), A, ift.from_random(cf.domain, "normal"))
-    silent = ift.GradientNormController(iteration_limit=12)
-    logged = ift.GradientNormController(iteration_limit=12)
+    silent = ift.GradientNormController(iteration_limit=8)
+    logged = ift.GradientNormController(iteration_limit=8)
     logged.enable_logging()
     assert fused_cg._count_silent(silent) and not fused_cg._count_silent(logged)
     r0 = fused_cg.FusedCG(core, W, shift, silent).run(e)
@@ -226,5 +227,8 @@ def test_logging_controller_sees_every_energy(ift):
     x1 = np.concatenate([r1[0].position[k].val.cpu().numpy().ravel() for k in cf.domain.keys()])
     assert rel(x1, x0) < 1e-10
     h = logged.history
-    assert len(h.energy_values) == logged._itcount + 1 == 13
+    # start() logs and then checks (itcount -1 -> 0), both record the start
+    # energy (iteration_controllers.py:95-112): 2 + 8 checks
+    assert len(h.energy_values) == logged._itcount + 2 == 10
+    assert h.energy_values[0] == h.energy_values[1]
     assert h.energy_values[-1] == pytest.approx(r1[0].value, rel=1e-9)

@@ -1,0 +1,49 @@
+"""LOS forward / adjoint timing on the bench's plan (2048^2, 16384 lines,
+K = 4 vectors, per-vector column scale as in the sampling metric); with
+NFT_LOS_DBG ablations of the items kernel (tuning probe only)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def timed(fn, reps=50):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / reps
+
+
+def main():
+    import nifty_amd as ift
+    from nifty_amd import _native as nat
+    ift.config.set_device("cuda:0")
+    cf, R, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
+    plan = R._box_plan()
+    k = 4
+    N = 2048 * 2048
+    X = torch.randn((k, N), dtype=torch.float64, device="cuda")
+    cs = torch.rand(N, dtype=torch.float64, device="cuda")
+    y = torch.empty((k, R.target.shape[0]), dtype=torch.float64, device="cuda")
+    out = torch.empty_like(X)
+    for dbg in os.environ.get("LOS_DBGS", "0,1,2,4,8,12,3").split(","):
+        os.environ["NFT_LOS_DBG"] = dbg
+        us = timed(lambda: nat.los_forward_batched(plan, X, y, colscale=cs))
+        print(f"fwd dbg={dbg} {us:.1f} us", flush=True)
+    os.environ["NFT_LOS_DBG"] = "0"
+    for ax in ("0", "1"):
+        os.environ["NFT_LOS_ADJ_XCD"] = ax
+        print(f"adj xcd={ax} {timed(lambda: nat.los_adjoint_batched(plan, y, out, rowscale=cs)):.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
