@@ -248,6 +248,9 @@ def newton_cg(e, newton_iters, max_cg=200, nreset=20, alpha=0.1, log=None):
     ls = LineSearch()
     gnorm = np.sqrt(vdot(e.gradient, e.gradient))
     if ctl.start(e.value, gnorm) != 1:
+        if log is not None:
+            log.setdefault("dir", []).append([])
+            log.setdefault("trial", []).append([])
         return e
     f_km1 = None
     dirs = []
