@@ -676,11 +676,17 @@ class FusedCGBatch(FusedCG):
         (gradients A x - b) are updated in place, Bv is b (or None).
         `starts`: per RHS an energy-like object (value, gradient_norm) for the
         controller's start().  Returns (X, [(status, moved)]) -- moved is None
-        for a RHS returned in its initial state."""
-        k = X.shape[0]
-        lay, core = self.layout, self.core
+        for a RHS returned in its initial state.
+
+        Once some right-hand sides have stopped, the live ones are compacted
+        into smaller buffers (and a metric restricted to them, core.subset)
+        when their controllers allow a few more iterations: the lock-step
+        batch then stops paying matvecs for frozen rows.  Per RHS the
+        arithmetic does not depend on the batch size (bitwise)."""
+        k0 = X.shape[0]
+        lay = self.layout
         n = lay.size
-        results = [None] * k
+        results = [None] * k0
         active = []
         for j, (e, ctl) in enumerate(zip(starts, self.controllers)):
             st = ctl.start(e)
@@ -690,30 +696,31 @@ class FusedCGBatch(FusedCG):
                 active.append(j)
         if not active:
             return X, results
+        core = self.core
         dev = core.device
-        D = Rr.clone()
-        Q = torch.zeros_like(X)
-        AX = None
         NS = _native.CG_NSCALARS
-        SC = torch.zeros((k, NS), dtype=torch.float64, device=dev)
-        host = torch.zeros((k, NS), dtype=torch.float64).pin_memory()
         lib = _native.load()
-        ws = _native.workspace(k * lib.nft_reduce_workspace(n), dev, "cgb")
         dt = _native.dtype_code(X.dtype)
         P = _native.ptr
         sh = self.shift
+        full_X, full_Rr = X, Rr
+        rows = list(range(k0))          # buffer position -> original RHS index
+        pos = {j: j for j in rows}      # original RHS index -> buffer position
+        SC = torch.zeros((k0, NS), dtype=torch.float64, device=dev)
+        host = torch.zeros((k0, NS), dtype=torch.float64).pin_memory()
+        ws = _native.workspace(k0 * lib.nft_reduce_workspace(n), dev, "cgb")
 
         def chk(st):
             _native._check(st)
 
         def finish(j, status):
             results[j] = (status, True)
-            SC[j, _native.CG_DONE] = 1.0
+            SC[pos[j], _native.CG_DONE] = 1.0
 
-        for j in range(k):
+        for j in range(k0):
             if results[j] is not None:
                 SC[j, _native.CG_DONE] = 1.0
-        chk(lib.nft_dot_batched(P(Rr), P(Rr), n, n, k, dt, P(SC[:, _native.CG_GAMMA:]), NS, P(ws),
+        chk(lib.nft_dot_batched(P(Rr), P(Rr), n, n, k0, dt, P(SC[:, _native.CG_GAMMA:]), NS, P(ws),
                                 _native.stream_ptr()))
         host.copy_(SC)
         for j in list(active):
@@ -732,20 +739,31 @@ class FusedCGBatch(FusedCG):
         # The update kernel's x.b partial only feeds the energy value; when no
         # controller reads the value (GradientNormController without a name),
         # b is not streamed and the value is computed on demand.
-        Bu = Bv if any(_reads_value(c) for c in self.controllers) else None
-
+        reads_value = any(_reads_value(c) for c in self.controllers)
         nq = _quad_blocks(core, self.W, X.dtype, self.controllers)
-        split = None
-        if nq:
-            nbd = int(lib.nft_cg_dd_blocks(n))
-            PQ = torch.empty((k, nbd + nq), dtype=torch.float64, device=dev)
-            if X.dtype == torch.float64 and Bu is None and _CarryIteration.supported(core, k):
-                split = _CarryIteration(lib, core, self.W, n, k, nq, sh)
-            elif _SPLIT and X.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
-                split = _SplitIteration(lib, core, self.W, n, k, nq, sh, Bu is not None)
+        D = Rr.clone()
+        st = {}
+
+        def setup(k):
+            """the k-dependent iteration state (partials, carried iteration)"""
+            st.clear()
+            st["Q"] = torch.zeros_like(X)
+            st["AX"] = None
+            st["Bu"] = Bv if reads_value else None
+            st["split"] = None
+            if nq:
+                st["nbd"] = int(lib.nft_cg_dd_blocks(n))
+                st["PQ"] = torch.empty((k, st["nbd"] + nq), dtype=torch.float64, device=dev)
+                if X.dtype == torch.float64 and st["Bu"] is None and _CarryIteration.supported(core, k):
+                    st["split"] = _CarryIteration(lib, core, self.W, n, k, nq, sh)
+                elif _SPLIT and X.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
+                    st["split"] = _SplitIteration(lib, core, self.W, n, k, nq, sh, st["Bu"] is not None)
+        setup(k0)
 
         def body(with_dir):
             s_ = _native.stream_ptr()
+            k = X.shape[0]
+            split, Q, Bu = st["split"], st["Q"], st["Bu"]
             if with_dir and isinstance(split, _CarryIteration):
                 split(X, Rr, D, Q, SC)
                 return
@@ -755,6 +773,7 @@ class FusedCGBatch(FusedCG):
             if with_dir and nq:
                 # curvature from the data space: shift * d.d partials while d is
                 # formed, (J d).W(J d) partials in the LOS forward reduce
+                nbd, PQ = st["nbd"], st["PQ"]
                 chk(lib.nft_cg_direction_dd_batched(P(D), P(Rr), n, n, k, dt, P(SC), sh, P(PQ), nbd + nq, s_))
                 core.metric_flat_batch(D, Q, self.W, 0.0, qpart=PQ[:, nbd:])
                 chk(lib.nft_fold_partials(P(PQ), nbd + nq, k, P(SC[:, _native.CG_CURV:]), NS, s_))
@@ -765,29 +784,67 @@ class FusedCGBatch(FusedCG):
                 chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), s_))
             chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws), s_))
 
+        def compact():
+            """restrict the buffers, the scalars and the metric to the live RHS"""
+            nonlocal X, Rr, Bv, D, SC, host, core, rows, pos, graph, eager, iter_seen
+            keep = sorted(pos[j] for j in active)
+            if X is not full_X:
+                idx = torch.tensor(rows, device=dev)
+                full_X.index_copy_(0, idx, X)
+                full_Rr.index_copy_(0, idx, Rr)
+            kt = torch.tensor(keep, device=dev)
+            X, Rr, D, SC = (t.index_select(0, kt) for t in (X, Rr, D, SC))
+            if Bv is not None:
+                Bv = Bv.index_select(0, kt)
+            host = torch.zeros((len(keep), NS), dtype=torch.float64).pin_memory()
+            iter_seen = iter_seen[keep]
+            rows = [rows[p] for p in keep]
+            pos = {j: p for p, j in enumerate(rows)}
+            sub = getattr(core, "subset", None)
+            if sub is not None:
+                # per-RHS metrics (NewtonCG directions): the live rows' metric
+                core = sub(rows)
+            setup(len(rows))
+            # one eager iteration warms the new batch size's caches, then the
+            # loop body is captured again
+            graph = None
+            eager = 1
+
+        # a core without `subset` applies one metric to every row; a per-RHS
+        # metric compacts only if it can restrict itself (subset not None)
+        can_compact = COMPACT and getattr(core, "subset", _shared) is not None
         graph = None
+        eager = 0
         ii = 0
         first = True
         # several graph replays per host read while every live controller only
         # counts (_count_silent) and no decision trace is recorded
         from . import trace
         chunkable = CHUNK and not trace.active() and all(_count_silent(self.controllers[j]) for j in active)
-        iter_seen = np.zeros(k)
+        # which iteration this solve runs (diagnostics: tools/demo_profile.py)
+        self.path = ("carry" if isinstance(st["split"], _CarryIteration) else "split" if st["split"] is not None
+                     else "quad" if nq else "plain") + ("+chunk" if chunkable else "")
+        self.compactions = 0
+        iter_seen = np.zeros(k0)
         while active:
             if chunkable and graph is not None and ii + 2 < self.nreset:
                 m = min(min(self.controllers[j]._iteration_limit - self.controllers[j]._itcount for j in active),
                         self.nreset - 1 - ii)
                 if m > 1:
-                    iter_seen = self._chunk(graph, m, SC, host, iter_seen, active, finish)
+                    iter_seen = self._chunk(graph, m, SC, host, iter_seen, active, finish, pos)
                     ii += m
+                    if can_compact and _worth_compacting(self.controllers, active, len(rows)):
+                        compact()
+                        self.compactions += 1
                     continue
             self.niter += 1
             ConjugateGradient.iterations_total += len(active)
             ii += 1
             sp = _native.stream_ptr()
             if ii < self.nreset:
-                if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER:
+                if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER or eager > 0:
                     body(not first)
+                    eager = max(0, eager - 1)
                 elif graph is None:
                     if any(_worth_capturing(self.controllers[j], self.niter) for j in active):
                         graph = _capture(lambda: body(True))
@@ -798,6 +855,8 @@ class FusedCGBatch(FusedCG):
                     graph.replay()
                 first = False
             else:
+                k = X.shape[0]
+                Q, Bu = st["Q"], st["Bu"]
                 if not first:
                     chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), sp))
                 first = False
@@ -805,8 +864,9 @@ class FusedCGBatch(FusedCG):
                 chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), sp))
                 gp = SC[:, _native.CG_GAMMA].clone()
                 chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws), sp))
-                if AX is None:
-                    AX = torch.zeros_like(X)
+                if st["AX"] is None:
+                    st["AX"] = torch.zeros_like(X)
+                AX = st["AX"]
                 core.metric_flat_batch(X, AX, self.W, 0.0)
                 flag = SC[:, _native.CG_FLAG].clone()
                 chk(lib.nft_cg_residual_batched(P(Rr), P(AX), P(X), P(Bv), n, n, k, dt, sh, P(SC), P(ws), sp))
@@ -818,9 +878,11 @@ class FusedCGBatch(FusedCG):
             torch.cuda.current_stream().synchronize()
             h = host.numpy()
             iter_seen = h[:, _native.CG_ITER].copy()
+            Bu = st["Bu"]
             for j in list(active):
                 ctl = self.controllers[j]
-                hj = h[j]
+                p = pos[j]
+                hj = h[p]
                 status = None
                 if hj[_native.CG_FLAG] != 0.0:
                     curv = hj[_native.CG_CURV]
@@ -844,32 +906,39 @@ class FusedCGBatch(FusedCG):
                     else:
                         cache = {}
 
-                        def lazy(j=j, cache=cache):
+                        def lazy(p=p, cache=cache, Xc=X, Rc=Rr):
                             if "v" not in cache:
-                                cache["v"] = (lay.unpack(X[j].double()), lay.unpack(Rr[j].double()))
+                                cache["v"] = (lay.unpack(Xc[p].double()), lay.unpack(Rc[p].double()))
                             return cache["v"]
                         xr, xb = float(hj[_native.CG_XR]), float(hj[_native.CG_XB])
                         if Bu is None and Bv is not None and ii != 0:
                             # x.b was not accumulated by the update kernel
-                            def value(j=j, xr=xr):
-                                xbj = float(torch.dot(X[j].double(), Bv[j].double()))
+                            def value(p=p, xr=xr, Xc=X, Bc=Bv):
+                                xbj = float(torch.dot(Xc[p].double(), Bc[p].double()))
                                 return 0.5 * (xr - xbj)
                         else:
                             value = 0.5 * (xr - xb)
                         state = _State(value, math.sqrt(gamma), lazy)
-                        st = ctl.check(state)
+                        sts = ctl.check(state)
                         if callable(state._value):
                             # not read during the check: the buffers move on with the
                             # next iteration, so a later read would see another iterate
                             state._value = _stale
-                        if st != ctl.CONTINUE:
-                            status = st
+                        if sts != ctl.CONTINUE:
+                            status = sts
                 if status is not None:
                     finish(j, status)
                     active.remove(j)
-        return X, results
+            if active and can_compact and _worth_compacting(self.controllers, active, len(rows)):
+                compact()
+                self.compactions += 1
+        if X is not full_X:
+            idx = torch.tensor(rows, device=dev)
+            full_X.index_copy_(0, idx, X)
+            full_Rr.index_copy_(0, idx, Rr)
+        return full_X, results
 
-    def _chunk(self, graph, m, SC, host, iter_seen, active, finish):
+    def _chunk(self, graph, m, SC, host, iter_seen, active, finish, pos):
         """m queued iterations (graph replays) and one host read.  A terminal
         step (guard tripped, gamma zero / negative / NaN) freezes its RHS on
         the device (NFT_CG_DONE = 2, with NFT_CG_AUTO set); every RHS's
@@ -886,8 +955,8 @@ class FusedCGBatch(FusedCG):
         h = host.numpy()
         for j in list(active):
             ctl = self.controllers[j]
-            hj = h[j]
-            p = int(round(hj[NS.CG_ITER] - iter_seen[j]))
+            hj = h[pos[j]]
+            p = int(round(hj[NS.CG_ITER] - iter_seen[pos[j]]))
             ConjugateGradient.iterations_total += p
             frozen = hj[NS.CG_DONE] == 2.0
             status = None
@@ -921,3 +990,25 @@ class FusedCGBatch(FusedCG):
                 finish(j, status)
                 active.remove(j)
         return h[:, NS.CG_ITER].copy()
+
+
+def _shared(rows):
+    raise AssertionError("a shared metric is not restricted")
+
+
+# compaction of the lock-step batch once right-hand sides stop
+# (NFT_CG_COMPACT=0: frozen rows ride along to the end)
+COMPACT = os.environ.get("NFT_CG_COMPACT", "1") != "0"
+
+
+def _worth_compacting(controllers, active, k, min_left=3):
+    """fewer live RHS than rows, and some live controller allows at least
+    `min_left` more iterations (a compaction re-captures the loop body)"""
+    if len(active) >= k:
+        return False
+    for j in active:
+        ctl = controllers[j]
+        lim = getattr(ctl, "_iteration_limit", None)
+        if lim is None or lim - getattr(ctl, "_itcount", 0) >= min_left:
+            return True
+    return False

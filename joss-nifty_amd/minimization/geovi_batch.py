@@ -596,9 +596,16 @@ class GeoVIBatch:
                 ediff = mz._alpha * (old - e.value)
                 ctls.append(AbsDeltaEnergyController(ediff, iteration_limit=mz._max_cg_iterations, name=mz._name))
             trace.tag(ctls[-1], ("dir", stag))
-        states = self.pipe.stack([(r[1].states, r[1].row) for _, r in reqs])
+        pairs = [(r[1].states, r[1].row) for _, r in reqs]
         G = torch.stack([r[1].g for _, r in reqs])
-        core = _MetricCore(self.metric_batch(states), self.layout)
+
+        def make(rows):
+            """the stacked Newton metrics of the requests `rows`; restricts
+            itself to any subset of them (FusedCGBatch compaction)"""
+            c = _MetricCore(self.metric_batch(self.pipe.stack([pairs[i] for i in rows])), self.layout)
+            c.subset = make
+            return c
+        core = make(list(range(len(pairs))))
         cg = FusedCGBatch(core, None, 0.0, ctls, mz._nreset)
         # QuadraticEnergy(0 * x, metric, g, _grad=-g) of NewtonCG.get_descent_direction:
         # value 0, |gradient| = |g|
@@ -619,6 +626,8 @@ class _MetricCore:
         self.mv = mv
         self.layout = layout
         self.device = layout.device
+        # restriction to a subset of the rows (original indices), or None
+        self.subset = None
 
     def metric_flat_batch(self, D, Q, W, shift):
         self.mv(D, Q)

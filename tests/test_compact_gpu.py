@@ -1,0 +1,110 @@
+"""Compaction of the lock-step batched CG (fused_cg.FusedCGBatch.run_packed):
+once some right-hand sides stop, the live ones continue in smaller buffers
+(and, for per-sample Newton metrics, a metric restricted to them).  Per RHS
+the arithmetic does not depend on the batch size, so every result is
+bitwise that of the uncompacted batch and of sequential solves."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from test_geovi_batch_gpu import CF_ARGS, _problem  # noqa: F401
+from test_parity_gpu import _gaussian, _los_problem, golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ift(dev):
+    import nifty_amd
+    return nifty_amd
+
+
+def _metric(ift, which):
+    from nifty_amd.minimization.fused_cg import fusable_metric
+    if which == "los":
+        cf, lh, pos = _los_problem(ift, golden("losmetric64.npz"))
+    else:
+        cf, lh, pos = _gaussian(ift, golden("metric128.npz"))
+    dtype, f_lh = lh.get_transformation()
+    fl = f_lh(ift.Linearization.make_var(pos))
+    A = (ift.SandwichOperator.make(fl.jac, ift.ScalingOperator(f_lh.target, 1., dtype))
+         + ift.ScalingOperator(fl.domain, 1., float))
+    return cf, A, fusable_metric(A)
+
+
+def _energies(ift, cf, A, k, seed):
+    with ift.random.Context(seed):
+        return [ift.QuadraticEnergy(0.1 * ift.from_random(cf.domain, "normal"), A,
+                                    ift.from_random(cf.domain, "normal")) for _ in range(k)]
+
+
+@pytest.mark.parametrize("which", ["los", "gauss"])
+def test_compacted_count_only_vs_sequential(ift, which):
+    """count-only controllers with different limits (queued chunks, then
+    compaction; 25 crosses the nreset=20 residual refresh): bitwise the
+    sequential single solves"""
+    from nifty_amd.minimization.fused_cg import FusedCG, FusedCGBatch
+    cf, A, (core, W, shift) = _metric(ift, which)
+    es = _energies(ift, cf, A, 3, 3)
+    lims = [4, 11, 25]
+    seq = [FusedCG(core, W, shift, ift.GradientNormController(iteration_limit=m)).run(e) for e, m in zip(es, lims)]
+    cg = FusedCGBatch(core, W, shift, [ift.GradientNormController(iteration_limit=m) for m in lims])
+    bat = cg.run(es)
+    assert cg.compactions >= 1
+    for (e1, s1), (e2, s2) in zip(seq, bat):
+        assert s1 == s2
+        for key in cf.domain.keys():
+            assert torch.equal(e1.position[key].val, e2.position[key].val), key
+
+
+@pytest.mark.parametrize("which", ["los", "gauss"])
+def test_compacted_value_controllers_bitwise(ift, which, monkeypatch):
+    """value-driven controllers stopping at different iterations: compacted
+    and uncompacted batches agree bitwise, with the same checks"""
+    from nifty_amd.minimization import fused_cg
+    cf, A, (core, W, shift) = _metric(ift, which)
+    es = _energies(ift, cf, A, 4, 8)
+    ctls = [ift.AbsDeltaEnergyController(d, iteration_limit=m)
+            for d, m in ((1e-1, 40), (1e-3, 7), (1e-6, 16), (1e-9, 30))]
+    out = {}
+    for on in (False, True):
+        monkeypatch.setattr(fused_cg, "COMPACT", on)
+        cs = [copy.deepcopy(c) for c in ctls]
+        cg = fused_cg.FusedCGBatch(core, W, shift, cs)
+        out[on] = (cg.run(es), [c._itcount for c in cs], cg.compactions)
+    assert out[True][2] >= 1 and out[False][2] == 0
+    assert out[True][1] == out[False][1]
+    assert len(set(out[True][1])) > 1
+    for (e1, s1), (e2, s2) in zip(out[False][0], out[True][0]):
+        assert s1 == s2
+        for key in cf.domain.keys():
+            assert torch.equal(e1.position[key].val, e2.position[key].val), key
+
+
+def test_compacted_newton_directions_bitwise(ift, monkeypatch):
+    """batched geoVI refinement with the demo's value-driven Newton
+    controllers: the NewtonCG direction solves (per-sample metrics, restricted
+    by core.subset on compaction) give bitwise the uncompacted samples"""
+    from nifty_amd.minimization import fused_cg
+    cf, lh, pos = _problem(ift, "los")
+    H = ift.StandardHamiltonian(lh, ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=30))
+    res, ncomp = {}, {}
+    orig = fused_cg.FusedCGBatch.run_packed
+
+    def counting(self, *a):
+        r = orig(self, *a)
+        ncomp[on] = ncomp.get(on, 0) + self.compactions
+        return r
+    monkeypatch.setattr(fused_cg.FusedCGBatch, "run_packed", counting)
+    for on in (False, True):
+        monkeypatch.setattr(fused_cg, "COMPACT", on)
+        mini = ift.NewtonCG(ift.AbsDeltaEnergyController(deltaE=0.5, convergence_level=2, iteration_limit=4))
+        ift.random.push_sseq_from_seed(21)
+        sl = ift.draw_samples(pos, H, mini, 2, True)
+        ift.random.pop_sseq()
+        res[on] = [np.concatenate([np.ravel(r[k].val.cpu().numpy()) for k in cf.domain.keys()]) for r in sl._r]
+    assert ncomp.get(True, 0) >= 1 and ncomp.get(False, 0) == 0
+    for a, b in zip(res[False], res[True]):
+        assert np.array_equal(a, b)
