@@ -52,6 +52,8 @@ from .energy import Energy
 
 NS = _native.CG_NSCALARS
 ENABLED = True   # tests compare against the per-sample path with ENABLED = False
+# NFT_GEOVI_DEFER_DIR=0: serve Newton-direction requests as soon as they come
+DEFER_DIR = os.environ.get("NFT_GEOVI_DEFER_DIR", "1") != "0"
 
 
 def _rowdots(pairs):
@@ -538,7 +540,10 @@ class GeoVIBatch:
             for i, req in pending.items():
                 kinds.setdefault(req[0], []).append(i)
             answers = {}
-            if "dir" in kinds:
+            # Newton directions wait while other samples still evaluate
+            # energies (their next requests are mostly directions too): larger
+            # direction batches, and the batched CG compacts as they stop
+            if "dir" in kinds and not (DEFER_DIR and "at" in kinds):
                 answers.update(self._serve_dir([(i, pending[i]) for i in kinds["dir"]]))
             if "at" in kinds:
                 answers.update(self._serve_at([(i, pending[i]) for i in kinds["at"]]))
