@@ -316,6 +316,12 @@ typedef struct nft_los_plan {
   const void* ent_lidx;
   int lidx8;
   const float* ent_wa;
+  /* optional (NULL: partials in line-major slots, seg_slot): the segment of
+   * every line-major slot.  Then the forward stores segment s's partial at
+   * index s (one contiguous run per work item) and the line reduce gathers
+   * its slots through slot_seg -- the same values summed in the same order
+   * (bitwise the line-major layout). */
+  const int* slot_seg;
 } nft_los_plan;
 
 size_t nft_los_workspace(const nft_los_plan* plan);

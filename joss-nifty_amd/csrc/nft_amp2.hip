@@ -47,7 +47,10 @@ namespace amp2 {
 using AmpConst = nft_amp_const;
 constexpr int NT = 256;
 constexpr int NW = NT / 64;
-constexpr int E = 4;          // bins per thread: tile = 1024 bins, whatever the batch size
+#ifndef NFT_AMP2_E
+#define NFT_AMP2_E 4
+#endif
+constexpr int E = NFT_AMP2_E;  // bins per thread: tile = E * 256 bins, whatever the batch size
 constexpr int TL = E * NT;
 constexpr int MAXR = 256;     // right-hand sides per launch (per-RHS arrival counters)
 constexpr int NS_ = NFT_CG_NSCALARS;

@@ -37,6 +37,12 @@ constexpr int LOS_KMAX = 8;      // vectors per batched launch
 constexpr int LOS_SEG_ROUNDS = 4;
 #ifndef NFT_LOS_UT
 #define NFT_LOS_UT 0
+#endif
+#ifndef NFT_LOS_VLOAD
+#define NFT_LOS_VLOAD 0  // entries staged from aligned 8-entry chunks (uint2 + 2 float4 per thread)
+#endif
+#ifndef NFT_LOS_PAIR
+#define NFT_LOS_PAIR 0  // segment loop: entries k and k + 4 of a lane read together
 #endif  // forward: <= 256 segments per item = 4 rounds of 64 quads (host-guaranteed)
 
 struct BoxGeom {
@@ -108,6 +114,9 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
   const int e0 = p.item_ent[it], e1 = p.item_ent[it + 1];
   const int n = e1 - e0;
   const bool staged = n <= LOS_CAP_F;  // host plans always fit; others take the direct path
+  // segment-major partials (slot_seg given): segment s at index s, so the
+  // item's stores form one contiguous run
+  const bool segmaj = p.slot_seg != nullptr;
   float wv[PER];
   unsigned char lv[PER];
   if (staged) {
@@ -138,7 +147,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
     const int s = sq + 64 * r;
     sa[r] = s < s1 ? p.seg_ent[s] - e0 : 0;
     sb[r] = s < s1 ? p.seg_ent[s + 1] - e0 : 0;
-    so[r] = s < s1 ? p.seg_slot[s] : 0;
+    so[r] = s < s1 ? (segmaj ? s : p.seg_slot[s]) : 0;
   }
   if (K > 1 && staged) {
 #pragma unroll
@@ -177,7 +186,8 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 #pragma unroll
     for (int r = 0; r < RND; ++r)
       if (sq + 64 * r < s1) seg1(so[r], sa[r], sb[r]);
-    for (int s = sq + 64 * RND; s < s1; s += 64) seg1(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
+    for (int s = sq + 64 * RND; s < s1; s += 64)
+      seg1(segmaj ? s : p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
     return;
   }
   auto segk = [&](int slot, int a, int e) {
@@ -203,7 +213,8 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 #pragma unroll
   for (int r = 0; r < RND; ++r)
     if (sq + 64 * r < s1) segk(so[r], sa[r], sb[r]);
-  for (int s = sq + 64 * RND; s < s1; s += 64) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
+  for (int s = sq + 64 * RND; s < s1; s += 64)
+    segk(segmaj ? s : p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
 }
 #undef UAT
 
@@ -213,10 +224,10 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 // vector the sum over its 4 lines of t_l * y_l, t_l = (R (cs x))_l before
 // the row scale -- the data-space quadratic form x . (cs R^T (rs' R cs x))
 // of the sampling-metric middle (nft_los_forward_quad_batched)
-template <typename T>
+template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const double* __restrict__ part,
                                                       const T* __restrict__ rs, T* __restrict__ y, double scale,
-                                                      int K, long long ys, double* __restrict__ qpart,
+                                                      long long ys, double* __restrict__ qpart,
                                                       long long qstride) {
   __shared__ double qs[4][LOS_KMAX];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -227,11 +238,43 @@ __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const doub
   for (int v = 0; v < LOS_KMAX; ++v) acc[v] = 0.0;
   if (valid) {
     const int a = p.los_ptr[l], b = p.los_ptr[l + 1];
-    for (int k = a + lane; k < b; k += 64) {
-      const double* q = part + (long long)k * K;
+    if (p.slot_seg) {
+      // segment-major partials: the lane's first RR slots' segment indices,
+      // then all their partials, in flight together; summed in slot order
+      // (bitwise the line-major layout)
+      constexpr int RR = 4;
+      int sg[RR];
 #pragma unroll
-      for (int v = 0; v < LOS_KMAX; ++v)
-        if (v < K) acc[v] += q[v];
+      for (int j = 0; j < RR; ++j) {
+        const int k = a + lane + 64 * j;
+        sg[j] = k < b ? p.slot_seg[k] : -1;
+      }
+      double qv[RR][K];
+#pragma unroll
+      for (int j = 0; j < RR; ++j) {
+        const double* q = part + (long long)(sg[j] < 0 ? 0 : sg[j]) * K;
+#pragma unroll
+        for (int v = 0; v < K; ++v) qv[j][v] = sg[j] >= 0 ? q[v] : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < RR; ++j)
+        if (sg[j] >= 0) {
+#pragma unroll
+          for (int v = 0; v < K; ++v) acc[v] += qv[j][v];
+        }
+      for (int k = a + lane + 64 * RR; k < b; k += 64) {
+        const double* q = part + (long long)p.slot_seg[k] * K;
+#pragma unroll
+        for (int v = 0; v < LOS_KMAX; ++v)
+          if (v < K) acc[v] += q[v];
+      }
+    } else {
+      for (int k = a + lane; k < b; k += 64) {
+        const double* q = part + (long long)k * K;
+#pragma unroll
+        for (int v = 0; v < LOS_KMAX; ++v)
+          if (v < K) acc[v] += q[v];
+      }
     }
   }
 #pragma unroll
@@ -286,6 +329,12 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   const int e0 = p.box_ent[box], n = p.box_ent[box + 1] - e0;
   const unsigned short* off = p.pix_off + (size_t)box * 257;
   const int a = off[t], b = off[t + 1];
+  // the pixel's row scales are loaded up front (off the tail of the block)
+  bool ok;
+  const long long px = g.pixel(box, t, ok);
+  double rsv[K];
+#pragma unroll
+  for (int v = 0; v < K; ++v) rsv[v] = (rs && ok) ? (double)rs[v * rss + px] : 1.0;
   // the first chunk's entry loads go out before the line-table staging so the
   // two dependent load chains overlap
   int lv[PER];
@@ -374,14 +423,12 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
       }
     }
   }
-  bool ok;
-  const long long px = g.pixel(box, t, ok);
   if (ok) {
     // pixel-side scale: shared by the vectors (rss = 0) or one per vector
 #pragma unroll
     for (int v = 0; v < K; ++v) {
       double o = acc[v] * scale;
-      if (rs) o *= (double)rs[v * rss + px];
+      if (rs) o *= rsv[v];
       out[v * os + px] = (T)o;
     }
   }
@@ -443,7 +490,7 @@ __global__ __launch_bounds__(256) void los_fwd_items_pf(nft_los_plan p, const T*
       const int s = sq + 64 * r;
       san[r] = s < s1n ? p.seg_ent[s] - e0n : 0;
       sbn[r] = s < s1n ? p.seg_ent[s + 1] - e0n : 0;
-      son[r] = s < s1n ? p.seg_slot[s] : 0;
+      son[r] = s < s1n ? (p.slot_seg ? s : p.seg_slot[s]) : 0;
     }
   };
   int it = blockIdx.x;
@@ -496,7 +543,8 @@ __global__ __launch_bounds__(256) void los_fwd_items_pf(nft_los_plan p, const T*
 #pragma unroll
     for (int r = 0; r < RND; ++r)
       if (sq + 64 * r < s1) segk(so[r], sa[r], sb[r]);
-    for (int s = sq + 64 * RND; s < s1; s += 64) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
+    for (int s = sq + 64 * RND; s < s1; s += 64)
+      segk(p.slot_seg ? s : p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
     __syncthreads();  // LDS free for the next item
     it = nx;
   }
@@ -569,9 +617,19 @@ static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, c
     }
   }
   prof_mark(s, "los_fwd_reduce");
-  if (p->nlos > 0)
-    hipLaunchKernelGGL(los_fwd_reduce<T>, dim3((unsigned)((p->nlos + 3) / 4)), dim3(256), 0, s, *p, part,
-                       (const T*)rs, (T*)y, scale, K, ys, qpart, qstride);
+  if (p->nlos > 0) {
+    const dim3 grid((unsigned)((p->nlos + 3) / 4));
+#define NFT_RED(KK)                                                                                          \
+  case KK:                                                                                                   \
+    hipLaunchKernelGGL((los_fwd_reduce<T, KK>), grid, dim3(256), 0, s, *p, part, (const T*)rs, (T*)y, scale, \
+                       ys, qpart, qstride);                                                                  \
+    break;
+    switch (K) {
+      NFT_RED(1) NFT_RED(2) NFT_RED(3) NFT_RED(4) NFT_RED(5) NFT_RED(6) NFT_RED(7) NFT_RED(8)
+      default: break;
+    }
+#undef NFT_RED
+  }
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

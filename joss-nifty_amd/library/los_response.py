@@ -9,6 +9,7 @@ csrc/nft_los.hip (box_plan): per 256-pixel box, the runs of each line (for
 R x) and the runs of each pixel (for R^T y), float32 weights as in the
 reference, fp64 accumulation in fixed order."""
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -135,6 +136,11 @@ def los_coo(shape, distances, starts, ends, sigmas=None, truncation=3.):
 
 
 LOS_CAP_F = 2048   # entries per forward work item (csrc/nft_los.hip)
+# forward partials stored segment-major and gathered by the line reduce
+# (nft_los_plan.slot_seg, NFT_LOS_SEG_MAJOR=1).  Measured at 4 x 2048^2 /
+# 16384 lines: items 131 -> 111 us, reduce 14 -> 45 us (random 32-byte
+# gathers): off by default, line-major slots
+SEG_MAJOR = os.environ.get("NFT_LOS_SEG_MAJOR", "0") == "1"
 LOS_KMAX = 8       # vectors per batched LOS launch (csrc/nft_los.hip)
 BOX = 256
 
@@ -201,6 +207,9 @@ def box_plan(rows, cols, w, shape, nlos):
     olm = np.lexsort((seg_box, seg_los))
     seg_slot = np.empty(nseg, dtype=np.int32)
     seg_slot[olm] = np.arange(nseg, dtype=np.int32)
+    # the segment of every slot: the forward stores partials segment-major
+    # (coalesced per item) and the reduce gathers them (nft_los_plan.slot_seg)
+    slot_seg = olm.astype(np.int32)
     los_ptr = np.r_[0, np.cumsum(np.bincount(seg_los, minlength=nlos))].astype(np.int32)
     # ---- adjoint: entries sorted by (box, local pixel)
     key2 = box * BOX + loc
@@ -223,7 +232,8 @@ def box_plan(rows, cols, w, shape, nlos):
                 nitems=len(item_box), nseg=nseg, L=L,
                 item_box=np.asarray(item_box, dtype=np.int32), item_seg=np.asarray(item_seg, dtype=np.int32),
                 item_ent=seg_ent[np.asarray(item_seg, dtype=np.int64)].astype(np.int32),
-                seg_ent=seg_ent, seg_slot=seg_slot, ent_loc=loc[of].astype(np.uint8), ent_wf=wf[of],
+                seg_ent=seg_ent, seg_slot=seg_slot, slot_seg=slot_seg, ent_loc=loc[of].astype(np.uint8),
+                ent_wf=wf[of],
                 los_ptr=los_ptr, box_ent=np.r_[0, np.cumsum(entcnt)].astype(np.int32), pix_off=pix_off,
                 box_lptr=box_lptr, box_lines=seg_los.astype(np.int32),
                 ent_lidx=lidx.astype(np.uint8 if lidx8 else np.uint16), lidx8=int(lidx8), ent_wa=wf[oa])
@@ -294,6 +304,8 @@ class LOSResponse(LinearOperator):
             for k in ("H", "W", "bh", "bw", "nby", "nbx", "nbox", "nlos", "nitems", "nseg", "lidx8"):
                 setattr(d, k, int(P[k]))
             for k, v in keep.items():
+                if k == "slot_seg" and not SEG_MAJOR:
+                    continue
                 setattr(d, k, v.data_ptr() if v.numel() else None)
             self._plan = (d, keep)
         return self._plan[0]

@@ -35,10 +35,29 @@ def main():
     cs = torch.rand(N, dtype=torch.float64, device="cuda")
     y = torch.empty((k, R.target.shape[0]), dtype=torch.float64, device="cuda")
     out = torch.empty_like(X)
-    for dbg in os.environ.get("LOS_DBGS", "0,1,2,4,8,12,3").split(","):
-        os.environ["NFT_LOS_DBG"] = dbg
-        us = timed(lambda: nat.los_forward_batched(plan, X, y, colscale=cs))
-        print(f"fwd dbg={dbg} {us:.1f} us", flush=True)
+    from nifty_amd.library import los_response
+    ref = None
+    for segmaj in (False, True):
+        los_response.SEG_MAJOR = segmaj
+        R._plan = None
+        plan = R._box_plan()
+        nat.los_forward_batched(plan, X, y, colscale=cs)
+        if ref is None:
+            ref = y.clone()
+        else:
+            print(f"segment-major bitwise equal: {bool(torch.equal(ref, y))}", flush=True)
+        for dbg in os.environ.get("LOS_DBGS", "0,1,2").split(","):
+            os.environ["NFT_LOS_DBG"] = dbg
+            us = timed(lambda: nat.los_forward_batched(plan, X, y, colscale=cs))
+            print(f"fwd segmaj={int(segmaj)} dbg={dbg} {us:.1f} us", flush=True)
+        os.environ["NFT_LOS_DBG"] = "0"
+        with nat.LaunchProfile() as prof:
+            for _ in range(10):
+                nat.los_forward_batched(plan, X, y, colscale=cs)
+        acc = {}
+        for lab, ms in prof.records:
+            acc.setdefault(lab, []).append(ms * 1e3)
+        print("   " + ", ".join(f"{k} {sum(v) / len(v):.1f} us" for k, v in acc.items()), flush=True)
     os.environ["NFT_LOS_DBG"] = "0"
     for ax in ("0", "1"):
         os.environ["NFT_LOS_ADJ_XCD"] = ax
