@@ -274,6 +274,13 @@ class LoweredMetric:
         y = self.fn(d, d if shift != 0.0 else None, shift)
         q.copy_(y.reshape(-1)[:q.numel()] if y.numel() >= q.numel() else y)
 
+    def metric_flat_batch(self, D, Q, W, shift):
+        """rows one after another (the batched CG loop with one right-hand
+        side runs exactly metric_flat)"""
+        for j in range(D.shape[0]):
+            self.metric_flat(D[j], Q[j], W, shift)
+        return Q
+
 
 def lowered_metric(A):
     """LoweredMetric for A if A is an endomorphic operator on a latent

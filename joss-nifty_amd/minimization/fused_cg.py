@@ -15,6 +15,7 @@ forming q = q' + shift d first), so the matvec never reads d a second time.
 All scalars stay on the device; one 16-double D2H read per iteration feeds the
 host-side controller, exactly as the reference decides on host floats.
 """
+import collections
 import ctypes
 import math
 import os
@@ -114,30 +115,36 @@ def _capture(fn):
 
 def _reads_value(ctl):
     """False for controllers that never look at the energy value
-    (GradientNormController.check without a name, without an energy history
-    and with the decision trace off, iteration_controllers.py:188-221).  A
-    subclass may read it in an overridden check, so only the exact class
-    qualifies."""
-    from . import trace
+    (GradientNormController.check without a name and without an energy
+    history, iteration_controllers.py:188-221).  A subclass may read it in an
+    overridden check, so only the exact class qualifies.  (The decision trace
+    reads values too, but from scalars recorded beside the iteration: it does
+    not change which iteration runs.)"""
     from .iteration_controllers import GradientNormController
     return not (type(ctl) is GradientNormController and getattr(ctl, "_name", None) is None
-                and getattr(ctl, "_history", None) is None and not trace.active())
+                and getattr(ctl, "_history", None) is None)
 
 
 # data-space curvature (nifty_amd.h "curvature from the data space"):
 # shift * d.d summed while d is formed, (J d).W(J d) while the LOS forward
 # reduces its lines -- no curvature pass over q and d (NFT_CURV_DATA=0: off)
 CURV_DATA = os.environ.get("NFT_CURV_DATA", "1") != "0"
+# ... also for value-driven controllers (energy deltas, gradient-norm
+# tolerances; NFT_CURV_DATA_VALUE=1, off by default).  Equal in exact
+# arithmetic, the data-space curvature rounds differently from the
+# reference's d.(A d), and alpha = gamma / curv then no longer cancels d.r
+# exactly in r -= alpha q: the CG energies leave the reference's trajectory
+# (measured: demo64's AbsDelta(0.05) sampling CG agrees to 1e-12 for 12
+# checks, then drifts -- 7e-7 relative at check 14 -- and stops after 24
+# checks, the reference and its three 1e-15-perturbed runs after 28).
+# Value-driven controllers therefore keep d.q, and with it the separate
+# update pass (the carried update needs alpha before the adjoint).
+CURV_DATA_VALUE = os.environ.get("NFT_CURV_DATA_VALUE", "0") == "1"
 
 
 def _count_only(ctl):
     """True for a controller whose decisions depend on the iteration count
-    alone (GradientNormController without tolerances): then the curvature may
-    be formed from the data space.  Equal in exact arithmetic, its rounding
-    differs from the reference's d.(A d), and long CG trajectories are
-    chaotic in the last bits, so value-driven controllers (energy deltas,
-    gradient-norm tolerances) keep the reference's formula and with it the
-    reference's decisions (tests/test_geovi_trace_gpu.py)."""
+    alone (GradientNormController without tolerances)."""
     from .iteration_controllers import GradientNormController
     return (type(ctl) is GradientNormController and ctl._tol_abs_gradnorm is None
             and ctl._tol_rel_gradnorm is None)
@@ -168,7 +175,7 @@ def _quad_blocks(core, W, dtype, controllers=()):
     """partials per RHS of the metric's data-space quadratic form, or 0"""
     if not CURV_DATA or dtype != torch.float64 or not callable(W):
         return 0
-    if not all(_count_only(c) for c in controllers):
+    if not CURV_DATA_VALUE and not all(_count_only(c) for c in controllers):
         return 0
     if not getattr(core, "supports_quad", False):
         return 0
@@ -213,6 +220,10 @@ def mixed_precision(core, W):
 
 
 class FusedCG:
+    """One fused solve: the batched loop (FusedCGBatch) with one right-hand
+    side -- per RHS the batched kernels run exactly the single-solve
+    arithmetic."""
+
     def __init__(self, core, W, shift, controller, nreset=20):
         self.core, self.W, self.shift = core, W, float(shift)
         self.controller = controller
@@ -220,147 +231,12 @@ class FusedCG:
         self.layout = core.layout
         self.niter = 0
 
-    def _energy(self, A, b, x, r):
-        from .quadratic_energy import QuadraticEnergy
-        lay = self.layout
-        return QuadraticEnergy(lay.unpack(x), A, b, _grad=lay.unpack(r))
-
     def run(self, energy):
-        ctl = self.controller
-        status = ctl.start(energy)
-        if status != ctl.CONTINUE:
-            return energy, status
-        lay, core = self.layout, self.core
-        A, b_mf = energy.metric, energy._b
-        x = lay.pack(energy.position)
-        r = lay.pack(energy.gradient)
-        b = lay.pack(b_mf) if b_mf is not None else None
-        d = r.clone()
-        q = lay.empty()
-        ax = None
-        n = lay.size
-        sc = torch.zeros(_native.CG_NSCALARS, dtype=torch.float64, device=x.device)
-        host = torch.zeros(_native.CG_NSCALARS, dtype=torch.float64).pin_memory()
-        lib = _native.load()
-        ws = _native.workspace(lib.nft_reduce_workspace(n), x.device, "cg")
-        dt = _native.dtype_code(x.dtype)
-        sp = _native.stream_ptr()
-        P = _native.ptr
-        sh = self.shift
-
-        def chk(st):
-            _native._check(st)
-
-        chk(lib.nft_dot(P(r), P(r), n, dt, P(sc[_native.CG_GAMMA:]), P(ws), sp))
-        gamma = sc[_native.CG_GAMMA].item()
-        if np.isnan(gamma):
-            logger.error("Error: ConjugateGradient: previous_gamma==NaN")
-            return energy, ctl.ERROR
-        if gamma == 0:
-            return energy, ctl.CONVERGED
-
-        nq = _quad_blocks(core, self.W, x.dtype, (ctl,))
-        split = None
-        if nq:
-            nbd = int(lib.nft_cg_dd_blocks(n))
-            pq = torch.empty((1, nbd + nq), dtype=torch.float64, device=x.device)
-            if x.dtype == torch.float64 and not _reads_value(ctl) and _CarryIteration.supported(core, 1):
-                # FusedCGBatch's iteration with k = 1 (same partial layout)
-                split = _CarryIteration(lib, core, self.W, n, 1, nq, sh)
-            elif _SPLIT and x.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
-                # FusedCGBatch's split iteration with k = 1 (same partial layout)
-                split = _SplitIteration(lib, core, self.W, n, 1, nq, sh, b is not None)
-
-        def body(with_dir):
-            s_ = _native.stream_ptr()
-            if with_dir and isinstance(split, _CarryIteration):
-                split(x.view(1, -1), r.view(1, -1), d.view(1, -1), q.view(1, -1), sc.view(1, -1))
-                return
-            if with_dir and split is not None:
-                split(x.view(1, -1), r.view(1, -1), d.view(1, -1), q.view(1, -1),
-                      b.view(1, -1) if b is not None else None, sc.view(1, -1))
-                return
-            if with_dir and nq:
-                # the same kernels and partial layout as FusedCGBatch with k = 1
-                chk(lib.nft_cg_direction_dd_batched(P(d), P(r), n, n, 1, dt, P(sc), sh, P(pq), nbd + nq, s_))
-                core.metric_flat(d, q, self.W, 0.0, qpart=pq[:, nbd:])
-                chk(lib.nft_fold_partials(P(pq), nbd + nq, 1, P(sc[_native.CG_CURV:]), _native.CG_NSCALARS, s_))
-            else:
-                if with_dir:
-                    chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), s_))
-                core.metric_flat(d, q, self.W, 0.0)
-                chk(lib.nft_cg_curv(P(d), P(q), n, dt, sh, P(sc), P(ws), s_))
-            chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, sh, P(sc), P(ws), s_))
-
-        graph = None
-        ii = 0
-        first = True
-        while True:
-            self.niter += 1
-            ConjugateGradient.iterations_total += 1
-            ii += 1
-            if ii < self.nreset:
-                if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER:
-                    body(not first)
-                elif graph is None:
-                    if _worth_capturing(ctl, self.niter):
-                        # capture dir + matvec + dot + update once (HIP graph); the
-                        # eager iterations have warmed every workspace/twiddle cache
-                        graph = _capture(lambda: body(True))
-                        graph.replay()
-                    else:
-                        body(True)
-                else:
-                    graph.replay()
-                first = False
-            else:
-                if not first:
-                    chk(lib.nft_cg_direction(P(d), P(r), n, dt, P(sc), sp))
-                first = False
-                core.metric_flat(d, q, self.W, 0.0)
-                chk(lib.nft_cg_curv(P(d), P(q), n, dt, sh, P(sc), P(ws), sp))
-                gp = sc[_native.CG_GAMMA].clone()
-                chk(lib.nft_cg_update(P(x), P(r), P(d), P(q), P(b), n, dt, sh, P(sc), P(ws), sp))
-                if ax is None:
-                    ax = lay.empty()
-                core.metric_flat(x, ax, self.W, 0.0)
-                flag = sc[_native.CG_FLAG].clone()
-                chk(lib.nft_cg_residual(P(r), P(ax), P(x), P(b), n, dt, sh, P(sc), P(ws), sp))
-                sc[_native.CG_GPREV] = gp
-                sc[_native.CG_FLAG] = flag
-                ii = 0
-            host.copy_(sc, non_blocking=True)
-            torch.cuda.current_stream().synchronize()
-            h = host.numpy()
-            if h[_native.CG_FLAG] != 0.0:
-                curv = h[_native.CG_CURV]
-                if np.isnan(curv):
-                    logger.error("Error: ConjugateGradient: curv==NaN")
-                elif curv == 0.:
-                    logger.error("Error: ConjugateGradient: curv==0.")
-                else:
-                    logger.error("Error: ConjugateGradient: alpha<0.")
-                return self._energy(A, b_mf, x, r), ctl.ERROR
-            gamma = float(h[_native.CG_GAMMA])
-            if np.isnan(gamma):
-                logger.error("Error: ConjugateGradient: gamma==NaN")
-                return self._energy(A, b_mf, x, r), ctl.ERROR
-            if gamma < 0:
-                logger.error("Positive definiteness of preconditioner violated!")
-                return self._energy(A, b_mf, x, r), ctl.ERROR
-            if gamma == 0:
-                return self._energy(A, b_mf, x, r), ctl.CONVERGED
-            cache = {}
-
-            def lazy():
-                if "v" not in cache:
-                    cache["v"] = (lay.unpack(x), lay.unpack(r))
-                return cache["v"]
-            value = 0.5 * (float(h[_native.CG_XR]) - float(h[_native.CG_XB]))
-            state = _State(value, math.sqrt(gamma), lazy)
-            status = ctl.check(state)
-            if status != ctl.CONTINUE:
-                return self._energy(A, b_mf, x, r), status
+        cg = FusedCGBatch(self.core, self.W, self.shift, [self.controller], self.nreset)
+        res = cg.run([energy])[0]
+        self.niter = cg.niter
+        self.path = getattr(cg, "path", None)
+        return res
 
 
 def batch_supported(core, W):
@@ -736,39 +612,72 @@ class FusedCGBatch(FusedCG):
         if not active:
             return X, results
 
-        # The update kernel's x.b partial only feeds the energy value; when no
-        # controller reads the value (GradientNormController without a name),
-        # b is not streamed and the value is computed on demand.
-        reads_value = any(_reads_value(c) for c in self.controllers)
+        # The energy value 0.5 (x.r - x.b) needs x.b: the update kernel sums
+        # it while streaming b, or -- in the carried iteration, which has no
+        # separate update -- one dot beside the iteration (reads x and b,
+        # changes nothing).  Value-blind controllers (GradientNormController
+        # without a name) get it on demand only.  The decision trace records
+        # each step's scalars from the device (HIST), so tracing changes
+        # neither the iteration nor the chunking.
+        from . import trace
+        tracing = trace.active()
+        need_value = tracing or any(_reads_value(c) for c in self.controllers)
         nq = _quad_blocks(core, self.W, X.dtype, self.controllers)
         D = Rr.clone()
         st = {}
+        # per step: gamma, x.r, x.b of every RHS (trace replay of queued chunks)
+        HIST = torch.zeros((k0, self.nreset + 1, 3), dtype=torch.float64, device=dev) if tracing else None
+        hsel = torch.tensor([_native.CG_GAMMA, _native.CG_XR, _native.CG_XB], device=dev)
 
         def setup(k):
             """the k-dependent iteration state (partials, carried iteration)"""
             st.clear()
             st["Q"] = torch.zeros_like(X)
             st["AX"] = None
-            st["Bu"] = Bv if reads_value else None
             st["split"] = None
+            carry = bool(nq) and X.dtype == torch.float64 and _CarryIteration.supported(core, k)
+            # x.b from the update kernel (b streamed) or from a dot beside
+            # the carried iteration
+            st["Bu"] = Bv if (need_value and not carry) else None
+            st["xbdot"] = carry and need_value and Bv is not None
             if nq:
                 st["nbd"] = int(lib.nft_cg_dd_blocks(n))
                 st["PQ"] = torch.empty((k, st["nbd"] + nq), dtype=torch.float64, device=dev)
-                if X.dtype == torch.float64 and st["Bu"] is None and _CarryIteration.supported(core, k):
+                if carry:
                     st["split"] = _CarryIteration(lib, core, self.W, n, k, nq, sh)
                 elif _SPLIT and X.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
                     st["split"] = _SplitIteration(lib, core, self.W, n, k, nq, sh, st["Bu"] is not None)
         setup(k0)
 
+        def record():
+            """HIST[r, ITER % (nreset + 1)] = (gamma, x.r, x.b) of every live
+            RHS after this step (device ops only: graph-capturable)"""
+            if HIST is None:
+                return
+            k = X.shape[0]
+            idx = (SC[:, _native.CG_ITER].long() % HIST.shape[1])
+            rows = torch.arange(k, device=dev)
+            live = (SC[:, _native.CG_DONE] == 0.0).unsqueeze(1)
+            cur = HIST[rows, idx]
+            HIST[rows, idx] = torch.where(live, SC.index_select(1, hsel), cur)
+
         def body(with_dir):
             s_ = _native.stream_ptr()
             k = X.shape[0]
             split, Q, Bu = st["split"], st["Q"], st["Bu"]
+            if st["xbdot"]:
+                # the first (direction-less) step runs the separate update:
+                # it streams b for x.b
+                Bu = Bv
             if with_dir and isinstance(split, _CarryIteration):
                 split(X, Rr, D, Q, SC)
+                if st["xbdot"]:
+                    chk(lib.nft_dot_batched(P(X), P(Bv), n, n, k, dt, P(SC[:, _native.CG_XB:]), NS, P(ws), s_))
+                record()
                 return
             if with_dir and split is not None:
                 split(X, Rr, D, Q, Bu, SC)
+                record()
                 return
             if with_dir and nq:
                 # curvature from the data space: shift * d.d partials while d is
@@ -783,10 +692,11 @@ class FusedCGBatch(FusedCG):
                 core.metric_flat_batch(D, Q, self.W, 0.0)
                 chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), s_))
             chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws), s_))
+            record()
 
         def compact():
             """restrict the buffers, the scalars and the metric to the live RHS"""
-            nonlocal X, Rr, Bv, D, SC, host, core, rows, pos, graph, eager, iter_seen
+            nonlocal X, Rr, Bv, D, SC, host, core, rows, pos, graph, eager, iter_seen, HIST
             keep = sorted(pos[j] for j in active)
             if X is not full_X:
                 idx = torch.tensor(rows, device=dev)
@@ -796,6 +706,8 @@ class FusedCGBatch(FusedCG):
             X, Rr, D, SC = (t.index_select(0, kt) for t in (X, Rr, D, SC))
             if Bv is not None:
                 Bv = Bv.index_select(0, kt)
+            if HIST is not None:
+                HIST = HIST.index_select(0, kt)
             host = torch.zeros((len(keep), NS), dtype=torch.float64).pin_memory()
             iter_seen = iter_seen[keep]
             rows = [rows[p] for p in keep]
@@ -818,9 +730,9 @@ class FusedCGBatch(FusedCG):
         ii = 0
         first = True
         # several graph replays per host read while every live controller only
-        # counts (_count_silent) and no decision trace is recorded
-        from . import trace
-        chunkable = CHUNK and not trace.active() and all(_count_silent(self.controllers[j]) for j in active)
+        # counts (_count_silent); a decision trace replays the queued steps'
+        # checks with their recorded scalars (HIST)
+        chunkable = CHUNK and all(_count_silent(self.controllers[j]) for j in active)
         # which iteration this solve runs (diagnostics: tools/demo_profile.py)
         self.path = ("carry" if isinstance(st["split"], _CarryIteration) else "split" if st["split"] is not None
                      else "quad" if nq else "plain") + ("+chunk" if chunkable else "")
@@ -831,17 +743,24 @@ class FusedCGBatch(FusedCG):
                 m = min(min(self.controllers[j]._iteration_limit - self.controllers[j]._itcount for j in active),
                         self.nreset - 1 - ii)
                 if m > 1:
-                    iter_seen = self._chunk(graph, m, SC, host, iter_seen, active, finish, pos)
+                    iter_seen = self._chunk(graph, m, SC, host, iter_seen, active, finish, pos, HIST)
+                    STATS["chunks"] += 1
+                    STATS["chunk_iters"] += m
+                    if isinstance(st["split"], _CarryIteration):
+                        STATS["carry_iters"] += m
                     ii += m
                     if can_compact and _worth_compacting(self.controllers, active, len(rows)):
                         compact()
                         self.compactions += 1
+                        STATS["compactions"] += 1
                     continue
             self.niter += 1
             ConjugateGradient.iterations_total += len(active)
             ii += 1
             sp = _native.stream_ptr()
             if ii < self.nreset:
+                if not first and isinstance(st["split"], _CarryIteration):
+                    STATS["carry_iters"] += 1
                 if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER or eager > 0:
                     body(not first)
                     eager = max(0, eager - 1)
@@ -873,12 +792,15 @@ class FusedCGBatch(FusedCG):
                 live = SC[:, _native.CG_DONE] == 0.0
                 SC[:, _native.CG_GPREV] = torch.where(live, gp, SC[:, _native.CG_GPREV])
                 SC[:, _native.CG_FLAG] = torch.where(live, flag, SC[:, _native.CG_FLAG])
+                record()
                 ii = 0
             host.copy_(SC, non_blocking=True)
             torch.cuda.current_stream().synchronize()
             h = host.numpy()
             iter_seen = h[:, _native.CG_ITER].copy()
-            Bu = st["Bu"]
+            # x.b of this step on the device: streamed by the update kernel,
+            # the dot beside the carried iteration, or the residual refresh
+            xb_dev = st["Bu"] is not None or st["xbdot"] or ii == 0
             for j in list(active):
                 ctl = self.controllers[j]
                 p = pos[j]
@@ -911,7 +833,7 @@ class FusedCGBatch(FusedCG):
                                 cache["v"] = (lay.unpack(Xc[p].double()), lay.unpack(Rc[p].double()))
                             return cache["v"]
                         xr, xb = float(hj[_native.CG_XR]), float(hj[_native.CG_XB])
-                        if Bu is None and Bv is not None and ii != 0:
+                        if not xb_dev and Bv is not None:
                             # x.b was not accumulated by the update kernel
                             def value(p=p, xr=xr, Xc=X, Bc=Bv):
                                 xbj = float(torch.dot(Xc[p].double(), Bc[p].double()))
@@ -932,13 +854,14 @@ class FusedCGBatch(FusedCG):
             if active and can_compact and _worth_compacting(self.controllers, active, len(rows)):
                 compact()
                 self.compactions += 1
+                STATS["compactions"] += 1
         if X is not full_X:
             idx = torch.tensor(rows, device=dev)
             full_X.index_copy_(0, idx, X)
             full_Rr.index_copy_(0, idx, Rr)
         return full_X, results
 
-    def _chunk(self, graph, m, SC, host, iter_seen, active, finish, pos):
+    def _chunk(self, graph, m, SC, host, iter_seen, active, finish, pos, HIST=None):
         """m queued iterations (graph replays) and one host read.  A terminal
         step (guard tripped, gamma zero / negative / NaN) freezes its RHS on
         the device (NFT_CG_DONE = 2, with NFT_CG_AUTO set); every RHS's
@@ -951,6 +874,7 @@ class FusedCGBatch(FusedCG):
         SC[:, NS.CG_AUTO] = 0.0
         self.niter += m
         host.copy_(SC, non_blocking=True)
+        hh = HIST.cpu().numpy() if HIST is not None else None
         torch.cuda.current_stream().synchronize()
         h = host.numpy()
         for j in list(active):
@@ -961,7 +885,12 @@ class FusedCGBatch(FusedCG):
             frozen = hj[NS.CG_DONE] == 2.0
             status = None
             for t in range(p - 1 if frozen else p):
-                st = ctl.check(_COUNT_ONLY_STATE)
+                state = _COUNT_ONLY_STATE
+                if hh is not None:
+                    # the step's recorded scalars (decision trace)
+                    g_, xr_, xb_ = hh[pos[j], (int(round(iter_seen[pos[j]])) + t + 1) % hh.shape[1]]
+                    state = _State(0.5 * (float(xr_) - float(xb_)), math.sqrt(float(g_)), lambda: None)
+                st = ctl.check(state)
                 if st != ctl.CONTINUE:
                     if t != p - 1:
                         raise RuntimeError("count-only controller stopped inside a queued chunk")
@@ -994,6 +923,10 @@ class FusedCGBatch(FusedCG):
 
 def _shared(rows):
     raise AssertionError("a shared metric is not restricted")
+
+
+# which iterations the batched loop ran (tests assert the timed path ran)
+STATS = collections.Counter()
 
 
 # compaction of the lock-step batch once right-hand sides stop

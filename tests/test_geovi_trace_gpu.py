@@ -133,8 +133,10 @@ def test_geovi_trace_golden(ift, G, name, batched):
     cf, lh, pos = _problem(ift, G, name)
     H = ift.StandardHamiltonian(lh, _ctl(ift, c["lin"]))
     mini = ift.NewtonCG(_ctl(ift, c["newton"]), max_cg_iterations=c["max_cg"])
+    from nifty_amd.minimization import fused_cg
     geovi_batch.ENABLED = batched
     trace.TRACE = []
+    fused_cg.STATS.clear()
     try:
         ift.random.push_sseq_from_seed(c["seed"])
         sl = ift.draw_samples(pos, H, mini, c["nsamp"], True, napprox=c.get("napprox", 0))
@@ -143,6 +145,10 @@ def test_geovi_trace_golden(ift, G, name, batched):
     finally:
         trace.TRACE = None
         geovi_batch.ENABLED = True
+    if c["problem"] == "los64" and c["lin"][0] == "gradnorm":
+        # the trace is path-neutral: the sampling CG ran the carried iteration
+        # and queued chunks as untraced
+        assert fused_cg.STATS["carry_iters"] > 0 and fused_cg.STATS["chunks"] > 0
     ns = int(G[name + "_nsamples"])
     assert len(sl._r) == ns
     all_stable = True
@@ -163,6 +169,56 @@ def test_geovi_trace_golden(ift, G, name, batched):
             e = np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-300)
             if all_stable:
                 assert e < tol, (i, k, e, tol)
+
+
+@pytest.mark.parametrize("name", ["bench64", "newton64", "demo64"])
+def test_untraced_timed_path_golden(ift, G, name):
+    """The draw exactly as the bench runs it -- no decision trace, default
+    switches -- against the traced draw and the reference.  The trace is
+    path-neutral (it records each step's scalars from the device), so both
+    draws give bitwise the same samples; with count-only sampling controllers
+    the untraced one ran the carried CG iteration and queued chunks (counted
+    in fused_cg.STATS); where the reference's trace is stable throughout the
+    samples match it at 10x its rounding sensitivity (bench64: 1.16e-8)."""
+    from nifty_amd.minimization import fused_cg, trace
+    c = CASES[name]
+    cf, lh, pos = _problem(ift, G, name)
+
+    def draw(traced):
+        H = ift.StandardHamiltonian(lh, _ctl(ift, c["lin"]))
+        mini = ift.NewtonCG(_ctl(ift, c["newton"]), max_cg_iterations=c["max_cg"])
+        fused_cg.STATS.clear()
+        trace.TRACE = [] if traced else None
+        try:
+            ift.random.push_sseq_from_seed(c["seed"])
+            sl = ift.draw_samples(pos, H, mini, c["nsamp"], True)
+            ift.random.pop_sseq()
+            return sl, trace.TRACE, dict(fused_cg.STATS)
+        finally:
+            trace.TRACE = None
+    slt, events, _ = draw(True)
+    sl, _, stats = draw(False)
+    if c["lin"][0] == "gradnorm":
+        # count-only sampling controllers: the bench's carried, queued path
+        # (value-driven ones keep the reference's d.q, fused_cg.CURV_DATA_VALUE)
+        assert stats.get("carry_iters", 0) >= 90 and stats.get("chunks", 0) > 0, stats
+    for a, b in zip(slt._r, sl._r):
+        for k in cf.domain.keys():
+            assert torch.equal(a[k].val, b[k].val), k
+    all_stable = True
+    for s_ in range(int(G[name + "_nsamples"])):
+        perts = [_ref_events(G, name, f"p{j + 1}_", s_) for j in range(int(G[name + "_nperturbed"]))]
+        _, stable, _, _ = compare(our_events(events, s_), _ref_events(G, name, "", s_), perts)
+        all_stable &= stable
+    assert all_stable or name != "bench64"
+    if not all_stable:
+        return
+    tol = max(1e-8, 10 * float(G[name + "_sens"]))
+    for i, r in enumerate(sl._r):
+        for k in cf.domain.keys():
+            ref = G[f"{name}_r{i}_{k}"]
+            e = np.linalg.norm(r[k].val.cpu().numpy() - ref) / max(np.linalg.norm(ref), 1e-300)
+            assert e < tol, (i, k, e, tol)
 
 
 def test_mgvi_absdelta_trace_golden(ift):
