@@ -751,9 +751,11 @@ __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __r
 #ifndef NFT_PRO_G
 #define NFT_PRO_G 2
 #endif
-template <typename T, int D, int NBM>
+template <typename T, int D, int NBM, bool PI>
 __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __restrict__ u, long long P, int nb,
                                                        long long ncell) {
+  // PI: A and xi0 per item (rows f.sa / f.sb apart: the batched geoVI
+  // refinement's per-sample Jacobians), else shared by the items
   // NBM: register capacity for the items (nb <= NBM; nb > 8 runs the item
   // loop of the last branch with NBM = 8)
   const T* __restrict__ px = (const T*)f.px;
@@ -860,8 +862,8 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
         const T bj = pb[j];
         for (int b = 0; b < nb; ++b) {
           T v = px[b * f.sx + j];
-          if (pa) v *= a;
-          v += bj * pc[b * f.sc + ix];
+          if (pa) v *= PI ? pa[b * f.sa + j] : a;
+          v += (PI ? pb[b * f.sb + j] : bj) * pc[b * f.sc + ix];
           u[b * P + j] = v;
         }
       }
@@ -871,18 +873,26 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
     for (int g0 = 0; g0 < NIMG; g0 += G) {
       unsigned jj[G];
       bool ok[G];
-      T av[G], bv[G], xv[G][NBM], rv[G][NBM];
+      constexpr int NA = PI ? NBM : 1;  // A / xi0 values per image
+      T av[G][NA], bv[G][NA], xv[G][NBM], rv[G][NBM];
 #pragma unroll
       for (int i = 0; i < G; ++i) {
         ok[i] = image(g0 + i, jj[i]);
         const unsigned j = jj[i];
-        av[i] = (T)1;
-        bv[i] = (T)0;
+#pragma unroll
+        for (int b = 0; b < NA; ++b) {
+          av[i][b] = (T)1;
+          bv[i][b] = (T)0;
+        }
 #pragma unroll
         for (int b = 0; b < NBM; ++b) xv[i][b] = rv[i][b] = (T)0;
         if (!ok[i]) continue;
-        if (pa) av[i] = pa[j];
-        bv[i] = pb[j];
+#pragma unroll
+        for (int b = 0; b < NA; ++b) {
+          if (b >= nb) break;
+          if (pa) av[i][b] = pa[b * f.sa + j];
+          bv[i][b] = pb[b * f.sb + j];
+        }
 #pragma unroll
         for (int b = 0; b < NBM; ++b) {
           if (b >= nb) break;
@@ -903,8 +913,8 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
             pd[b * f.sx + j] = v;
             dd[b] += (double)v * (double)v;
           }
-          if (pa) v *= av[i];
-          v += bv[i] * cv[b];
+          if (pa) v *= av[i][PI ? b : 0];
+          v += bv[i][PI ? b : 0] * cv[b];
           u[b * P + j] = v;
         }
       }
@@ -929,15 +939,23 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
   }
 }
 
-template <typename T, int D>
-static void launch_pro_fold(const fast::FuseArgs& f, T* u, long long ncell, hipStream_t s) {
+template <typename T, int D, bool PI>
+static void launch_pro_fold_pi(const fast::FuseArgs& f, T* u, long long ncell, hipStream_t s) {
   const dim3 grid((unsigned)((ncell + 255) / 256));
   if (f.nb <= 2)
-    hipLaunchKernelGGL((pro_fold_kernel<T, D, 2>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+    hipLaunchKernelGGL((pro_fold_kernel<T, D, 2, PI>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
   else if (f.nb <= 4)
-    hipLaunchKernelGGL((pro_fold_kernel<T, D, 4>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+    hipLaunchKernelGGL((pro_fold_kernel<T, D, 4, PI>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
   else
-    hipLaunchKernelGGL((pro_fold_kernel<T, D, 8>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+    hipLaunchKernelGGL((pro_fold_kernel<T, D, 8, PI>), grid, dim3(256), 0, s, f, u, f.P, f.nb, ncell);
+}
+
+template <typename T, int D>
+static void launch_pro_fold(const fast::FuseArgs& f, T* u, long long ncell, hipStream_t s) {
+  if (f.sa != 0 || f.sb != 0)
+    launch_pro_fold_pi<T, D, true>(f, u, ncell, s);
+  else
+    launch_pro_fold_pi<T, D, false>(f, u, ncell, s);
 }
 
 template <typename T>
@@ -982,6 +1000,9 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
   // the in-pass prologue measured 116 us at 2048^2 against about 45 for the
   // folded pass + the plain persistent R2C pass (NFT_PRO_SPLIT1=0: off)
   static const bool split1 = !getenv("NFT_PRO_SPLIT1") || atoi(getenv("NFT_PRO_SPLIT1")) != 0;
+  // per-item A / xi0 in the folded prologue pass (NFT_PRO_FOLD_PI=0: the
+  // in-pass prologue of the R2C row pass)
+  static const bool pi_fold = !getenv("NFT_PRO_FOLD_PI") || atoi(getenv("NFT_PRO_FOLD_PI")) != 0;
   if (split1 && !f.dr && f.P == 0 && f.fnd > 0 && f.pb && f.pro && !v1_only && !no_split &&
       ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
     fast::FuseArgs f1 = f;
@@ -996,7 +1017,10 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     f1.sx = f1.so = f1.sd = f1.s2 = ntot;
     return hartley_fused_impl<T>(f1, in, out, g, ax, sigma, scale, ws, ws_bytes, hws, s);
   }
-  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && (f.nb > 1 || f.dr || f.fnd > 0) &&
+  // per-item A / xi0 (f.sa, f.sb != 0) take the folded pass too (no carried direction)
+  const bool shared_ab = f.sa == 0 && f.sb == 0;
+  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && (shared_ab || (pi_fold && f.fnd > 0 && f.pb && !f.dr)) &&
+      f.P > 0 && (f.nb > 1 || f.dr || f.fnd > 0) &&
       (long long)f.nb * f.P == ntot &&
       ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
     T* u = (T*)((char*)ws + align256(hws));

@@ -1,0 +1,53 @@
+"""The bench's batched CG iteration (C3, 4 RHS) captured as the HIP graph the
+timed loop replays, replayed REPLAYS times (default 20) -- the command to
+run under rocprofv3 --kernel-trace so that tools/trace_labels.py can
+summarise the replayed kernels per label (profiles/*_trace_labels.json).
+Prints the HIP-event wall time per replay."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    import nifty_amd as ift
+    from nifty_amd import _native
+    from nifty_amd.minimization import fused_cg
+    ift.config.set_device("cuda:0")
+    cf, R, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
+    k = 4
+    lib = _native.load()
+    core, W, shift, XS = bench.probe_setup(ift, lh, pos, k)
+    X, Rr, D = XS[:k].clone(), XS[k:2 * k].clone(), XS[2 * k:].clone()
+    Q = torch.zeros_like(X)
+    SC = torch.zeros((k, _native.CG_NSCALARS), dtype=torch.float64, device=X.device)
+    SC[:, _native.CG_GAMMA] = 1.0
+    SC[:, _native.CG_GPREV] = 1.0
+    ws = _native.workspace(k * lib.nft_reduce_workspace(X.shape[1]), X.device, "cgb")
+    bufs = (X, Rr, D, Q, SC, ws)
+    SC0 = SC.clone()
+
+    def body():
+        SC.copy_(SC0)
+        bench.cg_iteration(lib, core, W, shift, bufs, k)
+    for _ in range(3):
+        body()
+    torch.cuda.synchronize()
+    g = fused_cg._capture(body)
+    g.replay()
+    torch.cuda.synchronize()
+    reps = int(os.environ.get("REPLAYS", "20"))
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        g.replay()
+    t1.record()
+    torch.cuda.synchronize()
+    print(f"graph replay: {t0.elapsed_time(t1) * 1e3 / reps:.1f} us per iteration ({reps} replays)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
