@@ -92,11 +92,18 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
   constexpr int PER = LOS_CAP_F / 256;
   // pixel-major tile: the K values of one pixel are adjacent (one or two
   // 16-byte LDS reads per entry instead of K 8-byte ones)
-#if NFT_LOS_UT
+#if NFT_LOS_UT == 1
   // vector-major tile: 8-byte reads of pixel l at bank 2 l mod 64 (the
   // pixel-major 32-byte rows put every pixel on one of 8 bank groups)
   __shared__ __align__(16) double ut[K][256];
 #define UAT(l, b) ut[b][l]
+#elif NFT_LOS_UT == 2
+  // pairs of vectors per 16-byte slot, one 256-slot array per pair: pixel l's
+  // slots start at bank quad l mod 16 in every array, so a 16-lane group of
+  // ds_read_b128 spreads over all 16 quads (the 32-byte pixel rows use 8)
+  constexpr int KP = K >= 2 ? K / 2 : 1;
+  __shared__ __align__(16) double ut[KP][256][K >= 2 ? 2 : 1];
+#define UAT(l, b) ut[(K >= 2 ? (b) >> 1 : 0)][l][K >= 2 ? ((b) & 1) : 0]
 #else
   __shared__ __align__(16) double u[256][K];
 #define UAT(l, b) u[l][b]

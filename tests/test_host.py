@@ -365,3 +365,53 @@ def test_abi_host_code_under_asan():
                        timeout=120, env=env)
     assert "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
     assert r.returncode == 0 and "abi host checks: ok" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
+def test_worth_compacting_host():
+    """FusedCGBatch compaction policy (fused_cg._worth_compacting): only with
+    fewer live rows than buffer rows, and only while some live controller
+    allows at least a few more iterations."""
+    import nifty_amd as ift
+    from nifty_amd.minimization.fused_cg import _worth_compacting
+    c = [ift.GradientNormController(iteration_limit=10) for _ in range(3)]
+    for x in c:
+        x._itcount = 5
+    assert not _worth_compacting(c, [0, 1, 2], 3)
+    assert _worth_compacting(c, [0, 2], 3)
+    for x in c:
+        x._itcount = 8
+    assert not _worth_compacting(c, [0, 2], 3)          # 2 iterations left
+    c[2] = ift.AbsDeltaEnergyController(0.1)            # no limit
+    c[2]._itcount = 50
+    assert _worth_compacting(c, [0, 2], 3)
+
+
+def test_trace_labels_host(tmp_path):
+    """tools/trace_labels.py: the periodic tail of a kernel trace is split
+    into iterations, dispatches labelled as bench.py labels them (the two
+    unpack passes by order), per-label means and the iteration span."""
+    import json
+    import subprocess
+    import sys
+    names = ["void nft::amp2::jvp2a_kernel<2>(x)", "void nft::fast::fast_kernel<double, 64, 256, 3, false, false>(a)",
+             "void nft::los_fwd_items<double, 4>(p)", "void nft::fast::fast_kernel<double, 64, 256, 3, false, false>(a)"]
+    rows, t = [], 0
+    for it in range(5):
+        for j, nm in enumerate(names):
+            d = 1000 * (j + 1)
+            rows.append((nm, t, t + d))
+            t += d + 100
+    f = tmp_path / "trace.csv"
+    with open(f, "w") as fh:
+        fh.write("Kernel_Name,Start_Timestamp,End_Timestamp\n")
+        for nm, a, b in rows:
+            fh.write(f"\"{nm}\",{a},{b}\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "trace_labels.py"), str(f), "3"],
+                         capture_output=True, text=True, check=True).stdout
+    d = json.loads(out)
+    assert d["dispatches_per_iteration"] == 4
+    lab = d["labels"]
+    assert lab["fft_unpack"]["avg_us"] == 2.0 and lab["fft_unpack+cg"]["avg_us"] == 4.0
+    assert lab["amp_jvp2a+dir"]["avg_us"] == 1.0 and lab["los_fwd_items"]["avg_us"] == 3.0
+    assert d["iteration_span_us"] == 10.3
