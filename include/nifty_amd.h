@@ -163,6 +163,17 @@ int nft_bin_scatter_ordered(const void* in, const int* perm, const int* offsets,
  * rounding (the images are added in pairs). */
 int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
                       hipStream_t stream);
+/* The half-grid fold of nft_bin_fold_half written in bin-sorted order, the
+ * pre items of a cell adjacent: out[cpos[cell] * pre + p], cpos the inverse
+ * of the folded bin index's stable bin -> cell permutation (1 <= pre <= 8).
+ * nft_bin_sum_sorted: out[p * nbins + b] = sum over i in [offsets[b],
+ * offsets[b+1]) of in[i * pre + p], ascending i -- together bitwise the
+ * fold + nft_bin_scatter over the folded cell (PowerDistributor adjoint,
+ * src/operators/distributors.py:92-105, on the mirror-folded cell). */
+int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t pre, int ndim,
+                             const int64_t* shape, int dtype, hipStream_t stream);
+int nft_bin_sum_sorted(const void* in, const int* offsets, void* out, int64_t pre, int64_t nbins, int dtype,
+                       hipStream_t stream);
 int nft_bin_fold(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
                  hipStream_t stream);
 

@@ -41,6 +41,8 @@ SIGNATURES = {
     "nft_bin_chunk": (_i, []),
     "nft_bin_fold": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_fold_half": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
+    "nft_bin_fold_half_sorted": (_i, [_p, _p, _p, _i64, _i, _p, _i, _p]),
+    "nft_bin_sum_sorted": (_i, [_p, _p, _p, _i64, _i64, _i, _p]),
     "nft_bin_scatter_ordered": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
     "nft_csr_rowblocks": (_i, [_p, _i64, _p, _i64, ctypes.POINTER(_i64)]),
@@ -308,6 +310,26 @@ def bin_fold_half(src, out, pre, shape):
     require_device(src, out)
     sh = (ctypes.c_int64 * len(shape))(*shape)
     _check(lib.nft_bin_fold_half(ptr(src), ptr(out), pre, len(shape), sh, dtype_code(src.dtype), stream_ptr()))
+    return out
+
+
+def bin_fold_half_sorted(src, out, cpos, pre, shape):
+    """the half-grid fold in bin-sorted order, items of a cell adjacent:
+    out[cpos[cell] * pre + p] (nft_bin_fold_half_sorted)"""
+    lib = load()
+    require_device(src, out, cpos)
+    sh = (ctypes.c_int64 * len(shape))(*shape)
+    _check(lib.nft_bin_fold_half_sorted(ptr(src), ptr(out), ptr(cpos), pre, len(shape), sh, dtype_code(src.dtype),
+                                        stream_ptr()))
+    return out
+
+
+def bin_sum_sorted(src, offsets, out, pre, nbins):
+    """out[p, b] = sum over bin b's contiguous run of src[i * pre + p]
+    (nft_bin_sum_sorted)"""
+    lib = load()
+    require_device(src, offsets, out)
+    _check(lib.nft_bin_sum_sorted(ptr(src), ptr(offsets), ptr(out), pre, nbins, dtype_code(src.dtype), stream_ptr()))
     return out
 
 

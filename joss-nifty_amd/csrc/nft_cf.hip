@@ -1,3 +1,4 @@
+#include <algorithm>
 // Power-bin gather / scatter (PowerDistributor) for gfx950.
 //
 //   nft_bin_gather   out[p, i, q] = in[p, pindex[i], q]
@@ -305,6 +306,93 @@ __global__ __launch_bounds__(256) void bin_fold_half_rows(const T* __restrict__ 
   }
 }
 
+// The half-grid fold written in bin-sorted order, the items of a cell
+// adjacent: out[cpos[cell] * pre + p] (cpos = inverse of the folded index's
+// stable bin -> cell permutation).  One workgroup per cell row, all pre items
+// per thread (<= 8: one 8 pre-byte store per cell).  Summation order and
+// start value as in bin_fold_half_kernel (bitwise); bin_sum_sorted then sums
+// each bin over a contiguous run, in the order of bin_scatter_chunk.
+template <typename T, int PRE>
+__global__ __launch_bounds__(256) void bin_fold_half_sorted(const T* __restrict__ in, T* __restrict__ out,
+                                                            const int* __restrict__ cpos, FoldShape fs,
+                                                            long long nrows, long long nhalf, int pre) {
+  const int D = fs.d;
+  const long long hl = fs.h[D - 1];
+  for (long long o = blockIdx.x; o < nrows; o += gridDim.x) {
+    long long r = o;
+    long long q[FOLD_MAXD], m[FOLD_MAXD];
+    bool two[FOLD_MAXD];
+#pragma unroll
+    for (int a = FOLD_MAXD - 1; a >= 0; --a) {
+      q[a] = m[a] = 0;
+      two[a] = false;
+      if (a < D - 1) {
+        q[a] = r % fs.h[a];
+        r /= fs.h[a];
+        m[a] = fs.n[a] - q[a];
+        two[a] = q[a] != 0 && m[a] != q[a];
+      }
+    }
+    long long roff[1 << (FOLD_MAXD - 1)];
+    bool rok[1 << (FOLD_MAXD - 1)];
+#pragma unroll
+    for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s) {
+      bool ok = true;
+      long long idx = 0;
+#pragma unroll
+      for (int a = 0; a < FOLD_MAXD - 1; ++a) {
+        if (a >= D - 1) continue;
+        const bool hi = (s >> (FOLD_MAXD - 2 - a)) & 1;
+        ok = ok && (!hi || two[a]);
+        idx = idx * fs.n[a] + (hi ? m[a] : q[a]);
+      }
+      for (int a = D - 1; a < FOLD_MAXD - 1; ++a) ok = ok && !((s >> (FOLD_MAXD - 2 - a)) & 1);
+      rok[s] = ok;
+      roff[s] = idx * hl;
+    }
+    const int* __restrict__ cp = cpos + o * hl;
+    for (long long x = threadIdx.x; x < hl; x += blockDim.x) {
+      const long long dpos = (long long)cp[x] * pre;
+      T v[PRE][1 << (FOLD_MAXD - 1)];
+#pragma unroll
+      for (int p = 0; p < PRE; ++p)
+#pragma unroll
+        for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s)
+          v[p][s] = (p < pre && rok[s]) ? in[p * nhalf + roff[s] + x] : (T)0;
+#pragma unroll
+      for (int p = 0; p < PRE; ++p) {
+        if (p >= pre) break;
+        T acc = (T)0;
+#pragma unroll
+        for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s)
+          if (rok[s]) acc += v[p][s];
+        out[dpos + p] = acc;
+      }
+    }
+  }
+}
+
+// out[p * nbins + b] = sum of in[i * pre + p] over i in [offs[b], offs[b+1])
+// in ascending i, from 0 (the per-bin order of bin_scatter_chunk: bitwise)
+template <typename T, int PRE>
+__global__ __launch_bounds__(256) void bin_sum_sorted(const T* __restrict__ in, const int* __restrict__ offs,
+                                                      T* __restrict__ out, long long nbins, int pre) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbins) return;
+  const int a = offs[b], e = offs[b + 1];
+  T acc[PRE];
+#pragma unroll
+  for (int p = 0; p < PRE; ++p) acc[p] = (T)0;
+  for (int i = a; i < e; ++i) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p)
+      if (p < pre) acc[p] += in[(long long)i * pre + p];
+  }
+#pragma unroll
+  for (int p = 0; p < PRE; ++p)
+    if (p < pre) out[p * nbins + b] = acc[p];
+}
+
 // I: index type -- 32-bit when pre * nin < 2^31 (the usual case: cheaper
 // div/mod per element), 64-bit otherwise
 template <typename T, typename I>
@@ -496,6 +584,85 @@ int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const in
     set_last_error("nft_bin_fold_half: bad dtype");
     return NFT_ERR_ARG;
   }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t pre, int ndim,
+                             const int64_t* shape, int dtype, hipStream_t stream) {
+  if (ndim < 1 || ndim > FOLD_MAXD || pre < 1 || pre > 8 || !cpos) {
+    set_last_error("nft_bin_fold_half_sorted: need 1 <= ndim <= 3, 1 <= pre <= 8 and cpos");
+    return NFT_ERR_ARG;
+  }
+  FoldShape fs{};
+  fs.d = ndim;
+  fs.nin = 1;
+  fs.nout = 1;
+  for (int a = 0; a < FOLD_MAXD; ++a) fs.n[a] = fs.h[a] = 1;
+  long long nhalf = 1;
+  for (int a = 0; a < ndim; ++a) {
+    if (shape[a] < 1) {
+      set_last_error("nft_bin_fold_half_sorted: bad shape");
+      return NFT_ERR_ARG;
+    }
+    fs.n[a] = shape[a];
+    fs.h[a] = shape[a] / 2 + 1;
+    fs.nin *= shape[a];
+    fs.nout *= fs.h[a];
+    nhalf *= (a == ndim - 1) ? fs.h[a] : shape[a];
+  }
+  const long long nrows = fs.nout / fs.h[ndim - 1];
+  const unsigned grid = (unsigned)std::min<long long>(nrows, 1LL << 20);
+  prof_mark(stream, "bin_fold");
+#define NFT_FS(TT, PP)                                                                                     \
+  hipLaunchKernelGGL((bin_fold_half_sorted<TT, PP>), dim3(grid), dim3(256), 0, stream, (const TT*)in, (TT*)out, \
+                     cpos, fs, nrows, nhalf, (int)pre)
+  if (dtype == 0) {
+    if (pre <= 1) NFT_FS(double, 1);
+    else if (pre <= 2) NFT_FS(double, 2);
+    else if (pre <= 4) NFT_FS(double, 4);
+    else NFT_FS(double, 8);
+  } else if (dtype == 1) {
+    if (pre <= 1) NFT_FS(float, 1);
+    else if (pre <= 2) NFT_FS(float, 2);
+    else if (pre <= 4) NFT_FS(float, 4);
+    else NFT_FS(float, 8);
+  } else {
+    set_last_error("nft_bin_fold_half_sorted: bad dtype");
+    return NFT_ERR_ARG;
+  }
+#undef NFT_FS
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_bin_sum_sorted(const void* in, const int* offsets, void* out, int64_t pre, int64_t nbins, int dtype,
+                       hipStream_t stream) {
+  if (pre < 1 || pre > 8 || nbins < 0 || !offsets) {
+    set_last_error("nft_bin_sum_sorted: need 1 <= pre <= 8, nbins >= 0 and offsets");
+    return NFT_ERR_ARG;
+  }
+  if (nbins == 0) return NFT_OK;
+  prof_mark(stream, "bin_scatter");
+  const unsigned grid = (unsigned)((nbins + 255) / 256);
+#define NFT_BS(TT, PP)                                                                                        \
+  hipLaunchKernelGGL((bin_sum_sorted<TT, PP>), dim3(grid), dim3(256), 0, stream, (const TT*)in, offsets, (TT*)out, \
+                     (long long)nbins, (int)pre)
+  if (dtype == 0) {
+    if (pre <= 1) NFT_BS(double, 1);
+    else if (pre <= 2) NFT_BS(double, 2);
+    else if (pre <= 4) NFT_BS(double, 4);
+    else NFT_BS(double, 8);
+  } else if (dtype == 1) {
+    if (pre <= 1) NFT_BS(float, 1);
+    else if (pre <= 2) NFT_BS(float, 2);
+    else if (pre <= 4) NFT_BS(float, 4);
+    else NFT_BS(float, 8);
+  } else {
+    set_last_error("nft_bin_sum_sorted: bad dtype");
+    return NFT_ERR_ARG;
+  }
+#undef NFT_BS
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

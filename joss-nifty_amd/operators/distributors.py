@@ -25,6 +25,14 @@ def _chunk_bins(offs, nbin, npix):
     return cb.astype(np.int32)
 
 
+class _SortedFold:
+    """fold_into's result in bin-sorted order (nf, pre): scatter_from sums
+    contiguous runs"""
+
+    def __init__(self, t):
+        self.t = t
+
+
 class BinIndex:
     """Device-resident bin index: pindex (int32) plus the stable bin->pixel
     permutation and CSR offsets for the adjoint.  Built once on the host."""
@@ -70,7 +78,10 @@ class BinIndex:
         offs = np.zeros(self.nbin + 1, dtype=np.int64)
         np.cumsum(np.bincount(f, minlength=self.nbin), out=offs[1:])
         cb = _chunk_bins(offs, self.nbin, f.size)
+        cpos = np.empty(f.size, dtype=np.int32)
+        cpos[perm] = np.arange(f.size, dtype=np.int32)
         return dict(shape=tuple(int(n) for n in shp), nf=int(f.size),
+                    cpos=torch.from_numpy(cpos).to(device),                   # cell -> sorted position
                     pindex=torch.from_numpy(f.astype(np.int32)).to(device),   # cell -> bin
                     perm=torch.from_numpy(perm.astype(np.int32)).to(device),
                     offsets=torch.from_numpy(offs.astype(np.int32)).to(device),
@@ -100,16 +111,25 @@ class BinIndex:
         return _native.bin_scatter(wf, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
                                    order=f["order"])
 
+    # the half-grid fold written in bin-sorted order and contiguous bin sums
+    # (nft_bin_fold_half_sorted + nft_bin_sum_sorted; NFT_BIN_SORTED=0: fold
+    # in cell order + gathering scatter) -- bitwise the same sums
+    SORTED = os.environ.get("NFT_BIN_SORTED", "1") != "0"
+
     def fold_into(self, w, wf, pre, half=False):
         """first half of scatter: the mirror fold of w into wf (pre, nf);
         returns the operand of scatter_from (wf, or w without a fold).
         half: w holds point-mirror pair sums on the half grid
-        (nft_hartley_fuse.epi_out2_pairs)"""
+        (nft_hartley_fuse.epi_out2_pairs); then, for pre <= 8, wf receives
+        the fold in bin-sorted order (nf, pre) and the operand is tagged so"""
         f = self.fold
         if f is None:
             if half:
                 raise ValueError("pair sums need the folded bin index")
             return w
+        if half and self.SORTED and 1 <= pre <= 8:
+            _native.bin_fold_half_sorted(w, wf, f["cpos"], pre, f["shape"])
+            return _SortedFold(wf)
         (_native.bin_fold_half if half else _native.bin_fold)(w, wf, pre, f["shape"])
         return wf
 
@@ -119,6 +139,8 @@ class BinIndex:
         if f is None:
             return _native.bin_scatter(src, self.perm, self.offsets, out, pre, self.npix, self.nbin, 1,
                                        order=self.gather_order)
+        if isinstance(src, _SortedFold):
+            return _native.bin_sum_sorted(src.t, f["offsets"], out, pre, self.nbin)
         return _native.bin_scatter(src, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
                                    order=f["order"])
 
