@@ -333,6 +333,11 @@ typedef struct nft_los_plan {
    * its slots through slot_seg -- the same values summed in the same order
    * (bitwise the line-major layout). */
   const int* slot_seg;
+  /* optional (NULL: one workgroup per work item): the work items of every
+   * box, items box_item[b] .. box_item[b+1] - 1 (nbox + 1 entries).  Then the
+   * batched forward runs one workgroup per box, the pixel tile staged once
+   * for all of the box's items (same products and order: bitwise). */
+  const int* box_item;
 } nft_los_plan;
 
 size_t nft_los_workspace(const nft_los_plan* plan);

@@ -105,7 +105,7 @@ class LosPlan(ctypes.Structure):
                 ("nbox", _i64), ("nlos", _i64), ("nitems", _i64), ("nseg", _i64)] + \
                [(n, _p) for n in ("item_box", "item_seg", "item_ent", "seg_ent", "seg_slot", "ent_loc", "ent_wf",
                                   "los_ptr", "box_ent", "pix_off", "box_lptr", "box_lines", "ent_lidx")] + \
-               [("lidx8", _i), ("ent_wa", _p), ("slot_seg", _p)]
+               [("lidx8", _i), ("ent_wa", _p), ("slot_seg", _p), ("box_item", _p)]
 
 
 class AmpConst(ctypes.Structure):

@@ -223,6 +223,139 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
   for (int s = sq + 64 * RND; s < s1; s += 64)
     segk(segmaj ? s : p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
 }
+
+// One workgroup per box (nft_los_plan.box_item given, K > 1): the pixel
+// tile's loads depend on the box index only, so they issue at once, beside
+// the box's segment / entry bounds (one workgroup per work item waits for
+// item_box first); a box of several work items (> LOS_CAP_F entries or > 256
+// segments) loops over them with the tile staged once (per item the items
+// kernel re-reads it: 20.5k items over 16.4k boxes at 2048^2 / 16384 lines).
+// Per segment and vector the products and their order are los_fwd_items'
+// (bitwise).  remap: XCD-contiguous box order.
+template <typename T, int K>
+__global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __restrict__ x,
+                                                     const T* __restrict__ cs, double* __restrict__ part,
+                                                     long long xs, int pk, long long css, int remap) {
+#pragma clang fp contract(off)
+  static_assert(K > 1, "one vector takes los_fwd_items");
+  constexpr int PER = LOS_CAP_F / 256;
+  constexpr int RND = LOS_SEG_ROUNDS;
+#if NFT_LOS_UT == 1
+  __shared__ __align__(16) double ut[K][256];
+#elif NFT_LOS_UT == 2
+  constexpr int KP = K / 2;
+  __shared__ __align__(16) double ut[KP][256][2];
+#else
+  __shared__ __align__(16) double u[256][K];
+#endif
+  __shared__ float ew[LOS_CAP_F];
+  __shared__ unsigned char el[LOS_CAP_F];
+  const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
+  const int box = remap ? xcd_unit(blockIdx.x, (int)p.nbox) : (int)blockIdx.x;
+  if (box >= p.nbox) return;
+  const int t = threadIdx.x;
+  bool ok;
+  const long long px = g.pixel(box, t, ok);
+  double xv[K];
+#pragma unroll
+  for (int b = 0; b < K; ++b) {
+    double v = 0.0;
+    if (ok) {
+      v = (double)x[b * xs + px];
+      if (cs) v *= (double)cs[b * css + px];
+    }
+    xv[b] = v;
+  }
+  const int bs0 = p.box_lptr[box], bs1 = p.box_lptr[box + 1];
+  const int be0 = p.box_ent[box], be1 = p.box_ent[box + 1];
+  const bool multi = (be1 - be0 > LOS_CAP_F) || (bs1 - bs0 > 256);
+  int ci = 0, ci1 = 0;
+  int s0 = bs0, s1 = bs1, e0 = be0, e1 = be1;
+  if (multi) {
+    ci = p.box_item[box];
+    ci1 = p.box_item[box + 1];
+    s1 = p.item_seg[ci + 1];
+    e1 = p.item_ent[ci + 1];
+  }
+  const int sub = t & 3;
+  for (bool first = true;; first = false) {
+    const int n = e1 - e0;
+    float wv[PER];
+    unsigned char lv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = t + i * 256;
+      wv[i] = k < n ? p.ent_wf[e0 + k] : 0.f;
+      lv[i] = k < n ? p.ent_loc[e0 + k] : 0;
+    }
+    const int sq = s0 + (t >> 2);
+    int sa[RND], sb[RND], so[RND];
+#pragma unroll
+    for (int r = 0; r < RND; ++r) {
+      const int s = sq + 64 * r;
+      sa[r] = s < s1 ? p.seg_ent[s] - e0 : 0;
+      sb[r] = s < s1 ? p.seg_ent[s + 1] - e0 : 0;
+      so[r] = s < s1 ? p.seg_slot[s] : 0;
+    }
+    if (first) {
+#if NFT_LOS_UT == 1
+#pragma unroll
+      for (int b = 0; b < K; ++b) ut[b][t] = xv[b];
+#elif NFT_LOS_UT == 2
+#pragma unroll
+      for (int b = 0; b < K; ++b) ut[b >> 1][t][b & 1] = xv[b];
+#else
+#pragma unroll
+      for (int b = 0; b < K; ++b) u[t][b] = xv[b];
+#endif
+    } else {
+      __syncthreads();  // the previous item's entries are read
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = t + i * 256;
+      if (k < n) {
+        ew[k] = wv[i];
+        el[k] = lv[i];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RND; ++r) {
+      if (sq + 64 * r < s1) {
+        double acc[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) acc[b] = 0.0;
+        for (int k = sa[r] + sub; k < sb[r]; k += 4) {
+          const double w = (double)ew[k];
+          const int l = el[k];
+#if NFT_LOS_UT == 1
+#pragma unroll
+          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * ut[b][l];
+#elif NFT_LOS_UT == 2
+#pragma unroll
+          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * ut[b >> 1][l][b & 1];
+#else
+#pragma unroll
+          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
+#endif
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+          double v = acc[b];
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          if ((b & 3) == sub) part[(long long)so[r] * pk + b] = v;
+        }
+      }
+    }
+    if (!multi || ++ci >= ci1) break;
+    s0 = s1;
+    e0 = e1;
+    s1 = p.item_seg[ci + 1];
+    e1 = p.item_ent[ci + 1];
+  }
+}
 #undef UAT
 
 // one wave per line of sight, all K vectors: the line's slots (boxes
@@ -561,6 +694,14 @@ template <typename T, int K>
 static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* part, long long xs, int pk,
                         long long css, hipStream_t s) {
   if constexpr (K > 1) {
+    if (p->box_item && !p->slot_seg) {
+      // NFT_LOS_BOX_REMAP (tuning probe, read per launch): XCD-contiguous box order
+      const char* rm = getenv("NFT_LOS_BOX_REMAP");
+      const int remap = rm ? atoi(rm) : 0;
+      const unsigned grid = remap ? (unsigned)(8 * ((p->nbox + 7) / 8)) : (unsigned)p->nbox;
+      hipLaunchKernelGGL((los_fwd_boxes<T, K>), dim3(grid), dim3(256), 0, s, *p, x, cs, part, xs, pk, css, remap);
+      return;
+    }
     // opt-in (NFT_LOS_PF=1, NFT_LOS_PF_WG workgroups per CU, default 8):
     // measured slower at 4 x 2048^2 / 16384 lines (CG iteration 1257 ->
     // 1310 / 1306 / 1291 us at 8 / 4 / 16 workgroups per CU) -- one item per

@@ -141,6 +141,10 @@ LOS_CAP_F = 2048   # entries per forward work item (csrc/nft_los.hip)
 # 16384 lines: items 131 -> 111 us, reduce 14 -> 45 us (random 32-byte
 # gathers): off by default, line-major slots
 SEG_MAJOR = os.environ.get("NFT_LOS_SEG_MAJOR", "0") == "1"
+# batched forward with one workgroup per box (nft_los_plan.box_item): the
+# pixel tile's loads issue beside the box metadata and a box of several work
+# items stages it once (NFT_LOS_BOX_WG=0: one workgroup per work item)
+BOX_WG = os.environ.get("NFT_LOS_BOX_WG", "1") != "0"
 LOS_KMAX = 8       # vectors per batched LOS launch (csrc/nft_los.hip)
 BOX = 256
 
@@ -203,6 +207,8 @@ def box_plan(rows, cols, w, shape, nlos):
             item_seg.append(s)
             s = e
     item_seg.append(nseg)
+    # the work items of every box (items are appended in box order)
+    box_item = np.r_[0, np.cumsum(np.bincount(np.asarray(item_box, dtype=np.int64), minlength=nbox))].astype(np.int32)
     # partial slots in line-major order (boxes ascending within a line)
     olm = np.lexsort((seg_box, seg_los))
     seg_slot = np.empty(nseg, dtype=np.int32)
@@ -234,7 +240,7 @@ def box_plan(rows, cols, w, shape, nlos):
                 item_ent=seg_ent[np.asarray(item_seg, dtype=np.int64)].astype(np.int32),
                 seg_ent=seg_ent, seg_slot=seg_slot, slot_seg=slot_seg, ent_loc=loc[of].astype(np.uint8),
                 ent_wf=wf[of],
-                los_ptr=los_ptr, box_ent=np.r_[0, np.cumsum(entcnt)].astype(np.int32), pix_off=pix_off,
+                box_item=box_item, los_ptr=los_ptr, box_ent=np.r_[0, np.cumsum(entcnt)].astype(np.int32), pix_off=pix_off,
                 box_lptr=box_lptr, box_lines=seg_los.astype(np.int32),
                 ent_lidx=lidx.astype(np.uint8 if lidx8 else np.uint16), lidx8=int(lidx8), ent_wa=wf[oa])
 
@@ -304,7 +310,7 @@ class LOSResponse(LinearOperator):
             for k in ("H", "W", "bh", "bw", "nby", "nbx", "nbox", "nlos", "nitems", "nseg", "lidx8"):
                 setattr(d, k, int(P[k]))
             for k, v in keep.items():
-                if k == "slot_seg" and not SEG_MAJOR:
+                if (k == "slot_seg" and not SEG_MAJOR) or (k == "box_item" and not BOX_WG):
                     continue
                 setattr(d, k, v.data_ptr() if v.numel() else None)
             self._plan = (d, keep)

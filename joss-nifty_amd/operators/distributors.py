@@ -112,9 +112,10 @@ class BinIndex:
                                    order=f["order"])
 
     # the half-grid fold written in bin-sorted order and contiguous bin sums
-    # (nft_bin_fold_half_sorted + nft_bin_sum_sorted; NFT_BIN_SORTED=0: fold
-    # in cell order + gathering scatter) -- bitwise the same sums
-    SORTED = os.environ.get("NFT_BIN_SORTED", "1") != "0"
+    # (nft_bin_fold_half_sorted + nft_bin_sum_sorted, NFT_BIN_SORTED=1) --
+    # bitwise the fold in cell order + gathering scatter.  Measured at 4 x
+    # 2048^2: fold 27.5 -> 64 us (its stores scatter), sums 35 -> 32 us: off
+    SORTED = os.environ.get("NFT_BIN_SORTED", "0") == "1"
 
     def fold_into(self, w, wf, pre, half=False):
         """first half of scatter: the mirror fold of w into wf (pre, nf);

@@ -1,6 +1,7 @@
 """LOS forward / adjoint timing on the bench's plan (2048^2, 16384 lines,
-K = 4 vectors, per-vector column scale as in the sampling metric); with
-NFT_LOS_DBG ablations of the items kernel (tuning probe only)."""
+K = 4 vectors, per-vector column scale as in the sampling metric): one
+workgroup per work item vs one per box (NFT_LOS_BOX_REMAP: XCD-contiguous box
+order), bitwise checked against each other (tuning probe only)."""
 import os
 import sys
 
@@ -28,40 +29,37 @@ def main():
     from nifty_amd import _native as nat
     ift.config.set_device("cuda:0")
     cf, R, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
-    plan = R._box_plan()
     k = 4
     N = 2048 * 2048
     X = torch.randn((k, N), dtype=torch.float64, device="cuda")
-    cs = torch.rand(N, dtype=torch.float64, device="cuda")
+    cs = torch.rand((k, N), dtype=torch.float64, device="cuda")
     y = torch.empty((k, R.target.shape[0]), dtype=torch.float64, device="cuda")
     out = torch.empty_like(X)
     from nifty_amd.library import los_response
     ref = None
-    for segmaj in (False, True):
-        los_response.SEG_MAJOR = segmaj
+    for name, boxwg, remap in (("items", False, "0"), ("boxes", True, "0"), ("boxes_remap", True, "1")):
+        los_response.BOX_WG = boxwg
+        os.environ["NFT_LOS_BOX_REMAP"] = remap
         R._plan = None
         plan = R._box_plan()
-        nat.los_forward_batched(plan, X, y, colscale=cs)
+        y.zero_()
+        nat.los_forward_ex(plan, X, y, colscale=cs, colscale_stride=N)
         if ref is None:
             ref = y.clone()
         else:
-            print(f"segment-major bitwise equal: {bool(torch.equal(ref, y))}", flush=True)
-        for dbg in os.environ.get("LOS_DBGS", "0,1,2").split(","):
-            os.environ["NFT_LOS_DBG"] = dbg
-            us = timed(lambda: nat.los_forward_batched(plan, X, y, colscale=cs))
-            print(f"fwd segmaj={int(segmaj)} dbg={dbg} {us:.1f} us", flush=True)
-        os.environ["NFT_LOS_DBG"] = "0"
+            print(f"{name} bitwise equal: {bool(torch.equal(ref, y))}", flush=True)
+        for rep in range(2):
+            us = timed(lambda: nat.los_forward_ex(plan, X, y, colscale=cs, colscale_stride=N))
+            print(f"fwd {name} {us:.1f} us", flush=True)
         with nat.LaunchProfile() as prof:
             for _ in range(10):
-                nat.los_forward_batched(plan, X, y, colscale=cs)
+                nat.los_forward_ex(plan, X, y, colscale=cs, colscale_stride=N)
         acc = {}
         for lab, ms in prof.records:
             acc.setdefault(lab, []).append(ms * 1e3)
         print("   " + ", ".join(f"{k} {sum(v) / len(v):.1f} us" for k, v in acc.items()), flush=True)
-    os.environ["NFT_LOS_DBG"] = "0"
-    for ax in ("0", "1"):
-        os.environ["NFT_LOS_ADJ_XCD"] = ax
-        print(f"adj xcd={ax} {timed(lambda: nat.los_adjoint_batched(plan, y, out, rowscale=cs)):.1f} us", flush=True)
+    os.environ["NFT_LOS_BOX_REMAP"] = "0"
+    print(f"adj {timed(lambda: nat.los_adjoint_batched(plan, y, out, rowscale=cs[0])):.1f} us", flush=True)
 
 
 if __name__ == "__main__":
