@@ -338,6 +338,19 @@ typedef struct nft_los_plan {
    * batched forward runs one workgroup per box, the pixel tile staged once
    * for all of the box's items (same products and order: bitwise). */
   const int* box_item;
+  /* optional (ntile = 0: partials per (line, box) segment): tiles of
+   * tile_S x tile_S boxes.  The forward then runs one workgroup per tile:
+   * tile_items[tile_iptr[T] .. tile_iptr[T+1]) are its work items in
+   * processing order (boxes in raster order), tile_lptr the CSR of the lines
+   * crossing it (at most tl_max per tile), seg_tl[s] segment s's index into
+   * its tile's line list; each line's segment sums are accumulated in LDS in
+   * that order and stored once per (line, tile) at tl_slot[tile_lptr[T] + j]
+   * (line-major slots; los_ptr then points at their line CSR). */
+  int tile_S;
+  int64_t ntile;
+  int tl_max;
+  const int *tile_iptr, *tile_items, *tile_lptr, *tl_slot;
+  const uint16_t* seg_tl;
 } nft_los_plan;
 
 size_t nft_los_workspace(const nft_los_plan* plan);

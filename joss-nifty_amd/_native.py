@@ -105,7 +105,9 @@ class LosPlan(ctypes.Structure):
                 ("nbox", _i64), ("nlos", _i64), ("nitems", _i64), ("nseg", _i64)] + \
                [(n, _p) for n in ("item_box", "item_seg", "item_ent", "seg_ent", "seg_slot", "ent_loc", "ent_wf",
                                   "los_ptr", "box_ent", "pix_off", "box_lptr", "box_lines", "ent_lidx")] + \
-               [("lidx8", _i), ("ent_wa", _p), ("slot_seg", _p), ("box_item", _p)]
+               [("lidx8", _i), ("ent_wa", _p), ("slot_seg", _p), ("box_item", _p),
+                ("tile_S", _i), ("ntile", _i64), ("tl_max", _i)] + \
+               [(n, _p) for n in ("tile_iptr", "tile_items", "tile_lptr", "tl_slot", "seg_tl")]
 
 
 class AmpConst(ctypes.Structure):

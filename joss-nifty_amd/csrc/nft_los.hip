@@ -358,6 +358,131 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
 }
 #undef UAT
 
+// One workgroup per tile of tile_S x tile_S boxes (nft_los_plan.ntile > 0):
+// the tile's work items in order (boxes in raster order), each staged and
+// summed per segment as in los_fwd_items, the segment sums added to the
+// line's LDS accumulator (a line has one segment per box, so one add per
+// line and box, boxes in order: a fixed order); one partial per (line, tile)
+// leaves the workgroup at the end.  The next item's entries, segment bounds
+// and (on a new box) pixel values are loaded into registers while the
+// current one is summed.  Every K (1 included) takes this kernel when the
+// plan has tiles: per vector the arithmetic does not depend on K (bitwise).
+template <typename T, int K>
+__global__ __launch_bounds__(256) void los_fwd_tiles(nft_los_plan p, const T* __restrict__ x,
+                                                     const T* __restrict__ cs, double* __restrict__ part,
+                                                     long long xs, int pk, long long css) {
+#pragma clang fp contract(off)
+  constexpr int PER = LOS_CAP_F / 256;
+  constexpr int RND = LOS_SEG_ROUNDS;
+  __shared__ __align__(16) double u[256][K];
+  __shared__ float ew[LOS_CAP_F];
+  __shared__ unsigned char el[LOS_CAP_F];
+  extern __shared__ __align__(16) double tacc[];  // [lines of the tile][K]
+  const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
+  const int tile = blockIdx.x, t = threadIdx.x, sub = t & 3;
+  const int i0 = p.tile_iptr[tile], i1 = p.tile_iptr[tile + 1];
+  const int l0 = p.tile_lptr[tile], ntl = p.tile_lptr[tile + 1] - l0;
+  for (int j = t; j < ntl * K; j += 256) tacc[j] = 0.0;
+  // the item in flight (registers)
+  int nbox = -1, ns0 = 0, ns1 = 0, ne0 = 0, nn = 0;
+  float wv[PER];
+  unsigned char lv[PER];
+  double xv[K];
+  int san[RND], sbn[RND], stn[RND];
+  auto load = [&](int ii, int prev) {
+    const int it = p.tile_items[ii];
+    nbox = p.item_box[it];
+    ns0 = p.item_seg[it];
+    ns1 = p.item_seg[it + 1];
+    ne0 = p.item_ent[it];
+    nn = p.item_ent[it + 1] - ne0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = t + i * 256;
+      wv[i] = k < nn ? p.ent_wf[ne0 + k] : 0.f;
+      lv[i] = k < nn ? p.ent_loc[ne0 + k] : 0;
+    }
+    if (nbox != prev) {
+      bool ok;
+      const long long px = g.pixel(nbox, t, ok);
+#pragma unroll
+      for (int b = 0; b < K; ++b) {
+        double v = 0.0;
+        if (ok) {
+          v = (double)x[b * xs + px];
+          if (cs) v *= (double)cs[b * css + px];
+        }
+        xv[b] = v;
+      }
+    }
+    const int sq = ns0 + (t >> 2);
+#pragma unroll
+    for (int r = 0; r < RND; ++r) {
+      const int s = sq + 64 * r;
+      san[r] = s < ns1 ? p.seg_ent[s] - ne0 : 0;
+      sbn[r] = s < ns1 ? p.seg_ent[s + 1] - ne0 : 0;
+      stn[r] = s < ns1 ? (int)p.seg_tl[s] : 0;
+    }
+  };
+  int cbox = -1;
+  if (i0 < i1) load(i0, -1);
+  for (int ii = i0; ii < i1; ++ii) {
+    const int s0 = ns0, s1 = ns1, n = nn;
+    const bool newbox = nbox != cbox;
+    cbox = nbox;
+    int sa[RND], sb[RND], st[RND];
+#pragma unroll
+    for (int r = 0; r < RND; ++r) {
+      sa[r] = san[r];
+      sb[r] = sbn[r];
+      st[r] = stn[r];
+    }
+    __syncthreads();  // the previous item's LDS reads (and the accumulator zeroing) are done
+    if (newbox) {
+#pragma unroll
+      for (int b = 0; b < K; ++b) u[t][b] = xv[b];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = t + i * 256;
+      if (k < n) {
+        ew[k] = wv[i];
+        el[k] = lv[i];
+      }
+    }
+    __syncthreads();
+    if (ii + 1 < i1) load(ii + 1, cbox);  // in flight while this item is summed
+    const int sq = s0 + (t >> 2);
+#pragma unroll
+    for (int r = 0; r < RND; ++r) {
+      if (sq + 64 * r < s1) {
+        double acc[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) acc[b] = 0.0;
+        for (int k = sa[r] + sub; k < sb[r]; k += 4) {
+          const double w = (double)ew[k];
+          const int l = el[k];
+#pragma unroll
+          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+          double v = acc[b];
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          if ((b & 3) == sub) tacc[st[r] * K + b] += v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int j = t; j < ntl; j += 256) {
+    double* dst = part + (long long)p.tl_slot[l0 + j] * pk;
+#pragma unroll
+    for (int b = 0; b < K; ++b) dst[b] = tacc[j * K + b];
+  }
+}
+
 // one wave per line of sight, all K vectors: the line's slots (boxes
 // ascending) hold K adjacent partials each; per vector a fixed-order sum
 // (lane strides, then a shuffle tree).  qpart (optional): per workgroup and
@@ -749,7 +874,26 @@ static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, c
                          double scale, int K, long long xs, long long ys, hipStream_t s, double* qpart = nullptr,
                          long long qstride = 0, long long css = 0) {
   prof_mark(s, "los_fwd_items");
-  if (p->nitems > 0) {
+  if (p->ntile > 0 && p->nitems > 0) {
+    for (int v = 0; v < K;) {
+      const int g = kgroup(K - v);
+      const T* xv = (const T*)x + v * xs;
+      const T* cv = cs ? (const T*)cs + v * css : nullptr;
+      double* pv = part + v;
+      const size_t lds = (size_t)p->tl_max * g * sizeof(double);
+      const dim3 grid((unsigned)p->ntile);
+#define NFT_TILES(KK)                                                                                  \
+  case KK:                                                                                             \
+    hipLaunchKernelGGL((los_fwd_tiles<T, KK>), grid, dim3(256), lds, s, *p, xv, cv, pv, xs, K, css); \
+    break;
+      switch (g) {
+        NFT_TILES(8) NFT_TILES(4) NFT_TILES(2) NFT_TILES(1)
+        default: break;
+      }
+#undef NFT_TILES
+      v += g;
+    }
+  } else if (p->nitems > 0) {
     for (int v = 0; v < K;) {
       const int g = kgroup(K - v);
       const T* xv = (const T*)x + v * xs;

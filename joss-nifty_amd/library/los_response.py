@@ -145,6 +145,13 @@ SEG_MAJOR = os.environ.get("NFT_LOS_SEG_MAJOR", "0") == "1"
 # pixel tile's loads issue beside the box metadata and a box of several work
 # items stages it once (NFT_LOS_BOX_WG=0: one workgroup per work item)
 BOX_WG = os.environ.get("NFT_LOS_BOX_WG", "1") != "0"
+# forward partials per (line, tile of TILE x TILE boxes) instead of per
+# (line, box): the tile's workgroup sums each line's box segments in LDS
+# (boxes in raster order within the tile) and stores one partial per line
+# crossing the tile -- fewer, and the line reduce reads fewer
+# (NFT_LOS_TILE=1: per-box partials)
+TILE = int(os.environ.get("NFT_LOS_TILE", "2"))
+TILE_LINES_MAX = 1024   # lines crossing one tile (LDS accumulators: lines x vectors x 8 B)
 LOS_KMAX = 8       # vectors per batched LOS launch (csrc/nft_los.hip)
 BOX = 256
 
@@ -234,7 +241,8 @@ def box_plan(rows, cols, w, shape, nlos):
         raise ValueError("more than 65535 lines of sight cross one 256-pixel box")
     lidx8 = segcnt.max(initial=0) <= 256
     wf = np.asarray(w, dtype=np.float32)
-    return dict(H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
+    tiles = _tile_plan(seg_box, seg_los, np.asarray(item_box, dtype=np.int64), L, nby, nbx, int(nlos), TILE)
+    return dict(tiles, H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
                 nitems=len(item_box), nseg=nseg, L=L,
                 item_box=np.asarray(item_box, dtype=np.int32), item_seg=np.asarray(item_seg, dtype=np.int32),
                 item_ent=seg_ent[np.asarray(item_seg, dtype=np.int64)].astype(np.int32),
@@ -243,6 +251,41 @@ def box_plan(rows, cols, w, shape, nlos):
                 box_item=box_item, los_ptr=los_ptr, box_ent=np.r_[0, np.cumsum(entcnt)].astype(np.int32), pix_off=pix_off,
                 box_lptr=box_lptr, box_lines=seg_los.astype(np.int32),
                 ent_lidx=lidx.astype(np.uint8 if lidx8 else np.uint16), lidx8=int(lidx8), ent_wa=wf[oa])
+
+
+def _tile_plan(seg_box, seg_los, item_box, L, nby, nbx, nlos, S):
+    """Tiles of S x S boxes for the forward (nft_los_plan.tile_*): the work
+    items of every tile in processing order (boxes in raster order within the
+    tile), the lines crossing it (ascending), every segment's index into its
+    tile's line list, and the partial slot of every (tile, line) pair in
+    line-major order (tiles ascending within a line) with its line CSR."""
+    if S <= 1:
+        return dict(tile_S=1, ntile=0)
+    nty, ntx = -(-nby // S), -(-nbx // S)
+    ntile = L * nty * ntx
+    bl, br = np.divmod(np.arange(L * nby * nbx, dtype=np.int64), nby * nbx)
+    by, bx = np.divmod(br, nbx)
+    tile_of_box = (bl * nty + by // S) * ntx + bx // S
+    seg_tile = tile_of_box[seg_box]
+    key = seg_tile * nlos + seg_los
+    uk, inv = np.unique(key, return_inverse=True)
+    tl_tile, tl_line = uk // nlos, uk % nlos
+    tile_lptr = np.r_[0, np.cumsum(np.bincount(tl_tile, minlength=ntile))].astype(np.int64)
+    seg_tl = inv.reshape(-1) - tile_lptr[seg_tile]
+    olm = np.lexsort((tl_tile, tl_line))
+    tl_slot = np.empty(len(uk), dtype=np.int64)
+    tl_slot[olm] = np.arange(len(uk))
+    los_ptr_t = np.r_[0, np.cumsum(np.bincount(tl_line, minlength=nlos))]
+    item_tile = tile_of_box[item_box]
+    order = np.argsort(item_tile, kind="stable")
+    tile_iptr = np.r_[0, np.cumsum(np.bincount(item_tile, minlength=ntile))]
+    tl_max = int(np.diff(tile_lptr).max(initial=0))
+    if tl_max > TILE_LINES_MAX or len(uk) >= 2 ** 31 - 1:
+        return dict(tile_S=1, ntile=0)
+    return dict(tile_S=int(S), ntile=int(ntile), tl_max=tl_max,
+                tile_iptr=tile_iptr.astype(np.int32), tile_items=order.astype(np.int32),
+                tile_lptr=tile_lptr.astype(np.int32), seg_tl=seg_tl.astype(np.uint16),
+                tl_slot=tl_slot.astype(np.int32), los_ptr_tile=los_ptr_t.astype(np.int32))
 
 
 def box_plan_apply(P, x, mode):
@@ -261,16 +304,24 @@ def box_plan_apply(P, x, mode):
         return (lyr * H + yy) * W + xx, ok
     if mode == "times":
         x = x.reshape(-1)
-        part = np.zeros(P["nseg"])
-        for i in range(P["nitems"]):
+        tiled = P.get("ntile", 0) > 0
+        part = np.zeros(len(P["tl_slot"]) if tiled else P["nseg"])
+        items = P["tile_items"] if tiled else range(P["nitems"])
+        for i in items:
             p, ok = pix(int(P["item_box"][i]))
             u = np.where(ok, x[np.where(ok, p, 0)], 0.)
             for s in range(P["item_seg"][i], P["item_seg"][i + 1]):
                 acc = 0.
                 for k in range(P["seg_ent"][s], P["seg_ent"][s + 1]):
                     acc += float(P["ent_wf"][k]) * u[P["ent_loc"][k]]
-                part[P["seg_slot"][s]] = acc
-        return np.array([part[P["los_ptr"][i]:P["los_ptr"][i + 1]].sum() for i in range(nlos)])
+                if tiled:
+                    # the tile's line accumulator (items in tile order)
+                    t = int(np.searchsorted(P["tile_iptr"], np.flatnonzero(P["tile_items"] == i)[0], "right")) - 1
+                    part[P["tl_slot"][P["tile_lptr"][t] + P["seg_tl"][s]]] += acc
+                else:
+                    part[P["seg_slot"][s]] = acc
+        lp = P["los_ptr_tile"] if tiled else P["los_ptr"]
+        return np.array([part[lp[i]:lp[i + 1]].sum() for i in range(nlos)])
     out = np.zeros(P["L"] * H * W)
     for b in range(P["nbox"]):
         p, ok = pix(b)
@@ -307,12 +358,18 @@ class LOSResponse(LinearOperator):
             keep = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
                     for k, v in P.items() if isinstance(v, np.ndarray)}
             d = _native.LosPlan()
-            for k in ("H", "W", "bh", "bw", "nby", "nbx", "nbox", "nlos", "nitems", "nseg", "lidx8"):
-                setattr(d, k, int(P[k]))
+            for k in ("H", "W", "bh", "bw", "nby", "nbx", "nbox", "nlos", "nitems", "nseg", "lidx8", "ntile", "tile_S",
+                      "tl_max"):
+                setattr(d, k, int(P.get(k, 0)))
             for k, v in keep.items():
                 if (k == "slot_seg" and not SEG_MAJOR) or (k == "box_item" and not BOX_WG):
                     continue
+                if k == "los_ptr_tile":
+                    continue
                 setattr(d, k, v.data_ptr() if v.numel() else None)
+            if P.get("ntile", 0) > 0:
+                # the line reduce walks the (line, tile) slots
+                d.los_ptr = keep["los_ptr_tile"].data_ptr()
             self._plan = (d, keep)
         return self._plan[0]
 
