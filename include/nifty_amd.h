@@ -172,6 +172,12 @@ int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const in
  * src/operators/distributors.py:92-105, on the mirror-folded cell). */
 int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t pre, int ndim,
                              const int64_t* shape, int dtype, hipStream_t stream);
+/* cpos = NULL in nft_bin_fold_half_sorted: the fold in cell order with the
+ * pre items interleaved, out[cell * pre + p]; nft_bin_scatter_il then sums
+ * the bins of that layout (pre in {2, 4, 8}), one 8 pre-byte gather per
+ * cell for all items -- bitwise nft_bin_fold_half + nft_bin_scatter. */
+int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void* out, int64_t pre, int64_t npix,
+                       int64_t nbins, int dtype, hipStream_t stream);
 int nft_bin_sum_sorted(const void* in, const int* offsets, void* out, int64_t pre, int64_t nbins, int dtype,
                        hipStream_t stream);
 int nft_bin_fold(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,

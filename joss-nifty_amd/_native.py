@@ -43,6 +43,7 @@ SIGNATURES = {
     "nft_bin_fold_half": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_fold_half_sorted": (_i, [_p, _p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_sum_sorted": (_i, [_p, _p, _p, _i64, _i64, _i, _p]),
+    "nft_bin_scatter_il": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "nft_bin_scatter_ordered": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
     "nft_csr_rowblocks": (_i, [_p, _i64, _p, _i64, ctypes.POINTER(_i64)]),
@@ -319,10 +320,21 @@ def bin_fold_half_sorted(src, out, cpos, pre, shape):
     """the half-grid fold in bin-sorted order, items of a cell adjacent:
     out[cpos[cell] * pre + p] (nft_bin_fold_half_sorted)"""
     lib = load()
-    require_device(src, out, cpos)
+    require_device(src, out) if cpos is None else require_device(src, out, cpos)
     sh = (ctypes.c_int64 * len(shape))(*shape)
     _check(lib.nft_bin_fold_half_sorted(ptr(src), ptr(out), ptr(cpos), pre, len(shape), sh, dtype_code(src.dtype),
                                         stream_ptr()))
+    return out
+
+
+def bin_scatter_il(src, perm, offsets, out, pre, npix, nbins):
+    """out[p, b] = sum over bin b's cells of src[cell * pre + p] (the
+    interleaved fold of bin_fold_half_sorted with cpos None;
+    nft_bin_scatter_il)"""
+    lib = load()
+    require_device(src, perm, offsets, out)
+    _check(lib.nft_bin_scatter_il(ptr(src), ptr(perm), ptr(offsets), ptr(out), pre, npix, nbins,
+                                  dtype_code(src.dtype), stream_ptr()))
     return out
 
 

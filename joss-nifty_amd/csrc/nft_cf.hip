@@ -350,25 +350,102 @@ __global__ __launch_bounds__(256) void bin_fold_half_sorted(const T* __restrict_
       rok[s] = ok;
       roff[s] = idx * hl;
     }
-    const int* __restrict__ cp = cpos + o * hl;
-    for (long long x = threadIdx.x; x < hl; x += blockDim.x) {
-      const long long dpos = (long long)cp[x] * pre;
-      T v[PRE][1 << (FOLD_MAXD - 1)];
+    // FU values per thread in flight (all their loads before the stores)
+    constexpr int FU = PRE <= 4 ? 2 : 1;
+    for (long long x0 = threadIdx.x; x0 < hl; x0 += FU * (long long)blockDim.x) {
+      T v[FU][PRE][1 << (FOLD_MAXD - 1)];
 #pragma unroll
-      for (int p = 0; p < PRE; ++p)
+      for (int u = 0; u < FU; ++u) {
+        const long long x = x0 + u * (long long)blockDim.x;
 #pragma unroll
-        for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s)
-          v[p][s] = (p < pre && rok[s]) ? in[p * nhalf + roff[s] + x] : (T)0;
+        for (int p = 0; p < PRE; ++p)
 #pragma unroll
-      for (int p = 0; p < PRE; ++p) {
-        if (p >= pre) break;
-        T acc = (T)0;
+          for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s)
+            v[u][p][s] = (x < hl && p < pre && rok[s]) ? in[p * nhalf + roff[s] + x] : (T)0;
+      }
 #pragma unroll
-        for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s)
-          if (rok[s]) acc += v[p][s];
-        out[dpos + p] = acc;
+      for (int u = 0; u < FU; ++u) {
+        const long long x = x0 + u * (long long)blockDim.x;
+        if (x >= hl) break;
+        const long long dpos = (cpos ? (long long)cpos[o * hl + x] : o * hl + x) * pre;
+#pragma unroll
+        for (int p = 0; p < PRE; ++p) {
+          if (p >= pre) break;
+          T acc = (T)0;
+#pragma unroll
+          for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s)
+            if (rok[s]) acc += v[u][p][s];
+          out[dpos + p] = acc;
+        }
       }
     }
+  }
+}
+
+// The bin sums of the fold in cell order with the items interleaved
+// (bin_fold_half_sorted with cpos = NULL: in[cell * PRE + p]): chunks of CH
+// bin-sorted positions as in bin_scatter_chunk, one 8 PRE-byte gather per
+// position for all items (the planar layout gathers PRE cache lines), bins
+// summed in ascending position from 0 (bitwise bin_scatter_chunk).
+template <typename T, int PRE, int CH>
+__global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, const int* __restrict__ perm,
+                                                      const int* __restrict__ offs, T* __restrict__ out,
+                                                      long long npix, long long nbins, int nchunks) {
+  constexpr int PER = CH / 256;
+  __shared__ T vals[PRE][CH];
+  __shared__ int bnd[2];
+  const int per = (nchunks + NXCD - 1) / NXCD;
+  const int c = (int)(blockIdx.x % NXCD) * per + (int)(blockIdx.x / NXCD);
+  if (c >= nchunks) return;
+  const long long j0 = (long long)c * CH;
+  const int t = threadIdx.x;
+  const int n = (int)(npix - j0 < CH ? npix - j0 : CH);
+  int pv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = t + i * 256;
+    pv[i] = e < n ? perm[j0 + e] : 0;
+  }
+  T v[PER][PRE];
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) v[i][p] = t + i * 256 < n ? in[(long long)pv[i] * PRE + p] : (T)0;
+  if (t < 2) {
+    // first bin whose start offset is >= j0 (+ CH)
+    const long long target = j0 + (t ? CH : 0);
+    long long lo = 0, hi = nbins;
+    while (lo < hi) {
+      const long long mid = (lo + hi) >> 1;
+      if ((long long)offs[mid] < target) lo = mid + 1;
+      else hi = mid;
+    }
+    bnd[t] = (t && j0 + CH >= npix) ? (int)nbins : (int)lo;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+#pragma unroll
+    for (int p = 0; p < PRE; ++p)
+      if (t + i * 256 < n) vals[p][t + i * 256] = v[i][p];
+  __syncthreads();
+  const int b0 = bnd[0], b1 = bnd[1];
+  for (int b = b0 + t; b < b1; b += 256) {
+    const long long a = offs[b], e = offs[b + 1];
+    T acc[PRE];
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) acc[p] = (T)0;
+    for (long long j = a; j < e; ++j) {
+      if (j - j0 < CH) {
+#pragma unroll
+        for (int p = 0; p < PRE; ++p) acc[p] += vals[p][j - j0];
+      } else {
+        const long long q = (long long)perm[j] * PRE;
+#pragma unroll
+        for (int p = 0; p < PRE; ++p) acc[p] += in[q + p];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) out[p * nbins + b] = acc[p];
   }
 }
 
@@ -590,8 +667,8 @@ int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const in
 
 int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t pre, int ndim,
                              const int64_t* shape, int dtype, hipStream_t stream) {
-  if (ndim < 1 || ndim > FOLD_MAXD || pre < 1 || pre > 8 || !cpos) {
-    set_last_error("nft_bin_fold_half_sorted: need 1 <= ndim <= 3, 1 <= pre <= 8 and cpos");
+  if (ndim < 1 || ndim > FOLD_MAXD || pre < 1 || pre > 8) {
+    set_last_error("nft_bin_fold_half_sorted: need 1 <= ndim <= 3 and 1 <= pre <= 8");
     return NFT_ERR_ARG;
   }
   FoldShape fs{};
@@ -632,6 +709,39 @@ int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t
     return NFT_ERR_ARG;
   }
 #undef NFT_FS
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void* out, int64_t pre, int64_t npix,
+                       int64_t nbins, int dtype, hipStream_t stream) {
+  if (!(pre == 2 || pre == 4 || pre == 8) || npix < 0 || nbins < 0 || !perm || !offsets) {
+    set_last_error("nft_bin_scatter_il: need pre in {2, 4, 8}, perm and offsets");
+    return NFT_ERR_ARG;
+  }
+  if (nbins == 0) return NFT_OK;
+  if (npix == 0) {
+    NFT_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)pre * nbins * (dtype == 0 ? 8 : 4), stream));
+    return NFT_OK;
+  }
+  prof_mark(stream, "bin_scatter");
+#define NFT_SIL(TT, PP)                                                                                       \
+  {                                                                                                           \
+    constexpr int CH = 2048 / PP;                                                                             \
+    const int nch = (int)((npix + CH - 1) / CH);                                                              \
+    const unsigned nb = (unsigned)(((nch + NXCD - 1) / NXCD) * NXCD);                                         \
+    hipLaunchKernelGGL((bin_scatter_il<TT, PP, CH>), dim3(nb), dim3(256), 0, stream, (const TT*)in, perm, offsets, \
+                       (TT*)out, (long long)npix, (long long)nbins, nch);                                     \
+  }
+  if (dtype == 0) {
+    if (pre == 2) NFT_SIL(double, 2) else if (pre == 4) NFT_SIL(double, 4) else NFT_SIL(double, 8)
+  } else if (dtype == 1) {
+    if (pre == 2) NFT_SIL(float, 2) else if (pre == 4) NFT_SIL(float, 4) else NFT_SIL(float, 8)
+  } else {
+    set_last_error("nft_bin_scatter_il: bad dtype");
+    return NFT_ERR_ARG;
+  }
+#undef NFT_SIL
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

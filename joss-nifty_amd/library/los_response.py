@@ -146,11 +146,13 @@ SEG_MAJOR = os.environ.get("NFT_LOS_SEG_MAJOR", "0") == "1"
 # items stages it once (NFT_LOS_BOX_WG=0: one workgroup per work item)
 BOX_WG = os.environ.get("NFT_LOS_BOX_WG", "1") != "0"
 # forward partials per (line, tile of TILE x TILE boxes) instead of per
-# (line, box): the tile's workgroup sums each line's box segments in LDS
-# (boxes in raster order within the tile) and stores one partial per line
-# crossing the tile -- fewer, and the line reduce reads fewer
-# (NFT_LOS_TILE=1: per-box partials)
-TILE = int(os.environ.get("NFT_LOS_TILE", "2"))
+# (line, box), NFT_LOS_TILE=2 / 4: the tile's workgroup sums each line's box
+# segments in LDS (boxes in raster order within the tile) and stores one
+# partial per line crossing the tile.  Measured at 4 x 2048^2 / 16384 lines:
+# half / a quarter of the partials, but items 117 (one workgroup per box) ->
+# 155 / 235 us (a quarter of the workgroups, lower occupancy, one item after
+# the other per workgroup): off
+TILE = int(os.environ.get("NFT_LOS_TILE", "1"))
 TILE_LINES_MAX = 1024   # lines crossing one tile (LDS accumulators: lines x vectors x 8 B)
 LOS_KMAX = 8       # vectors per batched LOS launch (csrc/nft_los.hip)
 BOX = 256

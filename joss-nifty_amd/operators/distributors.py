@@ -33,6 +33,10 @@ class _SortedFold:
         self.t = t
 
 
+class _ILFold(_SortedFold):
+    """fold_into's result in cell order with the items interleaved (nf, pre)"""
+
+
 class BinIndex:
     """Device-resident bin index: pindex (int32) plus the stable bin->pixel
     permutation and CSR offsets for the adjoint.  Built once on the host."""
@@ -117,6 +121,12 @@ class BinIndex:
     # 2048^2: fold 27.5 -> 64 us (its stores scatter), sums 35 -> 32 us: off
     SORTED = os.environ.get("NFT_BIN_SORTED", "0") == "1"
 
+    # the half-grid fold with the items interleaved (bin_fold_half_sorted,
+    # cpos None) + bin sums gathering all items of a cell at once
+    # (nft_bin_scatter_il; NFT_BIN_IL=0: planar fold + per-item gathers) --
+    # bitwise the same sums
+    IL = os.environ.get("NFT_BIN_IL", "1") != "0"
+
     def fold_into(self, w, wf, pre, half=False):
         """first half of scatter: the mirror fold of w into wf (pre, nf);
         returns the operand of scatter_from (wf, or w without a fold).
@@ -131,6 +141,9 @@ class BinIndex:
         if half and self.SORTED and 1 <= pre <= 8:
             _native.bin_fold_half_sorted(w, wf, f["cpos"], pre, f["shape"])
             return _SortedFold(wf)
+        if half and self.IL and pre in (2, 4, 8):
+            _native.bin_fold_half_sorted(w, wf, None, pre, f["shape"])
+            return _ILFold(wf)
         (_native.bin_fold_half if half else _native.bin_fold)(w, wf, pre, f["shape"])
         return wf
 
@@ -140,6 +153,8 @@ class BinIndex:
         if f is None:
             return _native.bin_scatter(src, self.perm, self.offsets, out, pre, self.npix, self.nbin, 1,
                                        order=self.gather_order)
+        if isinstance(src, _ILFold):
+            return _native.bin_scatter_il(src.t, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin)
         if isinstance(src, _SortedFold):
             return _native.bin_sum_sorted(src.t, f["offsets"], out, pre, self.nbin)
         return _native.bin_scatter(src, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
