@@ -1,7 +1,7 @@
 """LOS forward / adjoint timing on the bench's plan (2048^2, 16384 lines,
-K = 4 vectors, per-vector column scale as in the sampling metric): one
-workgroup per work item vs one per box (NFT_LOS_BOX_REMAP: XCD-contiguous box
-order), bitwise checked against each other (tuning probe only)."""
+K = 4 vectors, one shared column scale as in the sampling metric): one
+workgroup per work item vs one per box, segments in (box, line) order vs
+longest first, bitwise checked against each other (tuning probe only)."""
 import os
 import sys
 
@@ -38,9 +38,11 @@ def main():
     from nifty_amd.library import los_response
     ref = None
     sp = R.domain[0]
-    for name, boxwg, tile in (("items", False, 1), ("boxes", True, 1), ("tiles2", True, 2), ("tiles4", True, 4)):
+    for name, boxwg, tile, srt in (("items_nosort", False, 1, False), ("items", False, 1, True),
+                                   ("boxes_nosort", True, 1, False), ("boxes", True, 1, True)):
         los_response.BOX_WG = boxwg
         los_response.TILE = tile
+        los_response.SORT_SEGMENTS = srt
         R._plan_np = los_response.box_plan(*R._coo, sp.shape, R.target.shape[0])
         R._plan = None
         plan = R._box_plan()
