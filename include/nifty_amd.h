@@ -357,6 +357,12 @@ typedef struct nft_los_plan {
   int tl_max;
   const int *tile_iptr, *tile_items, *tile_lptr, *tl_slot;
   const uint16_t* seg_tl;
+  /* optional (lpad = 0: none): the lines crossing every box at a fixed
+   * stride, box_lines_pad[b * lpad + i] = box_lines[box_lptr[b] + i], -1
+   * past the box's count (lpad <= 256).  The batched adjoint then stages its
+   * line table without waiting for box_lptr (one dependent load fewer). */
+  int lpad;
+  const int* box_lines_pad;
 } nft_los_plan;
 
 size_t nft_los_workspace(const nft_los_plan* plan);

@@ -590,6 +590,21 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int box = remap ? xcd_unit(blockIdx.x, p.nbox) : (int)blockIdx.x, t = threadIdx.x;
   if (box >= p.nbox) return;
+  // padded line table (K > 1, lpad <= 256 lines): staged from the box index
+  // alone, before the box bounds arrive; slot i of vector v at yl[v lpad + i]
+  const int lp = (K > 1 && p.lpad > 0 && p.lpad * K <= YL) ? p.lpad : 0;
+  if (lp) {
+    const int li = t < lp ? p.box_lines_pad[(long long)box * lp + t] : -1;
+    if (li >= 0) {
+      const double c = cs ? (double)cs[li] : 1.0;
+#pragma unroll
+      for (int v = 0; v < K; ++v) {
+        double yy = (double)yv[v * ys + li];
+        if (cs) yy *= c;
+        yl[v * lp + t] = yy;
+      }
+    }
+  }
   const int l0 = p.box_lptr[box], nl = p.box_lptr[box + 1] - l0;
   const int e0 = p.box_ent[box], n = p.box_ent[box + 1] - e0;
   const unsigned short* off = p.pix_off + (size_t)box * 257;
@@ -600,6 +615,7 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   double rsv[K];
 #pragma unroll
   for (int v = 0; v < K; ++v) rsv[v] = (rs && ok) ? (double)rs[v * rss + px] : 1.0;
+  const int ystr = lp ? lp : nl;  // line-table stride per vector
   // the first chunk's entry loads go out before the line-table staging so the
   // two dependent load chains overlap
   int lv[PER];
@@ -610,8 +626,8 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
     lv[i] = k < n ? (int)lidx[e0 + k] : 0;
     wv[i] = k < n ? p.ent_wa[e0 + k] : 0.f;
   }
-  const bool tab = nl * K <= YL;  // line values of this box (all vectors) cached in LDS
-  if (tab) {
+  const bool tab = lp || nl * K <= YL;  // line values of this box (all vectors) cached in LDS
+  if (tab && !lp) {
     for (int i = t; i < nl; i += 256) {
       const int li = p.box_lines[l0 + i];
       const double c = cs ? (double)cs[li] : 1.0;
@@ -675,7 +691,7 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
       const int li = el[k - c0];
       if (tab) {
 #pragma unroll
-        for (int v = 0; v < K; ++v) acc[v] = acc[v] + w * yl[v * nl + li];
+        for (int v = 0; v < K; ++v) acc[v] = acc[v] + w * yl[v * ystr + li];
       } else {
         const int gl = p.box_lines[l0 + li];
         const double cc = cs ? (double)cs[gl] : 1.0;

@@ -154,6 +154,11 @@ BOX_WG = os.environ.get("NFT_LOS_BOX_WG", "1") != "0"
 # the other per workgroup): off
 TILE = int(os.environ.get("NFT_LOS_TILE", "1"))
 TILE_LINES_MAX = 1024   # lines crossing one tile (LDS accumulators: lines x vectors x 8 B)
+# the lines crossing every box at a fixed stride (nft_los_plan.box_lines_pad,
+# NFT_LOS_ADJ_PAD=1): the batched adjoint stages its line table without
+# waiting for the box bounds (bitwise).  Measured at 4 x 2048^2: 98 -> 103 us
+# (a whole 1 KB row per box read): off
+ADJ_PAD = os.environ.get("NFT_LOS_ADJ_PAD", "0") == "1"
 # forward segments of a work item longest first (_longest_first,
 # NFT_LOS_SORT_SEG=1; bitwise).  Measured at 4 x 2048^2 / 16384 lines: one
 # workgroup per box 116 us either way (items 130 -> 128 us): off
@@ -247,6 +252,13 @@ def box_plan(rows, cols, w, shape, nlos):
         raise ValueError("more than 65535 lines of sight cross one 256-pixel box")
     lidx8 = segcnt.max(initial=0) <= 256
     wf = np.asarray(w, dtype=np.float32)
+    pad = {}
+    if ADJ_PAD and lidx8 and nseg:
+        lpad = int(-(-segcnt.max() // 64) * 64)
+        blp = np.full((nbox, lpad), -1, dtype=np.int32)
+        sb = np.repeat(np.arange(nbox), segcnt)
+        blp[sb, np.arange(nseg) - box_lptr[sb]] = seg_los
+        pad = dict(lpad=lpad, box_lines_pad=blp.reshape(-1))
     tiles = _tile_plan(seg_box, seg_los, np.asarray(item_box, dtype=np.int64), L, nby, nbx, int(nlos), TILE)
     item_seg = np.asarray(item_seg, dtype=np.int64)
     fwd = dict(seg_ent=seg_ent, seg_slot=seg_slot, slot_seg=slot_seg, ent_loc=loc[of].astype(np.uint8), ent_wf=wf[of])
@@ -254,7 +266,7 @@ def box_plan(rows, cols, w, shape, nlos):
         fwd["seg_tl"] = tiles.pop("seg_tl")
     if SORT_SEGMENTS and nseg:
         fwd = _longest_first(fwd, item_seg)
-    return dict(tiles, H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
+    return dict(tiles, **pad, H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
                 nitems=len(item_box), nseg=nseg, L=L,
                 item_box=np.asarray(item_box, dtype=np.int32), item_seg=item_seg.astype(np.int32),
                 item_ent=seg_ent[item_seg].astype(np.int32), **fwd,
@@ -396,7 +408,7 @@ class LOSResponse(LinearOperator):
                     for k, v in P.items() if isinstance(v, np.ndarray)}
             d = _native.LosPlan()
             for k in ("H", "W", "bh", "bw", "nby", "nbx", "nbox", "nlos", "nitems", "nseg", "lidx8", "ntile", "tile_S",
-                      "tl_max"):
+                      "tl_max", "lpad"):
                 setattr(d, k, int(P.get(k, 0)))
             for k, v in keep.items():
                 if (k == "slot_seg" and not SEG_MAJOR) or (k == "box_item" and not BOX_WG):

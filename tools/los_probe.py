@@ -38,8 +38,7 @@ def main():
     from nifty_amd.library import los_response
     ref = None
     sp = R.domain[0]
-    for name, boxwg, tile, srt in (("items_nosort", False, 1, False), ("items", False, 1, True),
-                                   ("boxes_nosort", True, 1, False), ("boxes", True, 1, True)):
+    for name, boxwg, tile, srt in (("items", False, 1, False), ("boxes", True, 1, False)):
         los_response.BOX_WG = boxwg
         los_response.TILE = tile
         los_response.SORT_SEGMENTS = srt
@@ -63,8 +62,19 @@ def main():
         for lab, ms in prof.records:
             acc.setdefault(lab, []).append(ms * 1e3)
         print("   " + ", ".join(f"{k} {sum(v) / len(v):.1f} us" for k, v in acc.items()), flush=True)
-    os.environ["NFT_LOS_BOX_REMAP"] = "0"
-    print(f"adj {timed(lambda: nat.los_adjoint_batched(plan, y, out, rowscale=cs[0])):.1f} us", flush=True)
+    aref = None
+    for pad in (False, True, False, True):
+        los_response.ADJ_PAD = pad
+        R._plan_np = los_response.box_plan(*R._coo, sp.shape, R.target.shape[0])
+        R._plan = None
+        plan = R._box_plan()
+        out.zero_()
+        nat.los_adjoint_batched(plan, y, out, rowscale=cs[0])
+        if aref is None:
+            aref = out.clone()
+        eq = bool(torch.equal(aref, out))
+        print(f"adj pad={int(pad)} {timed(lambda: nat.los_adjoint_batched(plan, y, out, rowscale=cs[0])):.1f} us "
+              f"(bitwise equal: {eq})", flush=True)
 
 
 if __name__ == "__main__":
