@@ -508,7 +508,7 @@ def cpu_baseline_config(args, lat0, n, gpu_iters, gpu_samples):
                        f"at this CPU rate")}
 
 
-def demo_step(ift, lh, pos, nsamp, comm):
+def demo_step(ift, lh, pos, nsamp, comm, R=None):
     """One step with SURVEY §8(d)'s demo controllers: sampling
     AbsDeltaEnergyController(0.05, iteration_limit=100), NewtonCG(
     AbsDeltaEnergyController(0.5, convergence_level=2, iteration_limit=15))."""
@@ -528,10 +528,59 @@ def demo_step(ift, lh, pos, nsamp, comm):
     one()
     barrier_sync(1)
     el = time.perf_counter() - t
+    cg_iters = int(ift.ConjugateGradient.iterations_total - it0)
+    newton = newton_roofline(ift, one, R)
     ift.random.pop_sseq()
     return {"samples_per_s": round(2 * nsamp / el, 4), "ms_per_step": round(el * 1e3, 1),
-            "cg_iters": int(ift.ConjugateGradient.iterations_total - it0), "warmup_steps": 1,
-            "controllers": "sampling AbsDelta(0.05, 100); NewtonCG(AbsDelta(0.5, convergence_level=2, 15))"}
+            "cg_iters": cg_iters, "warmup_steps": 1,
+            "controllers": "sampling AbsDelta(0.05, 100); NewtonCG(AbsDelta(0.5, convergence_level=2, 15))",
+            "newton_cg": newton}
+
+
+def newton_roofline(ift, one, R):
+    """The geoVI Newton-direction CG of the demo controllers on the roofline:
+    one more (untimed) demo step with every batched solve of the lowered
+    Newton metric timed (device synchronised around it), SURVEY §8(d) bytes
+    per right-hand-side iteration with the matvec term and the LOS pair
+    doubled (M = B^T B, B = 1 + J0^T L0^T L J: 4 transforms, 2 LOS pairs):
+    N [2 ((4d+3) s + 8) + 10 s] + 2 (2 s N + 16 nnz)."""
+    from nifty_amd.minimization import fused_cg
+    if not torch.cuda.is_available():
+        return None
+    rec = [0, 0, 0.0]
+    orig = fused_cg.FusedCGBatch.run_packed
+
+    def run_packed(self, X, Rr, Bv, starts):
+        if type(self.core).__name__ != "_MetricCore":
+            return orig(self, X, Rr, Bv, starts)
+        torch.cuda.synchronize()
+        it0 = ift.ConjugateGradient.iterations_total
+        t = time.perf_counter()
+        r = orig(self, X, Rr, Bv, starts)
+        torch.cuda.synchronize()
+        rec[0] += 1
+        rec[1] += ift.ConjugateGradient.iterations_total - it0
+        rec[2] += time.perf_counter() - t
+        return r
+    fused_cg.FusedCGBatch.run_packed = run_packed
+    try:
+        one()
+    finally:
+        fused_cg.FusedCGBatch.run_packed = orig
+    if rec[1] == 0:
+        return None
+    if R is None:
+        return None
+    shp = R.domain[0].shape
+    N, s, d = int(np.prod(shp)), 8, len(shp)
+    nnz = int(R._plan_np["box_ent"][-1])
+    per = N * (2 * ((4 * d + 3) * s + 8) + 10 * s) + 2 * (2 * s * N + 16 * nnz)
+    gbs = per * rec[1] / rec[2] / 1e9
+    return {"solves": rec[0], "rhs_iters": rec[1], "ms": round(rec[2] * 1e3, 1),
+            "us_per_rhs_iter": round(rec[2] * 1e6 / rec[1], 1), "bytes_per_rhs_iter": per,
+            "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s", "frac": round(gbs / 8000.0, 4),
+            "path": "per-iteration host read, separate direction / curvature d.q / update passes "
+                    "(value-driven AbsDelta controller)"}
 
 
 class _TimedComm:
@@ -638,7 +687,7 @@ def main():
     roof = roofline_of(kp, cgit, cf, R, args.config) if kp else None
     demo = None
     if not args.no_demo and torch.cuda.is_available() and args.config == "C3":
-        demo = demo_step(ift, lh, pos, nsamp, comm)
+        demo = demo_step(ift, lh, pos, nsamp, comm, R)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.config != "C3":
         lat0 = {k: pos[k].val.cpu().numpy() for k in cf.domain.keys()}

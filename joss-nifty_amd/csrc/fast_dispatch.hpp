@@ -65,6 +65,9 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
       if constexpr (persist_ok<N, NT, KIND>())
         (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if constexpr (KIND == K_UNPACK && !ROWS)
+        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
   }
@@ -119,6 +122,13 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     if (!launched && !a.f.pro) {
       const long long grid = std::min<long long>(ntiles, (long long)ncu * std::max(1, per_cu));
       hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, true>), dim3((unsigned)grid), dim3(NT), lds, s, b);
+      launched = true;
+    }
+  }
+  if constexpr (KIND == K_UNPACK && !ROWS) {
+    if (!launched && a.f.cg) {
+      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, true>), dim3((unsigned)ntiles), dim3(NT), lds, s,
+                         b);
       launched = true;
     }
   }

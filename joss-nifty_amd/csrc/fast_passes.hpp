@@ -247,7 +247,9 @@ constexpr size_t pass_lds_bytes() {
   return tw_lds_offset<T, N, NT, KIND, ROWS>() + (size_t)(N / 4) * sizeof(cplx_t<T>);
 }
 
-template <typename T, int N, int NT, int KIND, bool ROWS, bool PF>
+// CGE (unpack passes): the CG-carrying epilogue (a.f.cg) compiled alone; the
+// plain unpack instance carries none of its registers (occupancy)
+template <typename T, int N, int NT, int KIND, bool ROWS, bool PF, bool CGE = false>
 __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   // Persistent: workgroup b processes tiles b, b + G, b + 2G, ...  The input
   // of tile t + G is loaded into registers while tile t is transformed and
@@ -447,7 +449,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       __syncthreads();
       const T sg = (T)a.sigma, sc = a.scale;
       const int Nf = a.Nfull;
-      if (!a.f.cg) {
+      if constexpr (!CGE) {
 #pragma unroll
         for (int r = 0; r < VPT; ++r) {
           int l, x;
