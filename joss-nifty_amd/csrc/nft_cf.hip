@@ -368,14 +368,31 @@ __global__ __launch_bounds__(256) void bin_fold_half_sorted(const T* __restrict_
         const long long x = x0 + u * (long long)blockDim.x;
         if (x >= hl) break;
         const long long dpos = (cpos ? (long long)cpos[o * hl + x] : o * hl + x) * pre;
+        T accs[PRE];
 #pragma unroll
         for (int p = 0; p < PRE; ++p) {
-          if (p >= pre) break;
           T acc = (T)0;
 #pragma unroll
           for (int s = 0; s < (1 << (FOLD_MAXD - 1)); ++s)
             if (rok[s]) acc += v[u][p][s];
-          out[dpos + p] = acc;
+          accs[p] = acc;
+        }
+        if (PRE % 2 == 0 && pre == PRE) {
+          // the cell's items as 2-wide vector stores (8 PRE-byte aligned run)
+          typedef T V2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+          for (int p = 0; p < PRE; p += 2) {
+            V2 w;
+            w.x = accs[p];
+            w.y = accs[p + 1];
+            *(V2*)(out + dpos + p) = w;
+          }
+        } else {
+#pragma unroll
+          for (int p = 0; p < PRE; ++p) {
+            if (p >= pre) break;
+            out[dpos + p] = accs[p];
+          }
         }
       }
     }

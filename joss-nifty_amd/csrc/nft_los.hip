@@ -326,6 +326,27 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
         double acc[K];
 #pragma unroll
         for (int b = 0; b < K; ++b) acc[b] = 0.0;
+#if NFT_LOS_PAIR && NFT_LOS_UT == 0
+        // entries k and k + 4 of the lane read together (two LDS chains in
+        // flight), summed in the same order
+        for (int k = sa[r] + sub; k < sb[r]; k += 8) {
+          const bool h = k + 4 < sb[r];
+          const double w0 = (double)ew[k], w1 = h ? (double)ew[k + 4] : 0.0;
+          const int l0 = el[k], l1 = h ? el[k + 4] : 0;
+          double v0[K], v1[K];
+#pragma unroll
+          for (int b = 0; b < K; ++b) {
+            v0[b] = u[l0][b];
+            v1[b] = u[l1][b];
+          }
+#pragma unroll
+          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w0 * v0[b];
+          if (h) {
+#pragma unroll
+            for (int b = 0; b < K; ++b) acc[b] = acc[b] + w1 * v1[b];
+          }
+        }
+#else
         for (int k = sa[r] + sub; k < sb[r]; k += 4) {
           const double w = (double)ew[k];
           const int l = el[k];
@@ -340,6 +361,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
           for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
 #endif
         }
+#endif
 #pragma unroll
         for (int b = 0; b < K; ++b) {
           double v = acc[b];
