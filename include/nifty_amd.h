@@ -363,6 +363,11 @@ typedef struct nft_los_plan {
    * line table without waiting for box_lptr (one dependent load fewer). */
   int lpad;
   const int* box_lines_pad;
+  /* optional (NULL: box_ent): the start of every box's adjoint entries
+   * (ent_lidx / ent_wa) when each box's run is padded to a multiple of 16
+   * entries (8-bit line indices; padding never summed: the pixel runs end
+   * before it).  The batched adjoint then stages them with 16-byte loads. */
+  const int* box_ent_adj;
 } nft_los_plan;
 
 size_t nft_los_workspace(const nft_los_plan* plan);

@@ -109,7 +109,7 @@ class LosPlan(ctypes.Structure):
                [("lidx8", _i), ("ent_wa", _p), ("slot_seg", _p), ("box_item", _p),
                 ("tile_S", _i), ("ntile", _i64), ("tl_max", _i)] + \
                [(n, _p) for n in ("tile_iptr", "tile_items", "tile_lptr", "tl_slot", "seg_tl")] + \
-               [("lpad", _i), ("box_lines_pad", _p)]
+               [("lpad", _i), ("box_lines_pad", _p), ("box_ent_adj", _p)]
 
 
 class AmpConst(ctypes.Structure):

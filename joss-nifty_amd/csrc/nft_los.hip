@@ -594,7 +594,7 @@ __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const doub
 // fp32 weight) are staged in LDS once; every pixel thread sums its run for
 // all K vectors in registers from the per-vector line tables.  Per vector the
 // products and their order are those of K = 1 (bitwise).
-template <typename T, typename IDX, int K>
+template <typename T, typename IDX, int K, bool VEC = false>
 __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* __restrict__ lidx,
                                                      const T* __restrict__ yv, const T* __restrict__ cs,
                                                      const T* __restrict__ rs, T* __restrict__ out, double scale,
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   __shared__ double yl[YL];
   // K == 1 uses ew as a double product buffer (LOS_CH_A doubles)
   __shared__ __align__(16) float ew[K == 1 ? 2 * LOS_CH_A : LOS_CH_A];
-  __shared__ IDX el[K == 1 ? 1 : LOS_CH_A];
+  __shared__ __align__(16) IDX el[K == 1 ? 1 : LOS_CH_A];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int box = remap ? xcd_unit(blockIdx.x, p.nbox) : (int)blockIdx.x, t = threadIdx.x;
   if (box >= p.nbox) return;
@@ -628,7 +628,10 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
     }
   }
   const int l0 = p.box_lptr[box], nl = p.box_lptr[box + 1] - l0;
-  const int e0 = p.box_ent[box], n = p.box_ent[box + 1] - e0;
+  // 16-entry chunks with 16-byte loads (box runs padded, box_ent_adj)
+  constexpr bool vec = VEC && sizeof(IDX) == 1 && K > 1;
+  const int* __restrict__ bent = p.box_ent_adj ? p.box_ent_adj : p.box_ent;
+  const int e0 = bent[box], n = bent[box + 1] - e0;
   const unsigned short* off = p.pix_off + (size_t)box * 257;
   const int a = off[t], b = off[t + 1];
   // the pixel's row scales are loaded up front (off the tail of the block)
@@ -642,11 +645,28 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   // two dependent load chains overlap
   int lv[PER];
   float wv[PER];
+  uint4 vl = make_uint4(0, 0, 0, 0);
+  float4 vw[4];
+  auto vload = [&](int c0, int cn) {
+    const int k = 16 * t;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int k = t + i * 256;
-    lv[i] = k < n ? (int)lidx[e0 + k] : 0;
-    wv[i] = k < n ? p.ent_wa[e0 + k] : 0.f;
+    for (int j = 0; j < 4; ++j) vw[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    vl = make_uint4(0, 0, 0, 0);
+    if (k < cn && k < LOS_CH_A) {
+      vl = *(const uint4*)((const unsigned char*)lidx + e0 + c0 + k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vw[j] = *(const float4*)(p.ent_wa + e0 + c0 + k + 4 * j);
+    }
+  };
+  if constexpr (vec) {
+    vload(0, min(LOS_CH_A, n));
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = t + i * 256;
+      lv[i] = k < n ? (int)lidx[e0 + k] : 0;
+      wv[i] = k < n ? p.ent_wa[e0 + k] : 0.f;
+    }
   }
   const bool tab = lp || nl * K <= YL;  // line values of this box (all vectors) cached in LDS
   if (tab && !lp) {
@@ -666,7 +686,9 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   for (int v = 0; v < K; ++v) acc[v] = 0.0;
   for (int c0 = 0; c0 < n; c0 += LOS_CH_A) {  // uniform over the block
     const int cn = min(LOS_CH_A, n - c0);
-    if (c0 > 0) {
+    if (c0 > 0 && vec) {
+      if constexpr (vec) vload(c0, cn);
+    } else if (c0 > 0) {
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int k = t + i * 256;
@@ -699,12 +721,21 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
       for (int k = lo; k < hi; ++k) acc[0] += prod[k - c0];
       continue;
     }
+    if constexpr (vec) {
+      const int k = 16 * t;
+      if (k < cn && k < LOS_CH_A) {
+        *(uint4*)((unsigned char*)el + k) = vl;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int k = t + i * 256;
-      if (k < cn) {
-        ew[k] = wv[i];
-        el[k] = (IDX)lv[i];
+        for (int j = 0; j < 4; ++j) *(float4*)(ew + k + 4 * j) = vw[j];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int k = t + i * 256;
+        if (k < cn) {
+          ew[k] = wv[i];
+          el[k] = (IDX)lv[i];
+        }
       }
     }
     __syncthreads();
@@ -900,6 +931,13 @@ static void adj_boxes_k(const nft_los_plan* p, const IDX* li, const T* y, const 
   const char* ab = getenv("NFT_LOS_ADJ_XCD");   // tuning probe (read per launch)
   const int remap = ab ? atoi(ab) : 0;
   const unsigned grid = remap ? (unsigned)(8 * ((p->nbox + 7) / 8)) : (unsigned)p->nbox;
+  if constexpr (K > 1 && sizeof(IDX) == 1) {
+    if (p->box_ent_adj) {
+      hipLaunchKernelGGL((los_adj_boxes<T, IDX, K, true>), dim3(grid), dim3(256), 0, s, *p, li, y, cs, rs, out, scale,
+                         ys, os, rss, remap);
+      return;
+    }
+  }
   hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), dim3(grid), dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys,
                      os, rss, remap);
 }

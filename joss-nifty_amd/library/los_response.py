@@ -159,6 +159,9 @@ TILE_LINES_MAX = 1024   # lines crossing one tile (LDS accumulators: lines x vec
 # waiting for the box bounds (bitwise).  Measured at 4 x 2048^2: 98 -> 103 us
 # (a whole 1 KB row per box read): off
 ADJ_PAD = os.environ.get("NFT_LOS_ADJ_PAD", "0") == "1"
+# the adjoint's entries padded per box to 16-entry chunks (box_ent_adj) and
+# staged with 16-byte loads (NFT_LOS_ADJ_VEC=1; bitwise the per-entry loads)
+ADJ_VEC = os.environ.get("NFT_LOS_ADJ_VEC", "0") == "1"
 # forward segments of a work item longest first (_longest_first,
 # NFT_LOS_SORT_SEG=1; bitwise).  Measured at 4 x 2048^2 / 16384 lines: one
 # workgroup per box 116 us either way (items 130 -> 128 us): off
@@ -272,7 +275,28 @@ def box_plan(rows, cols, w, shape, nlos):
                 item_ent=seg_ent[item_seg].astype(np.int32), **fwd,
                 box_item=box_item, los_ptr=los_ptr, box_ent=np.r_[0, np.cumsum(entcnt)].astype(np.int32), pix_off=pix_off,
                 box_lptr=box_lptr, box_lines=seg_los.astype(np.int32),
-                ent_lidx=lidx.astype(np.uint8 if lidx8 else np.uint16), lidx8=int(lidx8), ent_wa=wf[oa])
+                **_adj_entries(lidx.astype(np.uint8 if lidx8 else np.uint16), wf[oa], entcnt, lidx8))
+
+
+def _adj_entries(lidx, wa, entcnt, lidx8):
+    """The adjoint's entry arrays; with ADJ_VEC and 8-bit line indices every
+    box's run padded to a multiple of 16 entries (index 0, weight 0: never
+    summed, the pixel runs end before them) and its start in box_ent_adj, so
+    the adjoint stages them with 16-byte loads."""
+    out = dict(ent_lidx=lidx, lidx8=int(lidx8), ent_wa=wa)
+    if not (ADJ_VEC and lidx8) or len(entcnt) == 0:
+        return out
+    padded = -(-entcnt // 16) * 16
+    start = np.r_[0, np.cumsum(padded)]
+    n = int(start[-1])
+    src0 = np.r_[0, np.cumsum(entcnt)][:-1]
+    pos = np.repeat(start[:-1] - src0, entcnt) + np.arange(int(entcnt.sum()))
+    li = np.zeros(n, dtype=lidx.dtype)
+    w = np.zeros(n, dtype=np.float32)
+    li[pos] = lidx
+    w[pos] = wa
+    out.update(ent_lidx=li, ent_wa=w, box_ent_adj=start.astype(np.int32))
+    return out
 
 
 def _longest_first(fwd, item_seg):
@@ -374,7 +398,7 @@ def box_plan_apply(P, x, mode):
     out = np.zeros(P["L"] * H * W)
     for b in range(P["nbox"]):
         p, ok = pix(b)
-        e0 = P["box_ent"][b]
+        e0 = P["box_ent_adj"][b] if "box_ent_adj" in P else P["box_ent"][b]
         for tt in range(BOX):
             if not ok[tt]:
                 continue

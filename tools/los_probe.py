@@ -64,7 +64,8 @@ def main():
         print("   " + ", ".join(f"{k} {sum(v) / len(v):.1f} us" for k, v in acc.items()), flush=True)
     aref = None
     for pad in (False, True, False, True):
-        los_response.ADJ_PAD = pad
+        los_response.ADJ_VEC = pad
+        los_response.ADJ_PAD = False
         R._plan_np = los_response.box_plan(*R._coo, sp.shape, R.target.shape[0])
         R._plan = None
         plan = R._box_plan()
@@ -73,7 +74,7 @@ def main():
         if aref is None:
             aref = out.clone()
         eq = bool(torch.equal(aref, out))
-        print(f"adj pad={int(pad)} {timed(lambda: nat.los_adjoint_batched(plan, y, out, rowscale=cs[0])):.1f} us "
+        print(f"adj vec={int(pad)} {timed(lambda: nat.los_adjoint_batched(plan, y, out, rowscale=cs[0])):.1f} us "
               f"(bitwise equal: {eq})", flush=True)
 
 
