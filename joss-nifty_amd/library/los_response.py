@@ -160,8 +160,9 @@ TILE_LINES_MAX = 1024   # lines crossing one tile (LDS accumulators: lines x vec
 # (a whole 1 KB row per box read): off
 ADJ_PAD = os.environ.get("NFT_LOS_ADJ_PAD", "0") == "1"
 # the adjoint's entries padded per box to 16-entry chunks (box_ent_adj) and
-# staged with 16-byte loads (NFT_LOS_ADJ_VEC=1; bitwise the per-entry loads)
-ADJ_VEC = os.environ.get("NFT_LOS_ADJ_VEC", "0") == "1"
+# staged with 16-byte loads (bitwise the per-entry loads; 4 x 2048^2: 96.4 ->
+# 92.9 us, iteration -7 us; NFT_LOS_ADJ_VEC=0: per-entry loads)
+ADJ_VEC = os.environ.get("NFT_LOS_ADJ_VEC", "1") != "0"
 # forward segments of a work item longest first (_longest_first,
 # NFT_LOS_SORT_SEG=1; bitwise).  Measured at 4 x 2048^2 / 16384 lines: one
 # workgroup per box 116 us either way (items 130 -> 128 us): off

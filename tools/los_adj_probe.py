@@ -1,6 +1,9 @@
 """LOS adjoint ablations on the bench's plan (2048^2, 16384 lines, K = 4,
 pixel-side row scale shared): NFT_LOS_ADJ_DBG bits 1 no output stores, 2 no
-entry sums, 4 no line values, 8 no entry loads (tuning probe only)."""
+entry sums, 4 no line values, 8 no entry loads (tuning probe only).  The
+ablation bits live in a probe build of los_adj_boxes (remap bits 4..7, read
+from NFT_LOS_ADJ_DBG by adj_boxes_k; not in the product kernel, whose
+registers they would cost): run with NFT_LIB pointing at that build."""
 import os
 import sys
 
