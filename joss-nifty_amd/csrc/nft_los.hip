@@ -39,10 +39,13 @@ constexpr int LOS_SEG_ROUNDS = 4;
 #define NFT_LOS_UT 0
 #endif
 #ifndef NFT_LOS_VLOAD
-#define NFT_LOS_VLOAD 0  // entries staged from aligned 8-entry chunks (uint2 + 2 float4 per thread)
+#define NFT_LOS_VLOAD 0  // per-box forward: entries staged from aligned 16-entry chunks (uint4 + 4 float4 per thread)
 #endif
 #ifndef NFT_LOS_PAIR
 #define NFT_LOS_PAIR 0  // segment loop: entries k and k + 4 of a lane read together
+#endif
+#if NFT_LOS_PAIR && NFT_LOS_VLOAD
+#error "NFT_LOS_PAIR and NFT_LOS_VLOAD are exclusive"
 #endif  // forward: <= 256 segments per item = 4 rounds of 64 quads (host-guaranteed)
 
 struct BoxGeom {
@@ -248,8 +251,16 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
 #else
   __shared__ __align__(16) double u[256][K];
 #endif
+#if NFT_LOS_VLOAD
+  // entries staged from the aligned 16-entry chunks covering the item (one
+  // uint4 of pixel indices and four float4 of weights per thread); entry k
+  // of the item at LDS slot (e0 & 15) + k
+  __shared__ __align__(16) float ew[LOS_CAP_F + 16];
+  __shared__ __align__(16) unsigned char el[LOS_CAP_F + 16];
+#else
   __shared__ float ew[LOS_CAP_F];
   __shared__ unsigned char el[LOS_CAP_F];
+#endif
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int box = remap ? xcd_unit(blockIdx.x, (int)p.nbox) : (int)blockIdx.x;
   if (box >= p.nbox) return;
@@ -280,6 +291,20 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
   const int sub = t & 3;
   for (bool first = true;; first = false) {
     const int n = e1 - e0;
+#if NFT_LOS_VLOAD
+    const int eo = e0 & 15;
+    uint4 vl = make_uint4(0, 0, 0, 0);
+    float4 vw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vw[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (16 * t < eo + n) {
+      const long long c = (long long)(e0 - eo) + 16 * t;
+      vl = *(const uint4*)(p.ent_loc + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vw[j] = *(const float4*)(p.ent_wf + c + 4 * j);
+    }
+#else
+    constexpr int eo = 0;
     float wv[PER];
     unsigned char lv[PER];
 #pragma unroll
@@ -288,6 +313,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
       wv[i] = k < n ? p.ent_wf[e0 + k] : 0.f;
       lv[i] = k < n ? p.ent_loc[e0 + k] : 0;
     }
+#endif
     const int sq = s0 + (t >> 2);
     int sa[RND], sb[RND], so[RND];
 #pragma unroll
@@ -311,6 +337,13 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
     } else {
       __syncthreads();  // the previous item's entries are read
     }
+#if NFT_LOS_VLOAD
+    if (16 * t < eo + n) {
+      *(uint4*)(el + 16 * t) = vl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *(float4*)(ew + 16 * t + 4 * j) = vw[j];
+    }
+#else
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int k = t + i * 256;
@@ -319,6 +352,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
         el[k] = lv[i];
       }
     }
+#endif
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RND; ++r) {
@@ -347,7 +381,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
           }
         }
 #else
-        for (int k = sa[r] + sub; k < sb[r]; k += 4) {
+        for (int k = sa[r] + eo + sub; k < sb[r] + eo; k += 4) {
           const double w = (double)ew[k];
           const int l = el[k];
 #if NFT_LOS_UT == 1

@@ -270,6 +270,10 @@ def box_plan(rows, cols, w, shape, nlos):
         fwd["seg_tl"] = tiles.pop("seg_tl")
     if SORT_SEGMENTS and nseg:
         fwd = _longest_first(fwd, item_seg)
+    # 16 entries of padding: the per-box forward stages aligned 16-entry
+    # chunks, the last one may reach past an item's (and the array's) end
+    fwd["ent_loc"] = np.r_[fwd["ent_loc"], np.zeros(16, np.uint8)]
+    fwd["ent_wf"] = np.r_[fwd["ent_wf"], np.zeros(16, np.float32)]
     return dict(tiles, **pad, H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
                 nitems=len(item_box), nseg=nseg, L=L,
                 item_box=np.asarray(item_box, dtype=np.int32), item_seg=item_seg.astype(np.int32),
