@@ -730,6 +730,9 @@ int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t
   return NFT_OK;
 }
 
+#ifndef NFT_SIL_CH
+#define NFT_SIL_CH 2048  // build knob: bin-sorted positions x items per nft_bin_scatter_il workgroup
+#endif
 int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void* out, int64_t pre, int64_t npix,
                        int64_t nbins, int dtype, hipStream_t stream) {
   if (!(pre == 2 || pre == 4 || pre == 8) || npix < 0 || nbins < 0 || !perm || !offsets) {
@@ -744,7 +747,7 @@ int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void
   prof_mark(stream, "bin_scatter");
 #define NFT_SIL(TT, PP)                                                                                       \
   {                                                                                                           \
-    constexpr int CH = 2048 / PP;                                                                             \
+    constexpr int CH = NFT_SIL_CH / PP;                                                                       \
     const int nch = (int)((npix + CH - 1) / CH);                                                              \
     const unsigned nb = (unsigned)(((nch + NXCD - 1) / NXCD) * NXCD);                                         \
     hipLaunchKernelGGL((bin_scatter_il<TT, PP, CH>), dim3(nb), dim3(256), 0, stream, (const TT*)in, perm, offsets, \
