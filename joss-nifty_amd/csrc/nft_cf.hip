@@ -747,7 +747,7 @@ int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void
   prof_mark(stream, "bin_scatter");
 #define NFT_SIL(TT, PP)                                                                                       \
   {                                                                                                           \
-    constexpr int CH = NFT_SIL_CH / PP;                                                                       \
+    constexpr int CH = NFT_SIL_CH / PP >= 256 ? NFT_SIL_CH / PP : 256;                                       \
     const int nch = (int)((npix + CH - 1) / CH);                                                              \
     const unsigned nb = (unsigned)(((nch + NXCD - 1) / NXCD) * NXCD);                                         \
     hipLaunchKernelGGL((bin_scatter_il<TT, PP, CH>), dim3(nb), dim3(256), 0, stream, (const TT*)in, perm, offsets, \
