@@ -232,27 +232,20 @@ def cg_iteration(lib, core, W, shift, bufs, k):
 
 def cg_iteration_wall(lib, core, W, shift, bufs, k, reps=20):
     """Wall time of one batched CG iteration exactly as the timed loop runs it:
-    FusedCGBatch's iteration body (the two-stream split iteration where it
-    applies, fused_cg._SplitIteration) captured in a HIP graph and replayed
-    `reps` times between two events.  The CG scalars are restored at the start
-    of every replay (one 128-byte copy inside the graph), so every replay does
-    the full update."""
+    FusedCGBatch's iteration body captured in a HIP graph and replayed
+    `reps` times between two events.  Every replay continues the CG from the
+    previous one (the probe's scalars never freeze a right-hand side:
+    CG_AUTO is 0 and the metric is positive definite), so every replay does
+    the full update; the scalars are restored once afterwards."""
     from nifty_amd import _native
     from nifty_amd.minimization import fused_cg
     X, R, D, Q, SC, ws = bufs
     n = X.shape[1]
-    nq = fused_cg._quad_blocks(core, W, X.dtype)
-    split = None
-    if nq and fused_cg._SPLIT and hasattr(core, "mv_amp_jvp"):
-        split = fused_cg._SplitIteration(lib, core, W, n, k, nq, shift, False)
     SC0 = SC.clone()
 
     def body():
-        SC.copy_(SC0)
-        if split is not None:
-            split(X, R, D, Q, None, SC)
-        else:
-            cg_iteration(lib, core, W, shift, bufs, k)
+        cg_iteration(lib, core, W, shift, bufs, k)
+    assert float(SC[:, _native.CG_AUTO].abs().sum()) == 0.0
     for _ in range(2):
         body()
     torch.cuda.synchronize()
@@ -265,14 +258,18 @@ def cg_iteration_wall(lib, core, W, shift, bufs, k, reps=20):
         g.replay()
     t1.record()
     torch.cuda.synchronize()
+    if float(SC[:, _native.CG_DONE].abs().sum()) != 0.0:
+        raise RuntimeError("cg_iteration_wall: a right-hand side froze during the replays")
     SC.copy_(SC0)
-    return t0.elapsed_time(t1) * 1e3 / reps, split is not None
+    return t0.elapsed_time(t1) * 1e3 / reps
 
 
-def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False):
-    """Algorithmic bytes per launch (fp64, every operand array counted once per
+def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False, s=8):
+    """Algorithmic bytes per launch (every operand array counted once per
     launch; arrays shared by the k right-hand sides -- amplitude, xi0, pindex,
-    the LOS matrix and its scales -- once).  DESIGN.md §3."""
+    the LOS matrix and its scales -- once).  s: bytes per value of the CG
+    vectors and grid operands (8 fp64; 4 for C5's fp32 storage -- complex
+    values 2s, indices 4 bytes, LOS weights 4 bytes either way).  DESIGN.md §3."""
     shape = cf.target.shape
     N = int(np.prod(shape))
     Hh = N // shape[-1] * (shape[-1] // 2 + 1)
@@ -290,45 +287,45 @@ def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False):
     Nf = fold["nf"] if fold else N
     return {
         # prologue A*x + xi0*dA[pindex]: x (k), A, xi0, pindex, dA (k); half spectrum out (k)
-        "fft_r2c+pro": 8 * k * N + 8 * N + 8 * N + 4 * N + 8 * k * B + 16 * k * Hh,
+        "fft_r2c+pro": s * k * N + s * N + s * N + 4 * N + s * k * B + 2 * s * k * Hh,
         # batched prologue as its own pass: x (k), A, xi0, pindex, dA (k) -> u (k)
-        "pro_batch": 8 * k * N + 8 * N + 8 * N + 4 * N + 8 * k * B + 8 * k * N,
+        "pro_batch": s * k * N + s * N + s * N + 4 * N + s * k * B + s * k * N,
         # folded: the cell's bin (N_f), dA gathered per mirror class; no pindex
-        "pro_fold": 8 * k * N + 8 * N + 8 * N + 4 * Nf + 8 * k * B + 8 * k * N,
+        "pro_fold": s * k * N + s * N + s * N + 4 * Nf + s * k * B + s * k * N,
         # ... carrying the grid segment's CG direction: d, r in, d out (k)
-        "pro_fold+dir": 24 * k * N + 8 * N + 8 * N + 4 * Nf + 8 * k * B + 8 * k * N,
-        "fft_r2c": 8 * k * N + 16 * k * Hh,
-        "fft_c2c": 2 * 16 * k * Hh,
-        "fft_unpack": 16 * k * Hh + 8 * k * N,
+        "pro_fold+dir": 3 * s * k * N + s * N + s * N + 4 * Nf + s * k * B + s * k * N,
+        "fft_r2c": s * k * N + 2 * s * k * Hh,
+        "fft_c2c": 2 * 2 * s * k * Hh,
+        "fft_unpack": 2 * s * k * Hh + s * k * N,
         # epilogue: out = A*v (k), out2 = xi0*v (k), reads A, xi0
-        "fft_unpack+epi": 16 * k * Hh + 16 * N + 8 * k * N + 8 * k * (Hh if pairs else N),
+        "fft_unpack+epi": 2 * s * k * Hh + 2 * s * N + s * k * N + s * k * (Hh if pairs else N),
         # 5 B per nonzero, 12 B segment descriptors, x (k) and the column scale, partials (k)
-        "los_fwd_items": 5 * nnz + 12 * nseg + 8 * (k + 1) * N + 8 * k * nseg,
-        "los_fwd_reduce": 8 * k * nseg + 8 * k * nlos,
-        "los_adj_boxes": 5 * nnz + 4 * nseg + 2 * 257 * nbox + 8 * (k + 1) * N,
+        "los_fwd_items": 5 * nnz + 12 * nseg + s * (k + 1) * N + 8 * k * nseg,   # fp64 partials
+        "los_fwd_reduce": 8 * k * nseg + s * k * nlos,
+        "los_adj_boxes": 5 * nnz + 4 * nseg + 2 * 257 * nbox + s * (k + 1) * N,
         # mirror fold: w (k) in -- the half grid of point-mirror pair sums
         # with epi_out2_pairs -- folded cell (k) out
-        "bin_fold": 8 * k * (Hh if pairs else N) + 8 * k * Nf,
+        "bin_fold": s * k * (Hh if pairs else N) + s * k * Nf,
         # perm over the cell, cell values (k), bin offsets, sums (k)
-        "bin_scatter": 4 * Nf + 8 * k * Nf + 4 * B + 8 * k * B,
-        "cg_dir_kernel": 3 * 8 * k * n_lat,
+        "bin_scatter": 4 * Nf + s * k * Nf + 4 * B + s * k * B,
+        "cg_dir_kernel": 3 * s * k * n_lat,
         # whole vector, or (direction carried by the prologue) two launches
         # over the keys before / after the grid segment, half their bytes each
-        "cg_dir_dd": 3 * 8 * k * (n_lat if not dir_carried else (n_lat - N) // 2),
-        "curv_partial": 2 * 8 * k * n_lat,
+        "cg_dir_dd": 3 * s * k * (n_lat if not dir_carried else (n_lat - N) // 2),
+        "curv_partial": 2 * s * k * n_lat,
         # x, r, d, q in; x, r out (b is not streamed: the probe passes none,
         # and the sampling CG's value-blind controllers skip it too)
-        "cg_update_kernel": 6 * 8 * k * n_lat,
+        "cg_update_kernel": 6 * s * k * n_lat,
         # the amplitude keys' update (the grid segment's rides in the
         # epilogue): two launches, the keys before and after the grid
         # segment; per launch the model carries half of their bytes
-        "cg_update_seg": 3 * 8 * k * (n_lat - N),
+        "cg_update_seg": 3 * s * k * (n_lat - N),
         # both amplitude segments in one launch (nft_cg_*2_batched)
-        "cg_update_seg2": 6 * 8 * k * (n_lat - N),
-        "cg_dir_dd2": 3 * 8 * k * (n_lat - N),
+        "cg_update_seg2": 6 * s * k * (n_lat - N),
+        "cg_dir_dd2": 3 * s * k * (n_lat - N),
         # unpack + the grid segment's CG update: half spectrum (k), A, xi0;
         # x, r, d in (k), x, r and w = xi0*v out (k) -- q is not stored
-        "fft_unpack+cg": 16 * k * Hh + 16 * N + 40 * k * N + 8 * k * (Hh if pairs else N),
+        "fft_unpack+cg": 2 * s * k * Hh + 2 * s * N + 5 * s * k * N + s * k * (Hh if pairs else N),
     }
 
 
@@ -370,7 +367,8 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
     from nifty_amd.minimization import fused_cg
     dcar = bool(fused_cg._CARRY and fused_cg._CARRY_DIR and getattr(core, "dir_blocks", lambda k: 0)(k) > 0
                 and _CARRY_CACHE)
-    model = byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(getattr(core, "_pairs", lambda k: 0)(k)))
+    model = byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(getattr(core, "_pairs", lambda k: 0)(k)),
+                       s=X.element_size())
     out = {}
     tot_us, tot_b = 0.0, 0
     for lab, (cnt, tot) in acc.items():
@@ -380,9 +378,8 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
                     "gbs": round(by / (avg * 1e-6) / 1e9, 1) if by else None}
         tot_us += tot * 1e3 / reps
         tot_b += (by or 0) * (cnt // reps)
-    wall_us, two = cg_iteration_wall(lib, core, W, shift, bufs, k)
-    it = {"rhs": k, "us_per_iteration": round(wall_us, 1), "timing": "HIP graph replay of the iteration body"
-          + (" (two streams: amplitude chains beside the grid segment)" if two else ""),
+    wall_us = cg_iteration_wall(lib, core, W, shift, bufs, k)
+    it = {"rhs": k, "us_per_iteration": round(wall_us, 1), "timing": "HIP graph replay of the iteration body",
           "us_sum_of_launches": round(tot_us, 1), "algorithmic_bytes": tot_b,
           "gbs": round(tot_b / (wall_us * 1e-6) / 1e9, 1),
           "frac": round(tot_b / (wall_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -500,8 +497,9 @@ def cpu_baseline_config(args, lat0, n, gpu_iters, gpu_samples):
     cgps = iters / el
     value = gpu_samples / (gpu_iters / cgps)
     return {"value": round(value, 6), "unit": "samples/s", "cores": ncores, "kind": "port",
-            "cg_iter_per_s": round(cgps, 4),
-            "sample": (f"oracle geoVI draw (oracle/geovi.py: numpy, scipy.fft workers={ncores}) of 1 mirrored "
+            "cg_iter_per_s": round(cgps, 4), "projected": True,
+            "sample": (f"PROJECTION, not a timed draw: oracle geoVI draw (oracle/geovi.py: numpy, scipy.fft "
+                       f"workers={ncores}) of 1 mirrored "
                        f"pair on the same {'x'.join(map(str, shape))} problem, bounded to {args.cpu_lin_iters} "
                        f"linear-CG iteration(s) and no Newton step: {iters} CG iterations in {el:.1f} s (setup "
                        f"included); value = the GPU run's {gpu_iters} CG iterations for {gpu_samples} samples "

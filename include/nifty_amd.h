@@ -165,11 +165,7 @@ int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const in
                       hipStream_t stream);
 /* The half-grid fold of nft_bin_fold_half written in bin-sorted order, the
  * pre items of a cell adjacent: out[cpos[cell] * pre + p], cpos the inverse
- * of the folded bin index's stable bin -> cell permutation (1 <= pre <= 8).
- * nft_bin_sum_sorted: out[p * nbins + b] = sum over i in [offsets[b],
- * offsets[b+1]) of in[i * pre + p], ascending i -- together bitwise the
- * fold + nft_bin_scatter over the folded cell (PowerDistributor adjoint,
- * src/operators/distributors.py:92-105, on the mirror-folded cell). */
+ * of the folded bin index's stable bin -> cell permutation (1 <= pre <= 8). */
 int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t pre, int ndim,
                              const int64_t* shape, int dtype, hipStream_t stream);
 /* cpos = NULL in nft_bin_fold_half_sorted: the fold in cell order with the
@@ -178,8 +174,6 @@ int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t
  * cell for all items -- bitwise nft_bin_fold_half + nft_bin_scatter. */
 int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void* out, int64_t pre, int64_t npix,
                        int64_t nbins, int dtype, hipStream_t stream);
-int nft_bin_sum_sorted(const void* in, const int* offsets, void* out, int64_t pre, int64_t nbins, int dtype,
-                       hipStream_t stream);
 int nft_bin_fold(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
                  hipStream_t stream);
 
@@ -333,36 +327,13 @@ typedef struct nft_los_plan {
   const void* ent_lidx;
   int lidx8;
   const float* ent_wa;
-  /* optional (NULL: partials in line-major slots, seg_slot): the segment of
-   * every line-major slot.  Then the forward stores segment s's partial at
-   * index s (one contiguous run per work item) and the line reduce gathers
-   * its slots through slot_seg -- the same values summed in the same order
-   * (bitwise the line-major layout). */
-  const int* slot_seg;
   /* optional (NULL: one workgroup per work item): the work items of every
    * box, items box_item[b] .. box_item[b+1] - 1 (nbox + 1 entries).  Then the
    * batched forward runs one workgroup per box, the pixel tile staged once
-   * for all of the box's items (same products and order: bitwise). */
+   * for all of the box's items (same products and order: bitwise).  The
+   * per-box forward stages aligned 16-entry chunks of ent_loc / ent_wf: both
+   * arrays must hold 16 entries of padding past the last item. */
   const int* box_item;
-  /* optional (ntile = 0: partials per (line, box) segment): tiles of
-   * tile_S x tile_S boxes.  The forward then runs one workgroup per tile:
-   * tile_items[tile_iptr[T] .. tile_iptr[T+1]) are its work items in
-   * processing order (boxes in raster order), tile_lptr the CSR of the lines
-   * crossing it (at most tl_max per tile), seg_tl[s] segment s's index into
-   * its tile's line list; each line's segment sums are accumulated in LDS in
-   * that order and stored once per (line, tile) at tl_slot[tile_lptr[T] + j]
-   * (line-major slots; los_ptr then points at their line CSR). */
-  int tile_S;
-  int64_t ntile;
-  int tl_max;
-  const int *tile_iptr, *tile_items, *tile_lptr, *tl_slot;
-  const uint16_t* seg_tl;
-  /* optional (lpad = 0: none): the lines crossing every box at a fixed
-   * stride, box_lines_pad[b * lpad + i] = box_lines[box_lptr[b] + i], -1
-   * past the box's count (lpad <= 256).  The batched adjoint then stages its
-   * line table without waiting for box_lptr (one dependent load fewer). */
-  int lpad;
-  const int* box_lines_pad;
   /* optional (NULL: box_ent): the start of every box's adjoint entries
    * (ent_lidx / ent_wa) when each box's run is padded to a multiple of 16
    * entries (8-bit line indices; padding never summed: the pixel runs end
@@ -469,6 +440,10 @@ int nft_cg_finalize_batched(const double* part, int nbtot, int nrhs, double* sc,
 typedef struct nft_amp_const {
   const double *c0, *sf, *p0, *p1, *p2, *lv;
   const double *vslope, *sc, *Qf, *Qa, *mspec, *An;
+  /* tables of the two-phase kernels (nft_amp2_prepare; NULL until prepared):
+   * constant tile-local scans, constant tile sums and global sums of this
+   * linearisation point, nft_amp2_tab_len(B) doubles */
+  const double* tab;
   double fl, S, ls_f, sig_s, zm, ls_o, total_volume;
   int64_t B;
   int has_flex, has_asp, has_zm;
@@ -507,9 +482,15 @@ int nft_amp_vjp_batched(const nft_amp_const* c, const nft_amp_const* item_consts
                         int64_t g_stride, hipStream_t stream);
 
 /* Two-phase amplitude JVP / VJP (csrc/nft_amp2.hip: two launches each; the
- * first forms tile-local scans and per-tile sums, the second combines them
- * over the tiles in a fixed order); the batched forms above take this path
- * when it applies.  Key arrays are indexed fl, sl, flex, asp, zm, spec (NULL:
+ * first forms per-tile dot products of the tangent / cotangent with constant
+ * vectors, the second the tile carries in a fixed order, the tile-local scans
+ * and the outputs); the batched forms above take this path when it applies.
+ * The constant sets must carry their tables (nft_amp_const.tab), made once
+ * per linearisation point by nft_amp2_prepare: for the host set *c
+ * (item_consts NULL, tables into tab) or for nrow DEVICE sets item_consts[r]
+ * (tables into tab + r * tab_stride, item_consts[r].tab set on the device).
+ * These kernels keep device-global arrival counters: do not run them on two
+ * streams at once.  Key arrays are indexed fl, sl, flex, asp, zm, spec (NULL:
  * absent key), pointing at right-hand side 0, rows lat_stride elements apart.
  * item_mode: 0 = every RHS uses *c; 1 = item_consts is a DEVICE array of nrhs
  * constant sets (one per RHS); 2 = item_consts is ONE device constant set
@@ -541,6 +522,9 @@ int nft_amp2_enabled(void);
  * tests); on < 0: back to the environment (NFT_AMP2) */
 void nft_amp2_set_enabled(int on);
 int nft_amp2_tiles(int64_t B, int nrhs, int item_mode);
+int64_t nft_amp2_tab_len(int64_t B);
+int nft_amp2_prepare(const nft_amp_const* c, nft_amp_const* item_consts, int nrow, double* tab, int64_t tab_stride,
+                     hipStream_t stream);
 int nft_amp2_jvp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, double* const* t,
                  const double* const* r, int64_t lat_stride, double* da, int64_t da_stride, int64_t da_elem_stride,
                  double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift,

@@ -42,7 +42,6 @@ SIGNATURES = {
     "nft_bin_fold": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_fold_half": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_fold_half_sorted": (_i, [_p, _p, _p, _i64, _i, _p, _i, _p]),
-    "nft_bin_sum_sorted": (_i, [_p, _p, _p, _i64, _i64, _i, _p]),
     "nft_bin_scatter_il": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "nft_bin_scatter_ordered": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
@@ -79,6 +78,8 @@ SIGNATURES = {
     "nft_amp2_enabled": (_i, []),
     "nft_amp2_set_enabled": (None, [_i]),
     "nft_amp2_tiles": (_i, [_i64, _i, _i]),
+    "nft_amp2_tab_len": (_i64, [_i64]),
+    "nft_amp2_prepare": (_i, [_p, _p, _i, _p, _i64, _p]),
     "nft_amp2_jvp": (_i, [_p, _p, _i, _p, _p, _i64, _p, _i64, _i64, _p, _i, _p, _p, _i64, _d, _p]),
     "nft_amp2_vjp": (_i, [_p, _p, _i, _p, _i64, _p, _p, _p, _i64, _d, _p, _i, _p, _p, _i64, _p, _i64, _i64, _i, _p]),
     "nft_amp_forward_buf": (_i64, [_i64]),
@@ -106,16 +107,13 @@ class LosPlan(ctypes.Structure):
                 ("nbox", _i64), ("nlos", _i64), ("nitems", _i64), ("nseg", _i64)] + \
                [(n, _p) for n in ("item_box", "item_seg", "item_ent", "seg_ent", "seg_slot", "ent_loc", "ent_wf",
                                   "los_ptr", "box_ent", "pix_off", "box_lptr", "box_lines", "ent_lidx")] + \
-               [("lidx8", _i), ("ent_wa", _p), ("slot_seg", _p), ("box_item", _p),
-                ("tile_S", _i), ("ntile", _i64), ("tl_max", _i)] + \
-               [(n, _p) for n in ("tile_iptr", "tile_items", "tile_lptr", "tl_slot", "seg_tl")] + \
-               [("lpad", _i), ("box_lines_pad", _p), ("box_ent_adj", _p)]
+               [("lidx8", _i), ("ent_wa", _p), ("box_item", _p), ("box_ent_adj", _p)]
 
 
 class AmpConst(ctypes.Structure):
     """nft_amp_const (include/nifty_amd.h)."""
     _fields_ = [(n, _p) for n in ("c0", "sf", "p0", "p1", "p2", "lv", "vslope", "sc", "Qf", "Qa",
-                                  "mspec", "An")] + \
+                                  "mspec", "An", "tab")] + \
                [(n, _d) for n in ("fl", "S", "ls_f", "sig_s", "zm", "ls_o", "total_volume")] + \
                [("B", _i64), ("has_flex", _i), ("has_asp", _i), ("has_zm", _i)]
 
@@ -336,15 +334,6 @@ def bin_scatter_il(src, perm, offsets, out, pre, npix, nbins):
     require_device(src, perm, offsets, out)
     _check(lib.nft_bin_scatter_il(ptr(src), ptr(perm), ptr(offsets), ptr(out), pre, npix, nbins,
                                   dtype_code(src.dtype), stream_ptr()))
-    return out
-
-
-def bin_sum_sorted(src, offsets, out, pre, nbins):
-    """out[p, b] = sum over bin b's contiguous run of src[i * pre + p]
-    (nft_bin_sum_sorted)"""
-    lib = load()
-    require_device(src, offsets, out)
-    _check(lib.nft_bin_sum_sorted(ptr(src), ptr(offsets), ptr(out), pre, nbins, dtype_code(src.dtype), stream_ptr()))
     return out
 
 

@@ -21,12 +21,6 @@ inline bool is_pow2(long long n) { return n > 0 && (n & (n - 1)) == 0; }
 
 inline bool rows_supported(int N) { return is_pow2(N) && N >= 8 && N <= 8192; }
 inline bool strided_supported(int N) { return is_pow2(N) && N >= 8 && N <= 512; }
-// single-pass strided transform of a long axis (1024 / 2048: L = 8 / 4
-// adjacent columns, 135-139 KB LDS, one 1024-thread workgroup per CU)
-inline bool longcol_supported(int N) {
-  static const int on = getenv("NFT_COL1P") ? atoi(getenv("NFT_COL1P")) : 0;
-  return on && (N == 1024 || N == 2048);
-}
 // lengths handled as a four-step pair of strided passes
 inline bool fourstep_supported(int N) { return is_pow2(N) && N >= 1024 && N <= 16384; }
 inline void fourstep_split(int N, int& N1, int& N2) {
@@ -94,10 +88,8 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     // measured slower at 2048^2 with 4 items for the r2c prologue and the
     // plain epilogue (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us), faster
     // for the CG-carrying epilogue, which is bound by its HBM traffic (the
-    // contiguous flavour, 231 -> 221 us): default there only; NFT_BATCH_REMAP
-    // = 0 / 1 / 2 sets it for every pass
-    static const int env_mode = getenv("NFT_BATCH_REMAP") ? atoi(getenv("NFT_BATCH_REMAP")) : -1;
-    const int mode = env_mode >= 0 ? env_mode : (f.cg ? 2 : 0);
+    // contiguous flavour, 231 -> 221 us): that pass only
+    const int mode = f.cg ? 2 : 0;
     if (mode > 0 && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) {
       b.bgroup = f.nb;
       b.bmode = mode;
@@ -113,7 +105,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     else
       ncu = 256;
   }
-  static const int per_cu = getenv("NFT_FFT_WG_PER_CU") ? atoi(getenv("NFT_FFT_WG_PER_CU")) : 8;
+  constexpr int per_cu = 8;
   static const char* const kind_name[4] = {"fft_c2c", "fft_r2c", "fft_h1d", "fft_unpack"};
   static const char* const kind_fused[4] = {"fft_c2c", "fft_r2c+pro", "fft_h1d+fused", "fft_unpack+epi"};
   prof_mark(s, a.f.cg ? "fft_unpack+cg" : (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
@@ -151,7 +143,6 @@ static int launch_n(int N, const FastArgs<T>& a, hipStream_t s) {
   } else {
     switch (N) {
       NFT_CASE(8) NFT_CASE(16) NFT_CASE(32) NFT_CASE(64) NFT_CASE(128) NFT_CASE(256) NFT_CASE(512)
-      NFT_CASE(1024) NFT_CASE(2048)
     }
   }
 #undef NFT_CASE

@@ -211,21 +211,14 @@ constexpr bool persist_ok() {
 }
 
 // in-line LDS padding of a pass (fft_fast.hpp padx): every 8 elements for
-// the strided passes; NFT_PAD_ROWS / NFT_PAD_COLS override at build time
-// values per load group of the CG-carrying unpack epilogue (build-time knob)
-#ifndef NFT_CG_CH
-#define NFT_CG_CH 1
-#endif
-#ifndef NFT_PAD_ROWS
-#define NFT_PAD_ROWS -1
-#endif
-#ifndef NFT_PAD_COLS
-#define NFT_PAD_COLS 3
-#endif
+// the strided passes, none for the row passes
 template <int N, bool ROWS>
 constexpr int pass_pad() {
-  return ROWS ? NFT_PAD_ROWS : NFT_PAD_COLS;
+  return ROWS ? -1 : 3;
 }
+// values per load group of the CG-carrying unpack epilogue (2 measured
+// 209 -> 219 us at 4 x 2048^2)
+constexpr int CG_CH_VALUES = 1;
 // line pitch in LDS: the (padded) length, +1 for strided passes so the L
 // lines' element x fall in different banks
 template <int N, bool ROWS>
@@ -486,7 +479,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         // x and r cannot pass the previous stores to x and r otherwise
         // (same arrays, runtime offsets), which serialised one memory
         // round trip per element
-        constexpr int CG_CH = NFT_CG_CH;
+        constexpr int CG_CH = CG_CH_VALUES;
         const T* __restrict__ ea = (const T*)a.f.ea;
         const T* __restrict__ eb = (const T*)a.f.eb;
         const T* __restrict__ cd = (const T*)a.f.cd;

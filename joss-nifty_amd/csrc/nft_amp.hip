@@ -45,30 +45,6 @@ __device__ __forceinline__ void amp_out_offset(nft_amp_out& o, long long off) {
 }
 
 
-// Pointer to workspace data exchanged between workgroups inside one fused
-// launch: every access is a relaxed agent-scope atomic (device-coherent
-// load / write-through store), so no cache flush is needed at the grid
-// barriers.  The multi-kernel path instantiates the same bodies with plain
-// pointers.
-struct XRef {
-  double* p;
-  __device__ __forceinline__ operator double() const {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __device__ __forceinline__ double operator=(double v) const {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v;
-  }
-};
-struct XPtr {
-  double* p;
-  __device__ __forceinline__ XRef operator[](long long i) const { return XRef{p + i}; }
-  __device__ __forceinline__ XPtr& operator+=(long long o) {
-    p += o;
-    return *this;
-  }
-};
-
 constexpr int AT = 256;          // threads per block
 constexpr int AE = 4;            // elements per thread
 constexpr int ABLK = AT * AE;    // elements per block
@@ -705,454 +681,17 @@ __global__ __launch_bounds__(AT) void amp_vjp_6(AmpConst c_, const AmpConst* __r
   amp_vjp_6_body<double*>(blockIdx.x, blockIdx.y, gridDim.x, sh, c_, dcs, o, g, const_cast<double*>(part1), np1, const_cast<double*>(part23), np23, const_cast<double*>(part45), np45, ls, vs, wsd);
 }
 
-// ------------------------------------------------------------------ fused
-// One launch per JVP / VJP.  The workgroups of the grid are all resident
-// (the launcher checks occupancy), so the phases of the JVP / VJP -- scans,
-// their carries, the global sums of the normalisation -- are separated by
-// grid barriers instead of kernel boundaries, and every tile keeps its values
-// in registers from phase to phase (no loc / dapre / gapre round trips).
-// Workgroup i owns scan tile i (E*AT consecutive j = b - 2) of EVERY
-// right-hand side; block 0 also owns bins 0 and 1.  Carries and sums are the
-// same fixed-order sums as the multi-kernel path (tile totals in index order,
-// thread-strided then wave/LDS reduction), so results are deterministic.
-
-constexpr int NFT_FALLBACK = 1;  // fused path not applicable
-
-// Hierarchical: workgroup w arrives at group counter w % NG (its own 128-B
-// line); the last arrival of a group arrives at the top counter; the last
-// top arrival resets the counters and advances every group's generation
-// word, which only that group's workgroups poll.  Spreading arrivals and
-// polls over NG lines keeps the memory-side atomics off one hot address.
-constexpr int NG = 16;
-struct GridBar {
-  unsigned top, topgen, err, pad0[29];
-  struct {
-    unsigned count, gen, pad[30];
-  } grp[NG];
-};
-__device__ GridBar g_amp_bar[3];  // [0] JVP, [1] VJP, [2] probe (one stream per device)
-
-// The data handed between workgroups is read and written device-coherently
-// (XPtr), so arriving needs only this workgroup's stores to be complete.
-// The wait is bounded (about a second), so a logic error cannot hang the
-// GPU; err records it.
-__device__ __forceinline__ void grid_sync(GridBar* b) {
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned G = gridDim.x, w = blockIdx.x;
-    const unsigned q = w % NG;
-    const unsigned ng = G < NG ? G : NG;                  // groups in use
-    const unsigned gsize = G / NG + (q < G % NG ? 1 : 0);  // members of group q
-    auto& gr = b->grp[q];
-    const unsigned g0 = __hip_atomic_load(&gr.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bool last = false;
-    if (__hip_atomic_fetch_add(&gr.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
-      __hip_atomic_store(&gr.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
-      if (__hip_atomic_fetch_add(&b->top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
-        __hip_atomic_store(&b->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0);
-        for (unsigned k = 0; k < ng; ++k)
-          __hip_atomic_fetch_add(&b->grp[k].gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = true;
-      }
-    }
-    if (!last) {
-      int spins = 0;
-      while (__hip_atomic_load(&gr.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 22)) {
-          __hip_atomic_fetch_or(&b->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// barrier cost probe: nbar back-to-back grid barriers
-__global__ __launch_bounds__(AT) void amp_barrier_probe(int nbar) {
-  for (int k = 0; k < nbar; ++k) grid_sync(&g_amp_bar[2]);
-}
-
 static int nblk(long long n, int per) { return (int)std::max<long long>(1, (n + per - 1) / per); }
 
 // batched launches of the multi-kernel JVP / VJP: XCD-grouped right-hand
 // sides (amp_block) for the kernels it was measured to help (pref: the two
 // JVP scans, -3 us together at B = 313,847 with 4 RHS; the others measured
-// -0.5 to +1 us, within noise), never for a single right-hand side.
-// NFT_AMP_REMAP=0 / 2: off / on for every kernel.
-static bool amp_remap(unsigned ny, bool pref) {
-  static const int mode = getenv("NFT_AMP_REMAP") ? atoi(getenv("NFT_AMP_REMAP")) : 1;
-  return ny > 1 && (mode == 2 || (mode == 1 && pref));
-}
+// -0.5 to +1 us, within noise), never for a single right-hand side
+static bool amp_remap(unsigned ny, bool pref) { return ny > 1 && pref; }
 static dim3 amp_grid(int nbx, unsigned ny, bool pref = false) {
   return amp_remap(ny, pref) ? dim3((unsigned)(((nbx + 7) & ~7) * ny)) : dim3((unsigned)nbx, ny);
 }
 static int amp_nbx(int nbx, unsigned ny, bool pref = false) { return amp_remap(ny, pref) ? nbx : 0; }
-
-// Fused kernels: one launch per JVP / VJP.  Workgroup w owns scan tile
-// i = w % nbM (E*AT consecutive scan positions j = b - 2, striped) of
-// right-hand side r = w / nbM, and keeps that tile's values in registers
-// through every phase (block 0 of each RHS also owns bins 0 and 1).  Only
-// the tile totals / partial sums cross workgroups (XPtr, device-coherent);
-// the phases are separated by grid barriers, which needs every workgroup
-// resident: the launcher checks the occupancy and otherwise takes the
-// multi-kernel path.  Carries and global sums are fixed-order sums of the
-// tile totals (thread-strided, then the wave / LDS reduction of
-// block_total), so the results are deterministic and independent of how
-// many right-hand sides share the launch.
-
-template <int E, bool REV>
-__device__ __forceinline__ double scan_e(double (&v)[E], double* sh) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  constexpr int NW = AT / 64;
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    double x = v[k];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double y = REV ? __shfl_down(x, off, 64) : __shfl_up(x, off, 64);
-      if (REV ? (lane + off < 64) : (lane >= off)) x += y;
-    }
-    v[k] = x;
-    if (lane == (REV ? 0 : 63)) sh[k * NW + w] = x;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    const int me = k * NW + w;
-    double off = 0.0;
-    if (!REV) {
-      for (int q = 0; q < me; ++q) off += sh[q];
-    } else {
-      for (int q = E * NW - 1; q > me; --q) off += sh[q];
-    }
-    v[k] += off;
-  }
-  double t = 0.0;
-  if (!REV) {
-    for (int q = 0; q < E * NW; ++q) t += sh[q];
-  } else {
-    for (int q = E * NW - 1; q >= 0; --q) t += sh[q];
-  }
-  __syncthreads();
-  return t;
-}
-
-// fixed-order sum of p[q], q in [lo, hi) (REV: descending), coherent reads
-__device__ __forceinline__ double xsum(XPtr p, int lo, int hi, bool rev, double* sh) {
-  double s = 0;
-  if (!rev) {
-    for (int q = lo + threadIdx.x; q < hi; q += AT) s += p[q];
-  } else {
-    for (int q = hi - 1 - threadIdx.x; q >= lo; q -= AT) s += p[q];
-  }
-  return block_total(s, sh);
-}
-
-template <int E, bool DCS>
-__global__ __launch_bounds__(AT) void amp_jvp_fused(AmpConst c_, const AmpConst* __restrict__ dcs, int nbM,
-                                                    const double* tfl, const double* tsl, const double* tflex,
-                                                    const double* tasp, const double* tzm, const double* tspec,
-                                                    double* __restrict__ da, double* ws, long long ls, long long vs,
-                                                    long long wsd, long long des) {
-  __shared__ double sh[E * AT / 64 + 8];
-  const int r = blockIdx.x / nbM, i = blockIdx.x - r * nbM;
-  const AmpConst& c = DCS ? dcs[r] : c_;
-  const long long B = c.B, M = B - 2;
-  const bool flex = c.has_flex, asp = c.has_asp;
-  const long long j0 = (long long)i * (E * AT) + threadIdx.x;
-  const XPtr agg1{ws + r * wsd}, agg2{ws + r * wsd + nbM}, part{ws + r * wsd + 2 * nbM};
-  const double* ts = tspec ? tspec + r * ls : nullptr;
-  double v[E];
-  if (flex) {
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-      const long long j = j0 + (long long)k * AT;
-      v[k] = j < M ? ts[M + j] * c.sf[j] : 0.0;
-    }
-    double t = scan_e<E, false>(v, sh);
-    if (threadIdx.x == 0) agg1[i] = t;
-    grid_sync(&g_amp_bar[0]);
-    const double carry = xsum(agg1, 0, i, false, sh);
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-      const long long j = j0 + (long long)k * AT;
-      if (j < M) {
-        const double cj = v[k] + carry;
-        const double u1 = ts[M + j] * c.sf[j];
-        const double cp = cj - u1;
-        v[k] = (cj + cp) / 2 * c.lv[j] + ts[j] * c.c0[j];
-      } else {
-        v[k] = 0.0;
-      }
-    }
-    t = scan_e<E, false>(v, sh);
-    if (threadIdx.x == 0) agg2[i] = t;
-    grid_sync(&g_amp_bar[0]);
-  }
-  // dapre (kept in v) and the partial sum of mspec * dapre
-  double T = 0, cr = 0;
-  if (flex) {
-    T = xsum(agg2, 0, nbM, false, sh);
-    cr = xsum(agg2, 0, i, false, sh);
-  }
-  const double ssl = c.sig_s * tsl[r * ls];
-  const double sf_ = flex ? tflex[r * ls] : 0.0;
-  const double sa_ = asp ? tasp[r * ls] : 0.0;
-  const bool own01 = (i == 0 && threadIdx.x < 2);
-  double acc = 0.0, x01 = 0.0;
-  if (own01) {
-    const long long b = threadIdx.x;
-    double d = c.vslope[b] * ssl - T * c.sc[b];
-    if (flex) d += sf_ * c.Qf[b];
-    if (asp) d += sa_ * c.Qa[b];
-    x01 = d;
-    acc += c.mspec[b] * d;
-  }
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    const long long j = j0 + (long long)k * AT;
-    if (j < M) {
-      const long long b = j + 2;
-      const double tl = flex ? v[k] + cr : 0.0;
-      double d = c.vslope[b] * ssl + tl - T * c.sc[b];
-      if (flex) d += sf_ * c.Qf[b];
-      if (asp) d += sa_ * c.Qa[b];
-      v[k] = d;
-      acc += c.mspec[b] * d;
-    }
-  }
-  acc = block_total(acc, sh);
-  if (threadIdx.x == 0) part[i] = acc;
-  grid_sync(&g_amp_bar[0]);
-  const double dS = xsum(part, 0, nbM, false, sh);
-  double* d_ = da + r * vs;
-  const double dfl = c.fl * c.ls_f * tfl[r * ls];
-  if (own01) {
-    const long long b = threadIdx.x;
-    double val;
-    if (b == 0) {
-      val = c.has_zm ? c.zm * c.ls_o * tzm[r * ls] : 0.0;
-    } else {
-      const double An = c.An[b];
-      val = dfl * An + c.fl * An * (x01 / 2. - dS / (2. * c.S));
-    }
-    d_[b * des] = val * c.total_volume;
-  }
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    const long long j = j0 + (long long)k * AT;
-    if (j < M) {
-      const long long b = j + 2;
-      const double An = c.An[b];
-      d_[b * des] = (dfl * An + c.fl * An * (v[k] / 2. - dS / (2. * c.S))) * c.total_volume;
-    }
-  }
-}
-
-template <int E, bool DCS>
-__global__ __launch_bounds__(AT) void amp_vjp_fused(AmpConst c_, const AmpConst* __restrict__ dcs, int nbM, AmpOut o,
-                                                    const double* __restrict__ g, double* ws, long long ls,
-                                                    long long vs, long long wsd) {
-  __shared__ double sh[E * AT / 64 + 8];
-  const int r = blockIdx.x / nbM, i = blockIdx.x - r * nbM;
-  const AmpConst& c = DCS ? dcs[r] : c_;
-  const long long B = c.B, M = B - 2;
-  const bool flex = c.has_flex, asp = c.has_asp;
-  const long long j0 = (long long)i * (E * AT) + threadIdx.x;
-  double* w0 = ws + r * wsd;
-  const XPtr p1{w0}, p2{w0 + nbM}, p3{w0 + 2 * nbM}, a3{w0 + 3 * nbM}, a4{w0 + 4 * nbM}, p4{w0 + 5 * nbM},
-      p5{w0 + 6 * nbM};
-  amp_out_offset(o, r * ls);
-  const double* gr = g + r * vs;
-  const bool own01 = (i == 0 && threadIdx.x < 2);
-  // R1 = sum_{b >= 1} TV * g_b * An_b
-  double s = 0.0;
-  if (own01 && threadIdx.x == 1) s += c.total_volume * gr[1] * c.An[1];
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    const long long j = j0 + (long long)k * AT;
-    if (j < M) s += c.total_volume * gr[j + 2] * c.An[j + 2];
-  }
-  s = block_total(s, sh);
-  if (threadIdx.x == 0) p1[i] = s;
-  grid_sync(&g_amp_bar[1]);
-  const double R1 = xsum(p1, 0, nbM, false, sh);
-  const double kk = c.fl * R1 / (2. * c.S);
-  auto gapre = [&](long long b) {
-    const double gm = b > 0 ? c.total_volume * gr[b] : 0.0;
-    const double gAn = c.fl * gm;
-    return c.An[b] * gAn / 2. - c.mspec[b] * kk;
-  };
-  // gapre (v); partial sums R2 = sum vslope * gapre, R3 = sum gapre * sc
-  double v[E], u[E];
-  double s2 = 0.0, s3 = 0.0;
-  if (own01) {
-    const long long b = threadIdx.x;
-    const double ga = gapre(b);
-    s2 += c.vslope[b] * ga;
-    s3 += ga * c.sc[b];
-  }
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    const long long j = j0 + (long long)k * AT;
-    v[k] = 0.0;
-    if (j < M) {
-      const long long b = j + 2;
-      const double ga = gapre(b);
-      v[k] = ga;
-      s2 += c.vslope[b] * ga;
-      s3 += ga * c.sc[b];
-    }
-  }
-  s2 = block_total(s2, sh);
-  s3 = block_total(s3, sh);
-  if (threadIdx.x == 0) {
-    p2[i] = s2;
-    p3[i] = s3;
-  }
-  grid_sync(&g_amp_bar[1]);
-  double R4 = 0.0, R5 = 0.0;
-  if (flex) {
-    const double R3 = xsum(p3, 0, nbM, false, sh);
-    // gtl_j = gapre_{j+2} - [j+2 == B-1] R3 (kept in u for y_{j+1} = y_j - gtl_j); reverse scan
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-      const long long j = j0 + (long long)k * AT;
-      if (j < M) v[k] -= (j + 2 == B - 1 ? R3 : 0.0);
-      u[k] = v[k];
-    }
-    double t = scan_e<E, true>(v, sh);
-    if (threadIdx.x == 0) a3[i] = t;
-    grid_sync(&g_amp_bar[1]);
-    double carry = xsum(a3, i + 1, nbM, true, sh);
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-      const long long j = j0 + (long long)k * AT;
-      if (j < M) {
-        const double yj = v[k] + carry;
-        v[k] = yj;
-        const double zj = yj * c.lv[j] / 2.;
-        double zn = 0.0;
-        if (j + 1 < M) zn = (yj - u[k]) * c.lv[j + 1] / 2.;
-        u[k] = zj + zn;
-      } else {
-        u[k] = 0.0;
-      }
-    }
-    t = scan_e<E, true>(u, sh);
-    if (threadIdx.x == 0) a4[i] = t;
-    grid_sync(&g_amp_bar[1]);
-    carry = xsum(a4, i + 1, nbM, true, sh);
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-      const long long j = j0 + (long long)k * AT;
-      if (j < M) {
-        const double g0 = v[k];
-        const double g1 = u[k] + carry;
-        double t0 = g0 * c.c0[j], t1 = g1 * c.sf[j];
-        if (o.dspec) {
-          t0 += o.shift * o.dspec[j];
-          t1 += o.shift * o.dspec[M + j];
-        }
-        o.spec[j] = t0;
-        o.spec[M + j] = t1;
-        R4 += g0 * c.p0[j] + g1 * c.p2[j];
-        if (asp) R5 += g0 * c.p1[j];
-      }
-    }
-    R4 = block_total(R4, sh);
-    R5 = block_total(R5, sh);
-    if (threadIdx.x == 0) {
-      p4[i] = R4;
-      p5[i] = R5;
-    }
-    grid_sync(&g_amp_bar[1]);
-  }
-  if (i != 0) return;
-  // scalar cotangents (block 0 of each RHS)
-  const double R2 = xsum(p2, 0, nbM, false, sh);
-  if (flex) {
-    R4 = xsum(p4, 0, nbM, false, sh);
-    R5 = xsum(p5, 0, nbM, false, sh);
-  }
-  if (threadIdx.x == 0) {
-    const double sh_ = o.shift;
-    o.fl[0] = c.fl * c.ls_f * R1 + (o.dfl ? sh_ * o.dfl[0] : 0.0);
-    o.sl[0] = c.sig_s * R2 + (o.dsl ? sh_ * o.dsl[0] : 0.0);
-    if (flex) o.flex[0] = R4 + (o.dflex ? sh_ * o.dflex[0] : 0.0);
-    if (asp) o.asp[0] = R5 + (o.dasp ? sh_ * o.dasp[0] : 0.0);
-    if (c.has_zm) o.zm[0] = c.zm * c.ls_o * c.total_volume * gr[0] + (o.dzm ? sh_ * o.dzm[0] : 0.0);
-  }
-}
-
-// grid of the fused kernels: every workgroup resident at once (occupancy x
-// CUs), at most the largest phase's block count
-static int resident_cap(const void* fn) {
-  int dev = 0, ncu = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, AT, 0) != hipSuccess) return 0;
-  return ncu * per;
-}
-
-// Opt-in (NFT_AMP_FUSED=1).  Measured at the C3 size (B = 313,847, 4 RHS,
-// MI355X): fused 56 + 85 us against 54 + 78 us for the ten stream-ordered
-// kernels -- a grid barrier over ~1,200 resident workgroups costs 3-6 us,
-// the same as a kernel boundary inside a HIP graph, and each phase keeps
-// its dependent-load latency either way.
-static bool fused_enabled() {
-  static const int on = getenv("NFT_AMP_FUSED") ? atoi(getenv("NFT_AMP_FUSED")) : 0;
-  return on != 0;
-}
-
-
-template <int E>
-static int jvp_fused_try(const AmpConst& c, const AmpConst* dcs, int nr, const double* tfl, const double* tsl,
-                         const double* tflex, const double* tasp, const double* tzm, const double* tspec, double* da,
-                         double* ws, long long ls, long long vs, long long wsd, long long des, hipStream_t s) {
-  static int cap[2] = {-1, -1};
-  const int d = dcs != nullptr;
-  if (cap[d] < 0)
-    cap[d] = resident_cap(d ? (const void*)amp_jvp_fused<E, true> : (const void*)amp_jvp_fused<E, false>);
-  const int nbM = nblk(c.B - 2, E * AT);
-  const long long G = (long long)nr * nbM;
-  if (G > cap[d] || 3LL * nbM > wsd) return NFT_FALLBACK;
-  prof_mark(s, "amp_jvp");
-  if (d)
-    hipLaunchKernelGGL((amp_jvp_fused<E, true>), dim3((unsigned)G), dim3(AT), 0, s, c, dcs, nbM, tfl, tsl, tflex,
-                       tasp, tzm, tspec, da, ws, ls, vs, wsd, des);
-  else
-    hipLaunchKernelGGL((amp_jvp_fused<E, false>), dim3((unsigned)G), dim3(AT), 0, s, c, dcs, nbM, tfl, tsl, tflex,
-                       tasp, tzm, tspec, da, ws, ls, vs, wsd, des);
-  NFT_HIP_CHECK(hipGetLastError());
-  return NFT_OK;
-}
-
-template <int E>
-static int vjp_fused_try(const AmpConst& c, const AmpConst* dcs, int nr, const AmpOut& o, const double* g,
-                         double* ws, long long ls, long long vs, long long wsd, hipStream_t s) {
-  static int cap[2] = {-1, -1};
-  const int d = dcs != nullptr;
-  if (cap[d] < 0)
-    cap[d] = resident_cap(d ? (const void*)amp_vjp_fused<E, true> : (const void*)amp_vjp_fused<E, false>);
-  const int nbM = nblk(c.B - 2, E * AT);
-  const long long G = (long long)nr * nbM;
-  if (G > cap[d] || 7LL * nbM > wsd) return NFT_FALLBACK;
-  prof_mark(s, "amp_vjp");
-  if (d)
-    hipLaunchKernelGGL((amp_vjp_fused<E, true>), dim3((unsigned)G), dim3(AT), 0, s, c, dcs, nbM, o, g, ws, ls, vs, wsd);
-  else
-    hipLaunchKernelGGL((amp_vjp_fused<E, false>), dim3((unsigned)G), dim3(AT), 0, s, c, dcs, nbM, o, g, ws, ls, vs,
-                       wsd);
-  NFT_HIP_CHECK(hipGetLastError());
-  return NFT_OK;
-}
-
 
 // ------------------------------------------------------------------ forward
 // Amplitude value and linearisation constants at nrow latent points
@@ -1402,6 +941,7 @@ __global__ __launch_bounds__(AT) void amp_fwd_4(AmpModel m, FwdLat x, double* bu
     c.Qa = fx && m.has_asp ? w.Qa : nullptr;
     c.mspec = w.mspec;
     c.An = w.An;
+    c.tab = nullptr;  // nft_amp2_prepare fills it on first use
     c.fl = sc.fl;
     c.S = S;
     c.ls_f = m.ls_f;
@@ -1449,13 +989,6 @@ int nft_amp_jvp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
                                 s);
     if (st != NFT_AMP2_FALLBACK) return st;
   }
-  if (fused_enabled() && M >= 1) {
-    const long long des = da_elem_stride > 0 ? da_elem_stride : 1;
-    int st = jvp_fused_try<4>(c, dcs, nrhs, tfl, tsl, tflex, tasp, tzm, tspec, da, ws, ls, vs, wsd, des, s);
-    if (st == NFT_FALLBACK)
-      st = jvp_fused_try<8>(c, dcs, nrhs, tfl, tsl, tflex, tasp, tzm, tspec, da, ws, ls, vs, wsd, des, s);
-    if (st != NFT_FALLBACK) return st;
-  }
   const unsigned ny = (unsigned)nrhs;
   if (c.has_flex) {
     prof_mark(s, "amp_jvp_1");
@@ -1502,11 +1035,6 @@ int nft_amp_vjp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
                                 nullptr, 0, 0, 0, s);
     if (st != NFT_AMP2_FALLBACK) return st;
   }
-  if (fused_enabled() && M >= 1) {
-    int st = vjp_fused_try<4>(c, dcs, nrhs, o, g, ws, ls, vs, wsd, s);
-    if (st == NFT_FALLBACK) st = vjp_fused_try<8>(c, dcs, nrhs, o, g, ws, ls, vs, wsd, s);
-    if (st != NFT_FALLBACK) return st;
-  }
   const unsigned ny = (unsigned)nrhs;
   prof_mark(s, "amp_vjp_1");
   hipLaunchKernelGGL(amp_vjp_1, amp_grid(nr, ny), dim3(AT), 0, s, amp_nbx(nr, ny), c, dcs, g, part1, ls, vs, wsd);
@@ -1524,16 +1052,6 @@ int nft_amp_vjp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
   prof_mark(s, "amp_vjp_6");
   hipLaunchKernelGGL(amp_vjp_6, dim3(1, ny), dim3(AT), 0, s, c, dcs, o, g, part1, nr, part23, nr, part45,
                      c.has_flex ? nbM : 0, ls, vs, wsd);
-  NFT_HIP_CHECK(hipGetLastError());
-  return NFT_OK;
-}
-
-// tuning probe (not part of the public header): nbar grid barriers over G
-// workgroups (G <= 0: the fused kernels' resident capacity)
-int nft_amp_barrier_probe(int nbar, int G, hipStream_t s) {
-  if (G <= 0) G = resident_cap((const void*)amp_vjp_fused<4, false>);
-  prof_mark(s, "amp_barrier_probe");
-  hipLaunchKernelGGL(amp_barrier_probe, dim3(G), dim3(AT), 0, s, nbar);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

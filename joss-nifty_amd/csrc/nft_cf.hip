@@ -408,6 +408,7 @@ template <typename T, int PRE, int CH>
 __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, const int* __restrict__ perm,
                                                       const int* __restrict__ offs, T* __restrict__ out,
                                                       long long npix, long long nbins, int nchunks) {
+  static_assert(CH % 256 == 0, "bin_scatter_il loads CH / 256 positions per thread");
   constexpr int PER = CH / 256;
   __shared__ T vals[PRE][CH];
   __shared__ int bnd[2];
@@ -466,26 +467,6 @@ __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, 
   }
 }
 
-// out[p * nbins + b] = sum of in[i * pre + p] over i in [offs[b], offs[b+1])
-// in ascending i, from 0 (the per-bin order of bin_scatter_chunk: bitwise)
-template <typename T, int PRE>
-__global__ __launch_bounds__(256) void bin_sum_sorted(const T* __restrict__ in, const int* __restrict__ offs,
-                                                      T* __restrict__ out, long long nbins, int pre) {
-  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbins) return;
-  const int a = offs[b], e = offs[b + 1];
-  T acc[PRE];
-#pragma unroll
-  for (int p = 0; p < PRE; ++p) acc[p] = (T)0;
-  for (int i = a; i < e; ++i) {
-#pragma unroll
-    for (int p = 0; p < PRE; ++p)
-      if (p < pre) acc[p] += in[(long long)i * pre + p];
-  }
-#pragma unroll
-  for (int p = 0; p < PRE; ++p)
-    if (p < pre) out[p * nbins + b] = acc[p];
-}
 
 // I: index type -- 32-bit when pre * nin < 2^31 (the usual case: cheaper
 // div/mod per element), 64-bit otherwise
@@ -596,22 +577,14 @@ int nft_bin_scatter_ordered(const void* in, const int* perm, const int* offsets,
       return NFT_OK;
     }
     prof_mark(stream, "bin_scatter");
-    // K > 1 measured slower (2048^2, 4 items: K=1 109 us, K=2 118, K=4 133): default 1
-    static const int kmax = getenv("NFT_SCATTER_K") ? atoi(getenv("NFT_SCATTER_K")) : 1;
-    const int K = (pre % 4 == 0 && kmax >= 4) ? 4 : ((pre % 2 == 0 && kmax >= 2) ? 2 : 1);
-    const dim3 grid(nb, (unsigned)(pre / K));
+    // one item per workgroup row (several items per workgroup measured slower
+    // at 2048^2, 4 items: 109 us for one, 118 for two, 133 for four)
+    const dim3 grid(nb, (unsigned)pre);
 #define NFT_SCAT(TT, KK)                                                                                 \
   hipLaunchKernelGGL((bin_scatter_chunk<TT, KK>), grid, dim3(256), 0, stream, (const TT*)in, perm, offsets, gpix, \
                      (const unsigned short*)gslot, cbins, (TT*)out, (long long)npix, (long long)nbins, nchunks)
-    if (dtype == 0) {
-      if (K == 4) NFT_SCAT(double, 4);
-      else if (K == 2) NFT_SCAT(double, 2);
-      else NFT_SCAT(double, 1);
-    } else {
-      if (K == 4) NFT_SCAT(float, 4);
-      else if (K == 2) NFT_SCAT(float, 2);
-      else NFT_SCAT(float, 1);
-    }
+    if (dtype == 0) NFT_SCAT(double, 1);
+    else NFT_SCAT(float, 1);
 #undef NFT_SCAT
     NFT_HIP_CHECK(hipGetLastError());
     return NFT_OK;
@@ -658,8 +631,8 @@ int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const in
   const long long tot = pre * fs.nout;
   if (tot <= 0) return NFT_OK;
   prof_mark(stream, "bin_fold");
-  // one workgroup per output row (NFT_FOLD_ROWS=0: the element-per-thread kernel)
-  static const bool rows = !getenv("NFT_FOLD_ROWS") || atoi(getenv("NFT_FOLD_ROWS")) != 0;
+  // one workgroup per output row
+  constexpr bool rows = true;
   const long long nouter = tot / fs.h[ndim - 1];
   const unsigned rgrid = (unsigned)std::min<long long>(nouter, 1LL << 20);
   if (rows && dtype == 0)
@@ -730,9 +703,8 @@ int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t
   return NFT_OK;
 }
 
-#ifndef NFT_SIL_CH
-#define NFT_SIL_CH 2048  // build knob: bin-sorted positions x items per nft_bin_scatter_il workgroup
-#endif
+// bin-sorted positions x items per nft_bin_scatter_il workgroup (4096 measured 31 -> 36 us)
+constexpr int SIL_CH = 2048;
 int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void* out, int64_t pre, int64_t npix,
                        int64_t nbins, int dtype, hipStream_t stream) {
   if (!(pre == 2 || pre == 4 || pre == 8) || npix < 0 || nbins < 0 || !perm || !offsets) {
@@ -747,7 +719,7 @@ int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void
   prof_mark(stream, "bin_scatter");
 #define NFT_SIL(TT, PP)                                                                                       \
   {                                                                                                           \
-    constexpr int CH = NFT_SIL_CH / PP >= 256 ? NFT_SIL_CH / PP : 256;                                       \
+    constexpr int CH = SIL_CH / PP >= 256 ? (SIL_CH / PP) / 256 * 256 : 256;                                 \
     const int nch = (int)((npix + CH - 1) / CH);                                                              \
     const unsigned nb = (unsigned)(((nch + NXCD - 1) / NXCD) * NXCD);                                         \
     hipLaunchKernelGGL((bin_scatter_il<TT, PP, CH>), dim3(nb), dim3(256), 0, stream, (const TT*)in, perm, offsets, \
@@ -762,37 +734,6 @@ int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void
     return NFT_ERR_ARG;
   }
 #undef NFT_SIL
-  NFT_HIP_CHECK(hipGetLastError());
-  return NFT_OK;
-}
-
-int nft_bin_sum_sorted(const void* in, const int* offsets, void* out, int64_t pre, int64_t nbins, int dtype,
-                       hipStream_t stream) {
-  if (pre < 1 || pre > 8 || nbins < 0 || !offsets) {
-    set_last_error("nft_bin_sum_sorted: need 1 <= pre <= 8, nbins >= 0 and offsets");
-    return NFT_ERR_ARG;
-  }
-  if (nbins == 0) return NFT_OK;
-  prof_mark(stream, "bin_scatter");
-  const unsigned grid = (unsigned)((nbins + 255) / 256);
-#define NFT_BS(TT, PP)                                                                                        \
-  hipLaunchKernelGGL((bin_sum_sorted<TT, PP>), dim3(grid), dim3(256), 0, stream, (const TT*)in, offsets, (TT*)out, \
-                     (long long)nbins, (int)pre)
-  if (dtype == 0) {
-    if (pre <= 1) NFT_BS(double, 1);
-    else if (pre <= 2) NFT_BS(double, 2);
-    else if (pre <= 4) NFT_BS(double, 4);
-    else NFT_BS(double, 8);
-  } else if (dtype == 1) {
-    if (pre <= 1) NFT_BS(float, 1);
-    else if (pre <= 2) NFT_BS(float, 2);
-    else if (pre <= 4) NFT_BS(float, 4);
-    else NFT_BS(float, 8);
-  } else {
-    set_last_error("nft_bin_sum_sorted: bad dtype");
-    return NFT_ERR_ARG;
-  }
-#undef NFT_BS
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

@@ -23,7 +23,6 @@
 #include <vector>
 
 #include "fast_dispatch.hpp"
-#include "fast_pro.hpp"
 #include "fft_passes.hpp"
 #include <type_traits>
 
@@ -173,15 +172,7 @@ static bool plan_fits(const FftPlanDev& p, int L, int NT) {
   return true;
 }
 
-static size_t lds_budget() {
-  static size_t b = 0;
-  if (b == 0) {
-    const char* e = getenv("NFT_LDS_BUDGET");
-    b = e ? (size_t)atol(e) : (size_t)65536;
-    if (b > 163840) b = 163840;
-  }
-  return b;
-}
+static size_t lds_budget() { return (size_t)65536; }
 
 // choose NT, L, pitch for a pass of length n, element size es, tiling mode
 struct LaunchCfg {
@@ -483,32 +474,6 @@ static LineDesc make_desc(const Geo& g, const long long* cs, const std::vector<i
 }
 
 // geometry covered by hartley_v2's multi-axis path
-static bool v2_multi_ok(const Geo& g, const std::vector<int>& ax) {
-  using namespace fast;
-  const int m = (int)ax.size();
-  if (m < 2) return false;
-  const int h = ax[m - 1];
-  if (h != g.nd - 1 || !rows_supported((int)g.shape[h])) return false;
-  for (int k = 1; k < m - 1; ++k)
-    if (!strided_supported((int)g.shape[ax[k]])) return false;
-  const int N0 = (int)g.shape[ax[0]];
-  return strided_supported(N0) || fourstep_supported(N0);
-}
-
-// Last (unpack) pass with an epilogue whose operands (A, xi0) are shared by
-// the batch: the lines of 2^los items sit side by side in one tile, so the
-// items' reads of the shared operands hit the same CU's cache instead of
-// going to HBM once per item (NFT_EPI_LO = los).  Measured slower at 4 x
-// 2048^2 (140 / 152 / 163 us for los = 0 / 1 / 2: the narrower column runs
-// of each item cost more than the re-reads save), so off by default
-static int epi_los(const fast::FuseArgs* fz, long long O) {
-  static const int want = getenv("NFT_EPI_LO") ? atoi(getenv("NFT_EPI_LO")) : 0;
-  if (!fz || !fz->epi || fz->cg || fz->P <= 0 || fz->nb < 2) return 0;
-  if ((fz->ea && fz->sea) || (fz->eb && fz->seb)) return 0;
-  int los = want;
-  while (los > 0 && (O % (1LL << los)) != 0) --los;
-  return los;
-}
 
 // r2c_done: the R2C row pass has already written the half spectra to ws
 template <typename T>
@@ -595,7 +560,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
     const long long O = prod(cs, 0, axis);
     const long long rrs = prod(g.shape, axis + 1, g.nd);
     LineDesc desc = make_desc(g, cs, ax, axis, h);
-    if (strided_supported(N) || longcol_supported(N)) {
+    if (strided_supported(N)) {
       FastArgs<T> a;
       memset(&a, 0, sizeof(a));
       a.in = ws;
@@ -617,7 +582,6 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
         a.f = *fz;
         a.f.pro = 0;
       }
-      a.los = epi_los(fz, O);
       return launch<T>(K_UNPACK, false, N, a, s);
     }
     int N1, N2;
@@ -664,7 +628,6 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
         a.f = *fz;
         a.f.pro = 0;
       }
-      a.los = epi_los(fz, O);
       return launch<T>(K_UNPACK, false, N2, a, s);
     }
   }
@@ -747,10 +710,9 @@ __global__ __launch_bounds__(256) void pro_batch_kernel(fast::FuseArgs f, T* __r
 // D (the number of transform axes) is a template parameter so that the cell
 // coordinates and the per-item values stay in registers (a runtime D put
 // them in scratch).
-// images per load group of the folded prologue (build-time knob; 0: 16 / NBM)
-#ifndef NFT_PRO_G
-#define NFT_PRO_G 2
-#endif
+// images per load group of the folded prologue (1 / 4 measured 136 / 203 us
+// against 132 for 2 at 4 x 2048^2)
+constexpr int PRO_G = 2;
 template <typename T, int D, int NBM, bool PI>
 __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __restrict__ u, long long P, int nb,
                                                        long long ncell) {
@@ -799,7 +761,7 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
   // and per-image load / store pairs would serialise one memory round trip
   // per image and item
   constexpr int NIMG = 1 << D;
-  constexpr int G0 = NFT_PRO_G > 0 ? NFT_PRO_G : (16 / NBM > 0 ? 16 / NBM : 1);
+  constexpr int G0 = PRO_G;
   constexpr int G = G0 < NIMG ? G0 : NIMG;
   for (long long c = (long long)blockIdx.x * 256 + threadIdx.x; c < ncell; c += (long long)gridDim.x * 256) {
     unsigned cc[D], rest = (unsigned)c;
@@ -962,49 +924,17 @@ template <typename T>
 static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out, const Geo& g,
                               const std::vector<int>& ax, int sigma, double scale, void* ws, size_t ws_bytes,
                               size_t hws, hipStream_t s) {
-  static const bool v1_only = getenv("NFT_ENGINE_V1") != nullptr;
-  static const bool no_split = getenv("NFT_NO_PRO_SPLIT") != nullptr;
   const long long ntot = prod(g.shape, 0, g.nd);
-  // R2C+prologue in one pass (fast_pro.hpp): bitwise equal to the split
-  // path, but measured slower at 4 x 2048^2 (209 vs 128 + 73 us: the dA
-  // gathers, 32 B per pixel from a 10 MB table, stay latency-bound inside
-  // the FFT workgroup) -- opt-in, NFT_PRO_PAIRS=1
-  static const bool pairs = getenv("NFT_PRO_PAIRS") != nullptr;
-  if (!v1_only && pairs && !f.dr && f.pro && (f.pa || f.pb) && f.sa == 0 && f.sb == 0 && f.P > 0 && f.nb >= 1 &&
-      (long long)f.nb * f.P == ntot && v2_multi_ok(g, ax)) {
-    // R2C row pass with the prologue, the items' rows paired as in the plain pass
-    const int N = (int)g.shape[g.nd - 1];
-    const long long rows = f.P / N;
-    const int L = fast::pro_pairs_group(N, f.nb);
-    if (N >= 512 && N <= 4096 && f.P % N == 0 && rows % 2 == 0 && L > 0) {
-      long long cs[MAXD];
-      half_shape(g, g.nd - 1, cs);
-      const long long ostride = rows * cs[g.nd - 1];
-      int st = fast::launch_pro_pairs<T>(N, f, ws, rows, f.nb, ostride, cs[g.nd - 1], s);
-      if (st == NFT_OK) {
-        fast::FuseArgs f2 = f;
-        f2.pro = 0;
-        f2.px = f2.pa = f2.pb = f2.pc = nullptr;
-        f2.pidx = nullptr;
-        return hartley_v2<T>(nullptr, out, g, ax, sigma, scale, ws, hws, s, &f2, true);
-      }
-      if (st != 1) return st;
-    }
-  }
-  if (f.dr && !(f.fnd > 0 && f.pb && !v1_only && !no_split && f.sa == 0 && f.sb == 0 && f.P > 0 &&
+  if (f.dr && !(f.fnd > 0 && f.pb && f.sa == 0 && f.sb == 0 && f.P > 0 &&
                 (long long)f.nb * f.P == ntot && ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T))) {
     set_last_error("nft_hartley_fused: the direction carried by the prologue needs the folded batched prologue pass");
     return NFT_ERR_UNSUPPORTED;
   }
   // a single folded item (P = 0) takes the split path too, as a batch of one:
   // the in-pass prologue measured 116 us at 2048^2 against about 45 for the
-  // folded pass + the plain persistent R2C pass (NFT_PRO_SPLIT1=0: off)
-  static const bool split1 = !getenv("NFT_PRO_SPLIT1") || atoi(getenv("NFT_PRO_SPLIT1")) != 0;
-  // per-item A / xi0 in the folded prologue pass (NFT_PRO_FOLD_PI=0: the
-  // in-pass prologue of the R2C row pass)
-  static const bool pi_fold = !getenv("NFT_PRO_FOLD_PI") || atoi(getenv("NFT_PRO_FOLD_PI")) != 0;
-  if (split1 && !f.dr && f.P == 0 && f.fnd > 0 && f.pb && f.pro && !v1_only && !no_split &&
-      ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
+  // folded pass + the plain persistent R2C pass.  Per-item A / xi0 take the
+  // folded prologue pass as well (not the in-pass prologue of the R2C pass).
+  if (!f.dr && f.P == 0 && f.fnd > 0 && f.pb && f.pro && ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
     fast::FuseArgs f1 = f;
     f1.P = ntot;
     f1.nb = 1;
@@ -1019,14 +949,13 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
   }
   // per-item A / xi0 (f.sa, f.sb != 0) take the folded pass too (no carried direction)
   const bool shared_ab = f.sa == 0 && f.sb == 0;
-  if (!v1_only && !no_split && f.pro && (f.pa || f.pb) && (shared_ab || (pi_fold && f.fnd > 0 && f.pb && !f.dr)) &&
+  if (f.pro && (f.pa || f.pb) && (shared_ab || (f.fnd > 0 && f.pb && !f.dr)) &&
       f.P > 0 && (f.nb > 1 || f.dr || f.fnd > 0) &&
       (long long)f.nb * f.P == ntot &&
       ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T)) {
     T* u = (T*)((char*)ws + align256(hws));
     // one element per thread (no grid-stride chain of dependent gathers)
-    static const long long cap = getenv("NFT_PRO_NBLK") ? atoll(getenv("NFT_PRO_NBLK")) : (1LL << 30);
-    const unsigned nblk = (unsigned)std::min<long long>((f.P + 255) / 256, cap);
+    const unsigned nblk = (unsigned)((f.P + 255) / 256);
     if (f.fnd > 0 && f.pb) {
       long long ncell = 1;  // padded cell grid (pro_fold_kernel)
       for (int a = 0; a < f.fnd; ++a) ncell *= a == f.fnd - 1 ? ((f.fn[a] / 2 + 1 + 63) & ~63LL) : f.fn[a] / 2 + 1;
@@ -1050,7 +979,7 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     if (st != NFT_FALLBACK) return st;
     return hartley_fused_impl<T>(f2, u, out, g, ax, sigma, scale, ws, ws_bytes, hws, s);
   }
-  if (!v1_only) {
+  {
     int st = hartley_v2<T>(in, out, g, ax, sigma, scale, ws, ws_bytes, s, &f);
     if (st != NFT_FALLBACK) return st;
   }
@@ -1152,8 +1081,7 @@ int nft_hartley(const void* in, void* out, int ndim, const int64_t* shape, int n
   int st = parse_axes(ndim, shape, naxes, axes, g, ax);
   if (st != NFT_OK) return st;
   int sigma = convention == 0 ? 1 : -1;
-  static const bool v1_only = getenv("NFT_ENGINE_V1") != nullptr;
-  if (!v1_only && (dtype == 0 || dtype == 1)) {
+  if (dtype == 0 || dtype == 1) {
     if (dtype == 0) st = hartley_v2<double>(in, out, g, ax, sigma, scale, workspace, ws_bytes, stream);
     else if (dtype == 1) st = hartley_v2<float>(in, out, g, ax, sigma, scale, workspace, ws_bytes, stream);
     if (st != NFT_FALLBACK) return st;
@@ -1329,7 +1257,7 @@ int nft_hartley_cg_blocks(int ndim, const int64_t* shape, int naxes, const int* 
   const long long I = prod(cs, ax[0] + 1, g.nd);
   long long M = 1;
   int N = N0;
-  if (!(strided_supported(N0) || longcol_supported(N0))) {
+  if (!strided_supported(N0)) {
     if (!fourstep_supported(N0)) return 0;
     int N1, N2;
     fourstep_split(N0, N1, N2);

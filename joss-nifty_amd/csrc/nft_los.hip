@@ -34,20 +34,7 @@ constexpr int LOS_CAP_F = 2048;  // entries per forward work item (host-guarante
 constexpr int LOS_CH_A = 2048;   // adjoint: entries staged in LDS per chunk
 constexpr int LOS_YL = 2048;     // adjoint: LDS slots for the line values of a box (all batch vectors)
 constexpr int LOS_KMAX = 8;      // vectors per batched launch
-constexpr int LOS_SEG_ROUNDS = 4;
-#ifndef NFT_LOS_UT
-#define NFT_LOS_UT 0
-#endif
-#ifndef NFT_LOS_VLOAD
-#define NFT_LOS_VLOAD 1  // per-box forward: entries staged from aligned 16-entry chunks (uint4 + 4 float4 per thread; 123.5 -> 122.2 us)
-#endif
-#ifndef NFT_LOS_PAIR
-#define NFT_LOS_PAIR 0  // segment loop: entries k and k + 4 of a lane read together
-#endif
-#if NFT_LOS_PAIR && NFT_LOS_VLOAD
-#error "NFT_LOS_PAIR and NFT_LOS_VLOAD are exclusive"
-#endif  // forward: <= 256 segments per item = 4 rounds of 64 quads (host-guaranteed)
-
+constexpr int LOS_SEG_ROUNDS = 4;  // forward: <= 256 segments per item = 4 rounds of 64 quads (host-guaranteed)
 struct BoxGeom {
   long long H, W;
   int bh, bw, nby, nbx;
@@ -74,48 +61,23 @@ struct BoxGeom {
 // the reduce reads each line's slots contiguously.  The bounds and slots of
 // all of a thread's segments (LOS_SEG_ROUNDS rounds of 64) are loaded before
 // the barrier, off the critical path of the segment loop.
-// XCD-contiguous work order: workgroups are dealt to the 8 XCDs round-robin,
-// so workgroup w takes unit (w % 8) * ceil(n / 8) + w / 8 -- each XCD walks
-// one contiguous range of boxes, and neighbouring boxes (which share lines
-// of sight: adjacent partial slots forward, the same line values adjoint)
-// meet in that XCD's L2.  A bijection onto [0, n) for a grid of 8 ceil(n/8)
-// workgroups (the surplus ones return).
-__device__ __forceinline__ int xcd_unit(int w, int n) {
-  const int per = (n + 7) >> 3;
-  return (w & 7) * per + (w >> 3);
-}
 
 template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __restrict__ x,
                                                      const T* __restrict__ cs, double* __restrict__ part,
-                                                     long long xs, int pk, long long css, int dbg) {
+                                                     long long xs, int pk, long long css) {
   // every product is rounded before it is summed, in all K variants alike
   // (no FMA contraction): batched results are bitwise the K = 1 results
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CAP_F / 256;
   // pixel-major tile: the K values of one pixel are adjacent (one or two
   // 16-byte LDS reads per entry instead of K 8-byte ones)
-#if NFT_LOS_UT == 1
-  // vector-major tile: 8-byte reads of pixel l at bank 2 l mod 64 (the
-  // pixel-major 32-byte rows put every pixel on one of 8 bank groups)
-  __shared__ __align__(16) double ut[K][256];
-#define UAT(l, b) ut[b][l]
-#elif NFT_LOS_UT == 2
-  // pairs of vectors per 16-byte slot, one 256-slot array per pair: pixel l's
-  // slots start at bank quad l mod 16 in every array, so a 16-lane group of
-  // ds_read_b128 spreads over all 16 quads (the 32-byte pixel rows use 8)
-  constexpr int KP = K >= 2 ? K / 2 : 1;
-  __shared__ __align__(16) double ut[KP][256][K >= 2 ? 2 : 1];
-#define UAT(l, b) ut[(K >= 2 ? (b) >> 1 : 0)][l][K >= 2 ? ((b) & 1) : 0]
-#else
   __shared__ __align__(16) double u[256][K];
-#define UAT(l, b) u[l][b]
-#endif
   __shared__ float ew[K == 1 ? 1 : LOS_CAP_F];
   __shared__ unsigned char el[K == 1 ? 1 : LOS_CAP_F];
   __shared__ double prodbuf[K == 1 ? LOS_CAP_F : 1];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
-  const int it = (dbg & 16) ? xcd_unit(blockIdx.x, p.nitems) : (int)blockIdx.x, t = threadIdx.x;
+  const int it = (int)blockIdx.x, t = threadIdx.x;
   if (it >= p.nitems) return;
   const int box = p.item_box[it];
   bool ok;
@@ -124,28 +86,25 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
   const int e0 = p.item_ent[it], e1 = p.item_ent[it + 1];
   const int n = e1 - e0;
   const bool staged = n <= LOS_CAP_F;  // host plans always fit; others take the direct path
-  // segment-major partials (slot_seg given): segment s at index s, so the
-  // item's stores form one contiguous run
-  const bool segmaj = p.slot_seg != nullptr;
   float wv[PER];
   unsigned char lv[PER];
   if (staged) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int k = t + i * 256;
-      wv[i] = k < n ? ((dbg & 8) ? 1.f : p.ent_wf[e0 + k]) : 0.f;
-      lv[i] = k < n ? ((dbg & 8) ? (unsigned char)k : p.ent_loc[e0 + k]) : 0;
+      wv[i] = k < n ? p.ent_wf[e0 + k] : 0.f;
+      lv[i] = k < n ? p.ent_loc[e0 + k] : 0;
     }
   }
   // column (pixel-side) scale: shared by the vectors (css = 0) or one per vector
 #pragma unroll
   for (int b = 0; b < K; ++b) {
     double v = 0.0;
-    if (ok && !(dbg & 4)) {
+    if (ok) {
       v = (double)x[b * xs + px];
       if (cs) v *= (double)cs[b * css + px];
     }
-    UAT(t, b) = v;
+    u[t][b] = v;
   }
   // four lanes per segment: thread t serves segments sq + 64 r
   constexpr int RND = LOS_SEG_ROUNDS;
@@ -157,7 +116,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
     const int s = sq + 64 * r;
     sa[r] = s < s1 ? p.seg_ent[s] - e0 : 0;
     sb[r] = s < s1 ? p.seg_ent[s + 1] - e0 : 0;
-    so[r] = s < s1 ? (segmaj ? s : p.seg_slot[s]) : 0;
+    so[r] = s < s1 ? p.seg_slot[s] : 0;
   }
   if (K > 1 && staged) {
 #pragma unroll
@@ -177,7 +136,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int k = t + i * 256;
-        if (k < n) prod[k] = (double)wv[i] * UAT(lv[i], 0);
+        if (k < n) prod[k] = (double)wv[i] * u[lv[i]][0];
       }
     }
     __syncthreads();
@@ -186,8 +145,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       if (staged) {
         for (int k = a + sub; k < e; k += 4) a0 += prod[k];
       } else {
-        for (int k = a + sub; k < e; k += 4)
-          a0 = a0 + (double)p.ent_wf[e0 + k] * UAT(p.ent_loc[e0 + k], 0);
+        for (int k = a + sub; k < e; k += 4) a0 = a0 + (double)p.ent_wf[e0 + k] * u[p.ent_loc[e0 + k]][0];
       }
       a0 += __shfl_xor(a0, 1, 64);
       a0 += __shfl_xor(a0, 2, 64);
@@ -196,8 +154,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 #pragma unroll
     for (int r = 0; r < RND; ++r)
       if (sq + 64 * r < s1) seg1(so[r], sa[r], sb[r]);
-    for (int s = sq + 64 * RND; s < s1; s += 64)
-      seg1(segmaj ? s : p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
+    for (int s = sq + 64 * RND; s < s1; s += 64) seg1(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
     return;
   }
   auto segk = [&](int slot, int a, int e) {
@@ -208,7 +165,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       const double w = staged ? (double)ew[k] : (double)p.ent_wf[e0 + k];
       const int l = staged ? el[k] : p.ent_loc[e0 + k];
 #pragma unroll
-      for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * UAT(l, b);
+      for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
     }
 #pragma unroll
     for (int b = 0; b < K; ++b) {
@@ -216,53 +173,35 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       v += __shfl_xor(v, 1, 64);
       v += __shfl_xor(v, 2, 64);
       // every lane of the quad holds the sum: lane sub stores vectors sub, sub + 4
-      if ((b & 3) == sub && (!(dbg & 1) || v == 12345.678)) part[(long long)slot * pk + b] = v;
+      if ((b & 3) == sub) part[(long long)slot * pk + b] = v;
     }
   };
-  if (dbg & 2) return;
 #pragma unroll
   for (int r = 0; r < RND; ++r)
     if (sq + 64 * r < s1) segk(so[r], sa[r], sb[r]);
-  for (int s = sq + 64 * RND; s < s1; s += 64)
-    segk(segmaj ? s : p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
+  for (int s = sq + 64 * RND; s < s1; s += 64) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
 }
 
-// One workgroup per box (nft_los_plan.box_item given, K > 1): the pixel
-// tile's loads depend on the box index only, so they issue at once, beside
-// the box's segment / entry bounds (one workgroup per work item waits for
-// item_box first); a box of several work items (> LOS_CAP_F entries or > 256
-// segments) loops over them with the tile staged once (per item the items
-// kernel re-reads it: 20.5k items over 16.4k boxes at 2048^2 / 16384 lines).
-// Per segment and vector the products and their order are los_fwd_items'
-// (bitwise).  remap: XCD-contiguous box order.
+// One workgroup per box (nft_los_plan.box_item, K > 1): the pixel tile's
+// loads depend on the box index only, so they issue at once, beside the box's
+// segment / entry bounds; a box of several work items (> LOS_CAP_F entries
+// or > 256 segments) loops over them with the tile staged once.  The entries
+// of an item are staged from the aligned 16-entry chunks covering it (one
+// uint4 of pixel indices and four float4 of weights per thread; entry k of
+// the item at LDS slot (e0 & 15) + k).  Per segment and vector the products
+// and their order are los_fwd_items' (bitwise).
 template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __restrict__ x,
                                                      const T* __restrict__ cs, double* __restrict__ part,
-                                                     long long xs, int pk, long long css, int remap) {
+                                                     long long xs, int pk, long long css) {
 #pragma clang fp contract(off)
   static_assert(K > 1, "one vector takes los_fwd_items");
-  constexpr int PER = LOS_CAP_F / 256;
   constexpr int RND = LOS_SEG_ROUNDS;
-#if NFT_LOS_UT == 1
-  __shared__ __align__(16) double ut[K][256];
-#elif NFT_LOS_UT == 2
-  constexpr int KP = K / 2;
-  __shared__ __align__(16) double ut[KP][256][2];
-#else
   __shared__ __align__(16) double u[256][K];
-#endif
-#if NFT_LOS_VLOAD
-  // entries staged from the aligned 16-entry chunks covering the item (one
-  // uint4 of pixel indices and four float4 of weights per thread); entry k
-  // of the item at LDS slot (e0 & 15) + k
   __shared__ __align__(16) float ew[LOS_CAP_F + 16];
   __shared__ __align__(16) unsigned char el[LOS_CAP_F + 16];
-#else
-  __shared__ float ew[LOS_CAP_F];
-  __shared__ unsigned char el[LOS_CAP_F];
-#endif
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
-  const int box = remap ? xcd_unit(blockIdx.x, (int)p.nbox) : (int)blockIdx.x;
+  const int box = (int)blockIdx.x;
   if (box >= p.nbox) return;
   const int t = threadIdx.x;
   bool ok;
@@ -291,7 +230,6 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
   const int sub = t & 3;
   for (bool first = true;; first = false) {
     const int n = e1 - e0;
-#if NFT_LOS_VLOAD
     const int eo = e0 & 15;
     uint4 vl = make_uint4(0, 0, 0, 0);
     float4 vw[4];
@@ -303,17 +241,6 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
 #pragma unroll
       for (int j = 0; j < 4; ++j) vw[j] = *(const float4*)(p.ent_wf + c + 4 * j);
     }
-#else
-    constexpr int eo = 0;
-    float wv[PER];
-    unsigned char lv[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int k = t + i * 256;
-      wv[i] = k < n ? p.ent_wf[e0 + k] : 0.f;
-      lv[i] = k < n ? p.ent_loc[e0 + k] : 0;
-    }
-#endif
     const int sq = s0 + (t >> 2);
     int sa[RND], sb[RND], so[RND];
 #pragma unroll
@@ -324,35 +251,16 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
       so[r] = s < s1 ? p.seg_slot[s] : 0;
     }
     if (first) {
-#if NFT_LOS_UT == 1
-#pragma unroll
-      for (int b = 0; b < K; ++b) ut[b][t] = xv[b];
-#elif NFT_LOS_UT == 2
-#pragma unroll
-      for (int b = 0; b < K; ++b) ut[b >> 1][t][b & 1] = xv[b];
-#else
 #pragma unroll
       for (int b = 0; b < K; ++b) u[t][b] = xv[b];
-#endif
     } else {
       __syncthreads();  // the previous item's entries are read
     }
-#if NFT_LOS_VLOAD
     if (16 * t < eo + n) {
       *(uint4*)(el + 16 * t) = vl;
 #pragma unroll
       for (int j = 0; j < 4; ++j) *(float4*)(ew + 16 * t + 4 * j) = vw[j];
     }
-#else
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int k = t + i * 256;
-      if (k < n) {
-        ew[k] = wv[i];
-        el[k] = lv[i];
-      }
-    }
-#endif
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RND; ++r) {
@@ -360,42 +268,12 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
         double acc[K];
 #pragma unroll
         for (int b = 0; b < K; ++b) acc[b] = 0.0;
-#if NFT_LOS_PAIR && NFT_LOS_UT == 0
-        // entries k and k + 4 of the lane read together (two LDS chains in
-        // flight), summed in the same order
-        for (int k = sa[r] + sub; k < sb[r]; k += 8) {
-          const bool h = k + 4 < sb[r];
-          const double w0 = (double)ew[k], w1 = h ? (double)ew[k + 4] : 0.0;
-          const int l0 = el[k], l1 = h ? el[k + 4] : 0;
-          double v0[K], v1[K];
-#pragma unroll
-          for (int b = 0; b < K; ++b) {
-            v0[b] = u[l0][b];
-            v1[b] = u[l1][b];
-          }
-#pragma unroll
-          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w0 * v0[b];
-          if (h) {
-#pragma unroll
-            for (int b = 0; b < K; ++b) acc[b] = acc[b] + w1 * v1[b];
-          }
-        }
-#else
         for (int k = sa[r] + eo + sub; k < sb[r] + eo; k += 4) {
           const double w = (double)ew[k];
           const int l = el[k];
-#if NFT_LOS_UT == 1
-#pragma unroll
-          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * ut[b][l];
-#elif NFT_LOS_UT == 2
-#pragma unroll
-          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * ut[b >> 1][l][b & 1];
-#else
 #pragma unroll
           for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
-#endif
         }
-#endif
 #pragma unroll
         for (int b = 0; b < K; ++b) {
           double v = acc[b];
@@ -410,132 +288,6 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
     e0 = e1;
     s1 = p.item_seg[ci + 1];
     e1 = p.item_ent[ci + 1];
-  }
-}
-#undef UAT
-
-// One workgroup per tile of tile_S x tile_S boxes (nft_los_plan.ntile > 0):
-// the tile's work items in order (boxes in raster order), each staged and
-// summed per segment as in los_fwd_items, the segment sums added to the
-// line's LDS accumulator (a line has one segment per box, so one add per
-// line and box, boxes in order: a fixed order); one partial per (line, tile)
-// leaves the workgroup at the end.  The next item's entries, segment bounds
-// and (on a new box) pixel values are loaded into registers while the
-// current one is summed.  Every K (1 included) takes this kernel when the
-// plan has tiles: per vector the arithmetic does not depend on K (bitwise).
-template <typename T, int K>
-__global__ __launch_bounds__(256) void los_fwd_tiles(nft_los_plan p, const T* __restrict__ x,
-                                                     const T* __restrict__ cs, double* __restrict__ part,
-                                                     long long xs, int pk, long long css) {
-#pragma clang fp contract(off)
-  constexpr int PER = LOS_CAP_F / 256;
-  constexpr int RND = LOS_SEG_ROUNDS;
-  __shared__ __align__(16) double u[256][K];
-  __shared__ float ew[LOS_CAP_F];
-  __shared__ unsigned char el[LOS_CAP_F];
-  extern __shared__ __align__(16) double tacc[];  // [lines of the tile][K]
-  const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
-  const int tile = blockIdx.x, t = threadIdx.x, sub = t & 3;
-  const int i0 = p.tile_iptr[tile], i1 = p.tile_iptr[tile + 1];
-  const int l0 = p.tile_lptr[tile], ntl = p.tile_lptr[tile + 1] - l0;
-  for (int j = t; j < ntl * K; j += 256) tacc[j] = 0.0;
-  // the item in flight (registers)
-  int nbox = -1, ns0 = 0, ns1 = 0, ne0 = 0, nn = 0;
-  float wv[PER];
-  unsigned char lv[PER];
-  double xv[K];
-  int san[RND], sbn[RND], stn[RND];
-  auto load = [&](int ii, int prev) {
-    const int it = p.tile_items[ii];
-    nbox = p.item_box[it];
-    ns0 = p.item_seg[it];
-    ns1 = p.item_seg[it + 1];
-    ne0 = p.item_ent[it];
-    nn = p.item_ent[it + 1] - ne0;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int k = t + i * 256;
-      wv[i] = k < nn ? p.ent_wf[ne0 + k] : 0.f;
-      lv[i] = k < nn ? p.ent_loc[ne0 + k] : 0;
-    }
-    if (nbox != prev) {
-      bool ok;
-      const long long px = g.pixel(nbox, t, ok);
-#pragma unroll
-      for (int b = 0; b < K; ++b) {
-        double v = 0.0;
-        if (ok) {
-          v = (double)x[b * xs + px];
-          if (cs) v *= (double)cs[b * css + px];
-        }
-        xv[b] = v;
-      }
-    }
-    const int sq = ns0 + (t >> 2);
-#pragma unroll
-    for (int r = 0; r < RND; ++r) {
-      const int s = sq + 64 * r;
-      san[r] = s < ns1 ? p.seg_ent[s] - ne0 : 0;
-      sbn[r] = s < ns1 ? p.seg_ent[s + 1] - ne0 : 0;
-      stn[r] = s < ns1 ? (int)p.seg_tl[s] : 0;
-    }
-  };
-  int cbox = -1;
-  if (i0 < i1) load(i0, -1);
-  for (int ii = i0; ii < i1; ++ii) {
-    const int s0 = ns0, s1 = ns1, n = nn;
-    const bool newbox = nbox != cbox;
-    cbox = nbox;
-    int sa[RND], sb[RND], st[RND];
-#pragma unroll
-    for (int r = 0; r < RND; ++r) {
-      sa[r] = san[r];
-      sb[r] = sbn[r];
-      st[r] = stn[r];
-    }
-    __syncthreads();  // the previous item's LDS reads (and the accumulator zeroing) are done
-    if (newbox) {
-#pragma unroll
-      for (int b = 0; b < K; ++b) u[t][b] = xv[b];
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int k = t + i * 256;
-      if (k < n) {
-        ew[k] = wv[i];
-        el[k] = lv[i];
-      }
-    }
-    __syncthreads();
-    if (ii + 1 < i1) load(ii + 1, cbox);  // in flight while this item is summed
-    const int sq = s0 + (t >> 2);
-#pragma unroll
-    for (int r = 0; r < RND; ++r) {
-      if (sq + 64 * r < s1) {
-        double acc[K];
-#pragma unroll
-        for (int b = 0; b < K; ++b) acc[b] = 0.0;
-        for (int k = sa[r] + sub; k < sb[r]; k += 4) {
-          const double w = (double)ew[k];
-          const int l = el[k];
-#pragma unroll
-          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
-        }
-#pragma unroll
-        for (int b = 0; b < K; ++b) {
-          double v = acc[b];
-          v += __shfl_xor(v, 1, 64);
-          v += __shfl_xor(v, 2, 64);
-          if ((b & 3) == sub) tacc[st[r] * K + b] += v;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int j = t; j < ntl; j += 256) {
-    double* dst = part + (long long)p.tl_slot[l0 + j] * pk;
-#pragma unroll
-    for (int b = 0; b < K; ++b) dst[b] = tacc[j * K + b];
   }
 }
 
@@ -559,43 +311,11 @@ __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const doub
   for (int v = 0; v < LOS_KMAX; ++v) acc[v] = 0.0;
   if (valid) {
     const int a = p.los_ptr[l], b = p.los_ptr[l + 1];
-    if (p.slot_seg) {
-      // segment-major partials: the lane's first RR slots' segment indices,
-      // then all their partials, in flight together; summed in slot order
-      // (bitwise the line-major layout)
-      constexpr int RR = 4;
-      int sg[RR];
+    for (int k = a + lane; k < b; k += 64) {
+      const double* q = part + (long long)k * K;
 #pragma unroll
-      for (int j = 0; j < RR; ++j) {
-        const int k = a + lane + 64 * j;
-        sg[j] = k < b ? p.slot_seg[k] : -1;
-      }
-      double qv[RR][K];
-#pragma unroll
-      for (int j = 0; j < RR; ++j) {
-        const double* q = part + (long long)(sg[j] < 0 ? 0 : sg[j]) * K;
-#pragma unroll
-        for (int v = 0; v < K; ++v) qv[j][v] = sg[j] >= 0 ? q[v] : 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < RR; ++j)
-        if (sg[j] >= 0) {
-#pragma unroll
-          for (int v = 0; v < K; ++v) acc[v] += qv[j][v];
-        }
-      for (int k = a + lane + 64 * RR; k < b; k += 64) {
-        const double* q = part + (long long)p.slot_seg[k] * K;
-#pragma unroll
-        for (int v = 0; v < LOS_KMAX; ++v)
-          if (v < K) acc[v] += q[v];
-      }
-    } else {
-      for (int k = a + lane; k < b; k += 64) {
-        const double* q = part + (long long)k * K;
-#pragma unroll
-        for (int v = 0; v < LOS_KMAX; ++v)
-          if (v < K) acc[v] += q[v];
-      }
+      for (int v = 0; v < LOS_KMAX; ++v)
+        if (v < K) acc[v] += q[v];
     }
   }
 #pragma unroll
@@ -632,7 +352,7 @@ template <typename T, typename IDX, int K, bool VEC = false>
 __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* __restrict__ lidx,
                                                      const T* __restrict__ yv, const T* __restrict__ cs,
                                                      const T* __restrict__ rs, T* __restrict__ out, double scale,
-                                                     long long ys, long long os, long long rss, int remap) {
+                                                     long long ys, long long os, long long rss) {
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CH_A / 256;
   // line table: 256 lines per vector cover every box of an 8-bit-index plan
@@ -644,23 +364,8 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   __shared__ __align__(16) float ew[K == 1 ? 2 * LOS_CH_A : LOS_CH_A];
   __shared__ __align__(16) IDX el[K == 1 ? 1 : LOS_CH_A];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
-  const int box = remap ? xcd_unit(blockIdx.x, p.nbox) : (int)blockIdx.x, t = threadIdx.x;
+  const int box = (int)blockIdx.x, t = threadIdx.x;
   if (box >= p.nbox) return;
-  // padded line table (K > 1, lpad <= 256 lines): staged from the box index
-  // alone, before the box bounds arrive; slot i of vector v at yl[v lpad + i]
-  const int lp = (K > 1 && p.lpad > 0 && p.lpad * K <= YL) ? p.lpad : 0;
-  if (lp) {
-    const int li = t < lp ? p.box_lines_pad[(long long)box * lp + t] : -1;
-    if (li >= 0) {
-      const double c = cs ? (double)cs[li] : 1.0;
-#pragma unroll
-      for (int v = 0; v < K; ++v) {
-        double yy = (double)yv[v * ys + li];
-        if (cs) yy *= c;
-        yl[v * lp + t] = yy;
-      }
-    }
-  }
   const int l0 = p.box_lptr[box], nl = p.box_lptr[box + 1] - l0;
   // 16-entry chunks with 16-byte loads (box runs padded, box_ent_adj)
   constexpr bool vec = VEC && sizeof(IDX) == 1 && K > 1;
@@ -674,7 +379,7 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   double rsv[K];
 #pragma unroll
   for (int v = 0; v < K; ++v) rsv[v] = (rs && ok) ? (double)rs[v * rss + px] : 1.0;
-  const int ystr = lp ? lp : nl;  // line-table stride per vector
+  const int ystr = nl;  // line-table stride per vector
   // the first chunk's entry loads go out before the line-table staging so the
   // two dependent load chains overlap
   int lv[PER];
@@ -702,8 +407,8 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
       wv[i] = k < n ? p.ent_wa[e0 + k] : 0.f;
     }
   }
-  const bool tab = lp || nl * K <= YL;  // line values of this box (all vectors) cached in LDS
-  if (tab && !lp) {
+  const bool tab = nl * K <= YL;  // line values of this box (all vectors) cached in LDS
+  if (tab) {
     for (int i = t; i < nl; i += 256) {
       const int li = p.box_lines[l0 + i];
       const double c = cs ? (double)cs[li] : 1.0;
@@ -802,178 +507,31 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   }
 }
 
-// Persistent, prefetching variant for K > 1: workgroup w processes items
-// w, w + G, w + 2G, ... and loads the next item's entries, pixel values and
-// segment bounds into registers while the current one is summed from LDS
-// (one item per workgroup leaves each workgroup a load -> barrier -> sum ->
-// store chain with nothing to overlap).  Same products and summation order
-// per segment and vector as los_fwd_items (bitwise).
-template <typename T, int K>
-__global__ __launch_bounds__(256) void los_fwd_items_pf(nft_los_plan p, const T* __restrict__ x,
-                                                        const T* __restrict__ cs, double* __restrict__ part,
-                                                        long long xs, int pk, long long css) {
-#pragma clang fp contract(off)
-  static_assert(K > 1, "the persistent variant serves batched launches");
-  constexpr int PER = LOS_CAP_F / 256;
-  constexpr int RND = LOS_SEG_ROUNDS;
-  __shared__ double u[K][256];
-  __shared__ float ew[LOS_CAP_F];
-  __shared__ unsigned char el[LOS_CAP_F];
-  const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
-  const int t = threadIdx.x;
-  const int sub = t & 3;
-  // the item in flight (registers)
-  int e0n, nn, s0n, s1n;
-  float wv[PER];
-  unsigned char lv[PER];
-  double xv[K];
-  int san[RND], sbn[RND], son[RND];
-  auto load = [&](int it) {
-    const int box = p.item_box[it];
-    bool ok;
-    const long long px = g.pixel(box, t, ok);
-    s0n = p.item_seg[it];
-    s1n = p.item_seg[it + 1];
-    e0n = p.item_ent[it];
-    nn = p.item_ent[it + 1] - e0n;
-    const bool st = nn <= LOS_CAP_F;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int k = t + i * 256;
-      wv[i] = (st && k < nn) ? p.ent_wf[e0n + k] : 0.f;
-      lv[i] = (st && k < nn) ? p.ent_loc[e0n + k] : 0;
-    }
-#pragma unroll
-    for (int b = 0; b < K; ++b) {
-      double v = 0.0;
-      if (ok) {
-        v = (double)x[b * xs + px];
-        if (cs) v *= (double)cs[b * css + px];
-      }
-      xv[b] = v;
-    }
-    const int sq = s0n + (t >> 2);
-#pragma unroll
-    for (int r = 0; r < RND; ++r) {
-      const int s = sq + 64 * r;
-      san[r] = s < s1n ? p.seg_ent[s] - e0n : 0;
-      sbn[r] = s < s1n ? p.seg_ent[s + 1] - e0n : 0;
-      son[r] = s < s1n ? (p.slot_seg ? s : p.seg_slot[s]) : 0;
-    }
-  };
-  int it = blockIdx.x;
-  if (it < p.nitems) load(it);
-  while (it < p.nitems) {
-    // stage the current item, keep its segment bounds
-    const int e0 = e0n, n = nn, s0 = s0n, s1 = s1n;
-    const bool staged = n <= LOS_CAP_F;
-    int sa[RND], sb[RND], so[RND];
-#pragma unroll
-    for (int r = 0; r < RND; ++r) {
-      sa[r] = san[r];
-      sb[r] = sbn[r];
-      so[r] = son[r];
-    }
-#pragma unroll
-    for (int b = 0; b < K; ++b) u[b][t] = xv[b];
-    if (staged) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const int k = t + i * 256;
-        if (k < n) {
-          ew[k] = wv[i];
-          el[k] = lv[i];
-        }
-      }
-    }
-    __syncthreads();
-    const int nx = it + (int)gridDim.x;
-    if (nx < p.nitems) load(nx);  // in flight while this item is summed
-    auto segk = [&](int slot, int a, int e) {
-      double acc[K];
-#pragma unroll
-      for (int b = 0; b < K; ++b) acc[b] = 0.0;
-      for (int k = a + sub; k < e; k += 4) {
-        const double w = staged ? (double)ew[k] : (double)p.ent_wf[e0 + k];
-        const int l = staged ? el[k] : p.ent_loc[e0 + k];
-#pragma unroll
-        for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[b][l];
-      }
-#pragma unroll
-      for (int b = 0; b < K; ++b) {
-        double v = acc[b];
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        if ((b & 3) == sub) part[(long long)slot * pk + b] = v;
-      }
-    };
-    const int sq = s0 + (t >> 2);
-#pragma unroll
-    for (int r = 0; r < RND; ++r)
-      if (sq + 64 * r < s1) segk(so[r], sa[r], sb[r]);
-    for (int s = sq + 64 * RND; s < s1; s += 64)
-      segk(p.slot_seg ? s : p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
-    __syncthreads();  // LDS free for the next item
-    it = nx;
-  }
-}
-
 template <typename T, int K>
 static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* part, long long xs, int pk,
                         long long css, hipStream_t s) {
   if constexpr (K > 1) {
-    if (p->box_item && !p->slot_seg) {
-      // NFT_LOS_BOX_REMAP (tuning probe, read per launch): XCD-contiguous box order
-      const char* rm = getenv("NFT_LOS_BOX_REMAP");
-      const int remap = rm ? atoi(rm) : 0;
-      const unsigned grid = remap ? (unsigned)(8 * ((p->nbox + 7) / 8)) : (unsigned)p->nbox;
-      hipLaunchKernelGGL((los_fwd_boxes<T, K>), dim3(grid), dim3(256), 0, s, *p, x, cs, part, xs, pk, css, remap);
-      return;
-    }
-    // opt-in (NFT_LOS_PF=1, NFT_LOS_PF_WG workgroups per CU, default 8):
-    // measured slower at 4 x 2048^2 / 16384 lines (CG iteration 1257 ->
-    // 1310 / 1306 / 1291 us at 8 / 4 / 16 workgroups per CU) -- one item per
-    // workgroup, dispatched by the hardware, keeps more loads in flight
-    static const int pf = getenv("NFT_LOS_PF") ? atoi(getenv("NFT_LOS_PF")) : 0;
-    if (pf > 0) {
-      static int grid = 0;
-      if (grid == 0) {
-        int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-          ncu = 256;
-        const int per = getenv("NFT_LOS_PF_WG") ? atoi(getenv("NFT_LOS_PF_WG")) : 8;
-        grid = ncu * (per > 0 ? per : 8);
-      }
-      const unsigned gsz = (unsigned)std::min<long long>(p->nitems, grid);
-      hipLaunchKernelGGL((los_fwd_items_pf<T, K>), dim3(gsz), dim3(256), 0, s, *p, x, cs, part, xs, pk, css);
+    if (p->box_item) {
+      hipLaunchKernelGGL((los_fwd_boxes<T, K>), dim3((unsigned)p->nbox), dim3(256), 0, s, *p, x, cs, part, xs, pk,
+                         css);
       return;
     }
   }
-  // NFT_LOS_DBG (read per launch; tuning probe only): ablation bits of the
-  // items kernel -- 1 no partial stores, 2 no segment sums, 4 no pixel loads,
-  // 8 no entry loads
-  const char* dbs = getenv("NFT_LOS_DBG");
-  const int dbg = dbs ? atoi(dbs) : 0;
-  const unsigned grid = (dbg & 16) ? (unsigned)(8 * ((p->nitems + 7) / 8)) : (unsigned)p->nitems;
-  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3(grid), dim3(256), 0, s, *p, x, cs, part, xs, pk, css, dbg);
+  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, pk, css);
 }
 
 template <typename T, typename IDX, int K>
 static void adj_boxes_k(const nft_los_plan* p, const IDX* li, const T* y, const T* cs, const T* rs, T* out,
                         double scale, long long ys, long long os, long long rss, hipStream_t s) {
-  const char* ab = getenv("NFT_LOS_ADJ_XCD");   // tuning probe (read per launch)
-  const int remap = ab ? atoi(ab) : 0;
-  const unsigned grid = remap ? (unsigned)(8 * ((p->nbox + 7) / 8)) : (unsigned)p->nbox;
+  const dim3 grid((unsigned)p->nbox);
   if constexpr (K > 1 && sizeof(IDX) == 1) {
     if (p->box_ent_adj) {
-      hipLaunchKernelGGL((los_adj_boxes<T, IDX, K, true>), dim3(grid), dim3(256), 0, s, *p, li, y, cs, rs, out, scale,
-                         ys, os, rss, remap);
+      hipLaunchKernelGGL((los_adj_boxes<T, IDX, K, true>), grid, dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys, os,
+                         rss);
       return;
     }
   }
-  hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), dim3(grid), dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys,
-                     os, rss, remap);
+  hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), grid, dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys, os, rss);
 }
 
 // vectors are processed in groups of 8 / 4 / 2 / 1 (template sizes)
@@ -984,26 +542,7 @@ static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, c
                          double scale, int K, long long xs, long long ys, hipStream_t s, double* qpart = nullptr,
                          long long qstride = 0, long long css = 0) {
   prof_mark(s, "los_fwd_items");
-  if (p->ntile > 0 && p->nitems > 0) {
-    for (int v = 0; v < K;) {
-      const int g = kgroup(K - v);
-      const T* xv = (const T*)x + v * xs;
-      const T* cv = cs ? (const T*)cs + v * css : nullptr;
-      double* pv = part + v;
-      const size_t lds = (size_t)p->tl_max * g * sizeof(double);
-      const dim3 grid((unsigned)p->ntile);
-#define NFT_TILES(KK)                                                                                  \
-  case KK:                                                                                             \
-    hipLaunchKernelGGL((los_fwd_tiles<T, KK>), grid, dim3(256), lds, s, *p, xv, cv, pv, xs, K, css); \
-    break;
-      switch (g) {
-        NFT_TILES(8) NFT_TILES(4) NFT_TILES(2) NFT_TILES(1)
-        default: break;
-      }
-#undef NFT_TILES
-      v += g;
-    }
-  } else if (p->nitems > 0) {
+  if (p->nitems > 0) {
     for (int v = 0; v < K;) {
       const int g = kgroup(K - v);
       const T* xv = (const T*)x + v * xs;

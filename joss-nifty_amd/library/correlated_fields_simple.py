@@ -80,17 +80,33 @@ class AmpLin:
         h.has_flex, h.has_asp, h.has_zm = int(amp.has_flex), int(amp.has_asp), int(amp.has_zm)
         self.host = h
         self._rep = {}
+        self.tab = None
 
     @property
     def B(self):
         return self.host.B
 
+    def prepare(self):
+        """the two-phase kernels' tables of every row (nft_amp2_prepare: once
+        per linearisation point, on first use; sets the device structs' tab)"""
+        if self.tab is None and self.B >= 3:
+            import ctypes
+            lib = _native.load()
+            n = int(lib.nft_amp2_tab_len(self.B))
+            self.tab = torch.empty((self.k, n), dtype=torch.float64, device=self.dconst.device)
+            _native._check(lib.nft_amp2_prepare(ctypes.byref(self.host), ctypes.c_void_p(self.dconst.data_ptr()),
+                                                 self.k, ctypes.c_void_p(self.tab.data_ptr()), n,
+                                                 _native.stream_ptr()))
+        return self
+
     def row_bytes(self, r):
+        self.prepare()
         return self.dconst[r * self.size:(r + 1) * self.size]
 
     def items(self, k, row=0):
         """device pointer of k consecutive structs: row `row` shared by k
         right-hand sides"""
+        self.prepare()
         if self.k == 1 and k == 1:
             return self.dconst.data_ptr()
         key = (k, row)
@@ -256,6 +272,15 @@ class _AmplitudeModel:
         k.total_volume = self.total_vol
         k.B = self.B
         k.has_flex, k.has_asp, k.has_zm = int(self.has_flex), int(self.has_asp), int(self.has_zm)
+        if self.B >= 3:
+            # the two-phase kernels' tables of this linearisation point
+            import ctypes
+            lib = _native.load()
+            n = int(lib.nft_amp2_tab_len(self.B))
+            keep["tab"] = torch.empty(n, dtype=torch.float64, device=keep["An"].device)
+            k.tab = keep["tab"].data_ptr()
+            _native._check(lib.nft_amp2_prepare(ctypes.byref(k), None, 1, ctypes.c_void_p(k.tab), n,
+                                                 _native.stream_ptr()))
         return k, keep
 
     # ------------------------------------------------- native forward
@@ -337,6 +362,7 @@ class _AmplitudeModel:
         without per-item constants is ONE device constant set shared by every
         right-hand side (mode 2)"""
         if isinstance(const, AmpLin):
+            const.prepare()
             if item_consts is None:
                 return const.host, const.items(1), 2
             return const.host, item_consts, 1

@@ -136,37 +136,6 @@ def los_coo(shape, distances, starts, ends, sigmas=None, truncation=3.):
 
 
 LOS_CAP_F = 2048   # entries per forward work item (csrc/nft_los.hip)
-# forward partials stored segment-major and gathered by the line reduce
-# (nft_los_plan.slot_seg, NFT_LOS_SEG_MAJOR=1).  Measured at 4 x 2048^2 /
-# 16384 lines: items 131 -> 111 us, reduce 14 -> 45 us (random 32-byte
-# gathers): off by default, line-major slots
-SEG_MAJOR = os.environ.get("NFT_LOS_SEG_MAJOR", "0") == "1"
-# batched forward with one workgroup per box (nft_los_plan.box_item): the
-# pixel tile's loads issue beside the box metadata and a box of several work
-# items stages it once (NFT_LOS_BOX_WG=0: one workgroup per work item)
-BOX_WG = os.environ.get("NFT_LOS_BOX_WG", "1") != "0"
-# forward partials per (line, tile of TILE x TILE boxes) instead of per
-# (line, box), NFT_LOS_TILE=2 / 4: the tile's workgroup sums each line's box
-# segments in LDS (boxes in raster order within the tile) and stores one
-# partial per line crossing the tile.  Measured at 4 x 2048^2 / 16384 lines:
-# half / a quarter of the partials, but items 117 (one workgroup per box) ->
-# 155 / 235 us (a quarter of the workgroups, lower occupancy, one item after
-# the other per workgroup): off
-TILE = int(os.environ.get("NFT_LOS_TILE", "1"))
-TILE_LINES_MAX = 1024   # lines crossing one tile (LDS accumulators: lines x vectors x 8 B)
-# the lines crossing every box at a fixed stride (nft_los_plan.box_lines_pad,
-# NFT_LOS_ADJ_PAD=1): the batched adjoint stages its line table without
-# waiting for the box bounds (bitwise).  Measured at 4 x 2048^2: 98 -> 103 us
-# (a whole 1 KB row per box read): off
-ADJ_PAD = os.environ.get("NFT_LOS_ADJ_PAD", "0") == "1"
-# the adjoint's entries padded per box to 16-entry chunks (box_ent_adj) and
-# staged with 16-byte loads (bitwise the per-entry loads; 4 x 2048^2: 96.4 ->
-# 92.9 us, iteration -7 us; NFT_LOS_ADJ_VEC=0: per-entry loads)
-ADJ_VEC = os.environ.get("NFT_LOS_ADJ_VEC", "1") != "0"
-# forward segments of a work item longest first (_longest_first,
-# NFT_LOS_SORT_SEG=1; bitwise).  Measured at 4 x 2048^2 / 16384 lines: one
-# workgroup per box 116 us either way (items 130 -> 128 us): off
-SORT_SEGMENTS = os.environ.get("NFT_LOS_SORT_SEG", "0") == "1"
 LOS_KMAX = 8       # vectors per batched LOS launch (csrc/nft_los.hip)
 BOX = 256
 
@@ -235,9 +204,6 @@ def box_plan(rows, cols, w, shape, nlos):
     olm = np.lexsort((seg_box, seg_los))
     seg_slot = np.empty(nseg, dtype=np.int32)
     seg_slot[olm] = np.arange(nseg, dtype=np.int32)
-    # the segment of every slot: the forward stores partials segment-major
-    # (coalesced per item) and the reduce gathers them (nft_los_plan.slot_seg)
-    slot_seg = olm.astype(np.int32)
     los_ptr = np.r_[0, np.cumsum(np.bincount(seg_los, minlength=nlos))].astype(np.int32)
     # ---- adjoint: entries sorted by (box, local pixel)
     key2 = box * BOX + loc
@@ -256,25 +222,13 @@ def box_plan(rows, cols, w, shape, nlos):
         raise ValueError("more than 65535 lines of sight cross one 256-pixel box")
     lidx8 = segcnt.max(initial=0) <= 256
     wf = np.asarray(w, dtype=np.float32)
-    pad = {}
-    if ADJ_PAD and lidx8 and nseg:
-        lpad = int(-(-segcnt.max() // 64) * 64)
-        blp = np.full((nbox, lpad), -1, dtype=np.int32)
-        sb = np.repeat(np.arange(nbox), segcnt)
-        blp[sb, np.arange(nseg) - box_lptr[sb]] = seg_los
-        pad = dict(lpad=lpad, box_lines_pad=blp.reshape(-1))
-    tiles = _tile_plan(seg_box, seg_los, np.asarray(item_box, dtype=np.int64), L, nby, nbx, int(nlos), TILE)
     item_seg = np.asarray(item_seg, dtype=np.int64)
-    fwd = dict(seg_ent=seg_ent, seg_slot=seg_slot, slot_seg=slot_seg, ent_loc=loc[of].astype(np.uint8), ent_wf=wf[of])
-    if "seg_tl" in tiles:
-        fwd["seg_tl"] = tiles.pop("seg_tl")
-    if SORT_SEGMENTS and nseg:
-        fwd = _longest_first(fwd, item_seg)
+    fwd = dict(seg_ent=seg_ent, seg_slot=seg_slot, ent_loc=loc[of].astype(np.uint8), ent_wf=wf[of])
     # 16 entries of padding: the per-box forward stages aligned 16-entry
     # chunks, the last one may reach past an item's (and the array's) end
     fwd["ent_loc"] = np.r_[fwd["ent_loc"], np.zeros(16, np.uint8)]
     fwd["ent_wf"] = np.r_[fwd["ent_wf"], np.zeros(16, np.float32)]
-    return dict(tiles, **pad, H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
+    return dict(H=H, W=W, bh=bh, bw=bw, nby=nby, nbx=nbx, nbox=nbox, nlos=int(nlos),
                 nitems=len(item_box), nseg=nseg, L=L,
                 item_box=np.asarray(item_box, dtype=np.int32), item_seg=item_seg.astype(np.int32),
                 item_ent=seg_ent[item_seg].astype(np.int32), **fwd,
@@ -284,12 +238,12 @@ def box_plan(rows, cols, w, shape, nlos):
 
 
 def _adj_entries(lidx, wa, entcnt, lidx8):
-    """The adjoint's entry arrays; with ADJ_VEC and 8-bit line indices every
-    box's run padded to a multiple of 16 entries (index 0, weight 0: never
-    summed, the pixel runs end before them) and its start in box_ent_adj, so
-    the adjoint stages them with 16-byte loads."""
+    """The adjoint's entry arrays; with 8-bit line indices every box's run
+    padded to a multiple of 16 entries (index 0, weight 0: never summed, the
+    pixel runs end before them) and its start in box_ent_adj, so the batched
+    adjoint stages them with 16-byte loads (4 x 2048^2: 96.4 -> 92.9 us)."""
     out = dict(ent_lidx=lidx, lidx8=int(lidx8), ent_wa=wa)
-    if not (ADJ_VEC and lidx8) or len(entcnt) == 0:
+    if not lidx8 or len(entcnt) == 0:
         return out
     padded = -(-entcnt // 16) * 16
     start = np.r_[0, np.cumsum(padded)]
@@ -302,68 +256,6 @@ def _adj_entries(lidx, wa, entcnt, lidx8):
     w[pos] = wa
     out.update(ent_lidx=li, ent_wa=w, box_ent_adj=start.astype(np.int32))
     return out
-
-
-def _longest_first(fwd, item_seg):
-    """The forward arrays with every work item's segments reordered longest
-    first (stable).  The forward kernels give segments to 4-lane groups in
-    order, 16 per wave: a wave runs as long as its longest segment, so
-    segments of similar length in one wave idle fewer lanes.  Entries keep
-    their order within a segment (each segment's sum is unchanged, bitwise);
-    item, box and line ranges are unchanged (segments move within their work
-    item only); the adjoint's arrays do not depend on this order."""
-    seg_ent = fwd["seg_ent"].astype(np.int64)
-    ln = np.diff(seg_ent)
-    nseg = len(ln)
-    item_of = np.repeat(np.arange(len(item_seg) - 1), np.diff(item_seg))
-    perm = np.lexsort((np.arange(nseg), -ln, item_of))
-    nl = ln[perm]
-    new_ent = np.r_[0, np.cumsum(nl)]
-    # entry index of every new position: the old run of its segment
-    idx = np.repeat(seg_ent[perm] - new_ent[:-1], nl) + np.arange(new_ent[-1])
-    out = dict(fwd, seg_ent=new_ent.astype(np.int32), seg_slot=fwd["seg_slot"][perm],
-               ent_loc=fwd["ent_loc"][idx], ent_wf=fwd["ent_wf"][idx])
-    inv = np.empty(nseg, dtype=np.int64)
-    inv[perm] = np.arange(nseg)
-    out["slot_seg"] = inv[fwd["slot_seg"]].astype(np.int32)
-    if "seg_tl" in fwd:
-        out["seg_tl"] = fwd["seg_tl"][perm]
-    return out
-
-
-def _tile_plan(seg_box, seg_los, item_box, L, nby, nbx, nlos, S):
-    """Tiles of S x S boxes for the forward (nft_los_plan.tile_*): the work
-    items of every tile in processing order (boxes in raster order within the
-    tile), the lines crossing it (ascending), every segment's index into its
-    tile's line list, and the partial slot of every (tile, line) pair in
-    line-major order (tiles ascending within a line) with its line CSR."""
-    if S <= 1:
-        return dict(tile_S=1, ntile=0)
-    nty, ntx = -(-nby // S), -(-nbx // S)
-    ntile = L * nty * ntx
-    bl, br = np.divmod(np.arange(L * nby * nbx, dtype=np.int64), nby * nbx)
-    by, bx = np.divmod(br, nbx)
-    tile_of_box = (bl * nty + by // S) * ntx + bx // S
-    seg_tile = tile_of_box[seg_box]
-    key = seg_tile * nlos + seg_los
-    uk, inv = np.unique(key, return_inverse=True)
-    tl_tile, tl_line = uk // nlos, uk % nlos
-    tile_lptr = np.r_[0, np.cumsum(np.bincount(tl_tile, minlength=ntile))].astype(np.int64)
-    seg_tl = inv.reshape(-1) - tile_lptr[seg_tile]
-    olm = np.lexsort((tl_tile, tl_line))
-    tl_slot = np.empty(len(uk), dtype=np.int64)
-    tl_slot[olm] = np.arange(len(uk))
-    los_ptr_t = np.r_[0, np.cumsum(np.bincount(tl_line, minlength=nlos))]
-    item_tile = tile_of_box[item_box]
-    order = np.argsort(item_tile, kind="stable")
-    tile_iptr = np.r_[0, np.cumsum(np.bincount(item_tile, minlength=ntile))]
-    tl_max = int(np.diff(tile_lptr).max(initial=0))
-    if tl_max > TILE_LINES_MAX or len(uk) >= 2 ** 31 - 1:
-        return dict(tile_S=1, ntile=0)
-    return dict(tile_S=int(S), ntile=int(ntile), tl_max=tl_max,
-                tile_iptr=tile_iptr.astype(np.int32), tile_items=order.astype(np.int32),
-                tile_lptr=tile_lptr.astype(np.int32), seg_tl=seg_tl.astype(np.uint16),
-                tl_slot=tl_slot.astype(np.int32), los_ptr_tile=los_ptr_t.astype(np.int32))
 
 
 def box_plan_apply(P, x, mode):
@@ -382,23 +274,16 @@ def box_plan_apply(P, x, mode):
         return (lyr * H + yy) * W + xx, ok
     if mode == "times":
         x = x.reshape(-1)
-        tiled = P.get("ntile", 0) > 0
-        part = np.zeros(len(P["tl_slot"]) if tiled else P["nseg"])
-        items = P["tile_items"] if tiled else range(P["nitems"])
-        for i in items:
+        part = np.zeros(P["nseg"])
+        for i in range(P["nitems"]):
             p, ok = pix(int(P["item_box"][i]))
             u = np.where(ok, x[np.where(ok, p, 0)], 0.)
             for s in range(P["item_seg"][i], P["item_seg"][i + 1]):
                 acc = 0.
                 for k in range(P["seg_ent"][s], P["seg_ent"][s + 1]):
                     acc += float(P["ent_wf"][k]) * u[P["ent_loc"][k]]
-                if tiled:
-                    # the tile's line accumulator (items in tile order)
-                    t = int(np.searchsorted(P["tile_iptr"], np.flatnonzero(P["tile_items"] == i)[0], "right")) - 1
-                    part[P["tl_slot"][P["tile_lptr"][t] + P["seg_tl"][s]]] += acc
-                else:
-                    part[P["seg_slot"][s]] = acc
-        lp = P["los_ptr_tile"] if tiled else P["los_ptr"]
+                part[P["seg_slot"][s]] = acc
+        lp = P["los_ptr"]
         return np.array([part[lp[i]:lp[i + 1]].sum() for i in range(nlos)])
     out = np.zeros(P["L"] * H * W)
     for b in range(P["nbox"]):
@@ -436,18 +321,10 @@ class LOSResponse(LinearOperator):
             keep = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
                     for k, v in P.items() if isinstance(v, np.ndarray)}
             d = _native.LosPlan()
-            for k in ("H", "W", "bh", "bw", "nby", "nbx", "nbox", "nlos", "nitems", "nseg", "lidx8", "ntile", "tile_S",
-                      "tl_max", "lpad"):
+            for k in ("H", "W", "bh", "bw", "nby", "nbx", "nbox", "nlos", "nitems", "nseg", "lidx8"):
                 setattr(d, k, int(P.get(k, 0)))
             for k, v in keep.items():
-                if (k == "slot_seg" and not SEG_MAJOR) or (k == "box_item" and not BOX_WG):
-                    continue
-                if k == "los_ptr_tile":
-                    continue
                 setattr(d, k, v.data_ptr() if v.numel() else None)
-            if P.get("ntile", 0) > 0:
-                # the line reduce walks the (line, tile) slots
-                d.los_ptr = keep["los_ptr_tile"].data_ptr()
             self._plan = (d, keep)
         return self._plan[0]
 

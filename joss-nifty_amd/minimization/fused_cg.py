@@ -268,101 +268,6 @@ def fused_cg_batch_or_none(energies, controllers, nreset):
     return FusedCGBatch(core, W, shift, controllers, nreset).run(energies)
 
 
-# Split iteration of the batched solve (data-space curvature only, opt-in
-# NFT_CG_SPLIT=1): the amplitude keys' JVP / VJP chains -- a dozen small
-# latency-bound launches, ~190 us per iteration at 2048^2 x 4 RHS -- on a
-# second (high-priority) stream next to the grid segment's direction and
-# update passes.  Measured (tools/split_check.py, rocprofv3 kernel trace): the
-# streams do overlap, but the side chain's bin scatter and scans slow from 36
-# to ~145 us under the grid update's full-bandwidth stream (their gathers
-# wait on a saturated memory system), so the iteration gains ~1 % (1232 ->
-# 1222 us graph replay): off by default.
-_SPLIT = os.environ.get("NFT_CG_SPLIT", "0") == "1"
-_SIDE = None
-
-
-def _side_stream():
-    global _SIDE
-    if _SIDE is None:
-        # high priority: the grid segment's streaming kernels occupy every CU,
-        # so the side stream's short launches must win the freed slots
-        _SIDE = torch.cuda.Stream(priority=-1)
-    return _SIDE
-
-
-class _SplitIteration:
-    """One CG iteration of FusedCGBatch with the packed vectors cut into the
-    grid segment G (the 'xi' key) and the amplitude segments A (the keys before
-    and after it):
-
-      main:  dir(A) | dir(G)        | grid matvec, fold curv, mirror fold | update(G)  | finalize
-      side:         | amplitude JVP |                                     | bin sums, amplitude VJP, update(A)
-
-    The per-element arithmetic is that of the one-stream iteration; the dot
-    partials of the three segments are folded in one fixed order."""
-
-    def __init__(self, lib, core, W, n, k, nq, shift, with_b):
-        self.lib, self.core, self.W = lib, core, W
-        self.n, self.k, self.nq, self.shift = n, k, nq, shift
-        g0, g1 = core.grid_segment()
-        rng = [(0, g0), (g0, g1), (g1, n)]
-        self.ranges = [(o, e - o) for o, e in rng if e > o]
-        nb = [int(lib.nft_cg_dd_blocks(ln)) for _, ln in self.ranges]
-        self.blk0 = [sum(nb[:i]) for i in range(len(nb))]
-        self.nbtot = sum(nb)
-        dev = core.device
-        self.PQ = torch.empty((k, self.nbtot + nq), dtype=torch.float64, device=dev)
-        self.UP = torch.empty((k, 3 * self.nbtot), dtype=torch.float64, device=dev)
-        self.grid_i = [i for i, (o, _) in enumerate(self.ranges) if o == g0][0]
-
-    def _dir(self, i, D, Rr, SC, s_):
-        o, ln = self.ranges[i]
-        e = 8  # fp64 bytes
-        _native._check(self.lib.nft_cg_direction_dd_batched(
-            ctypes.c_void_p(D.data_ptr() + o * e), ctypes.c_void_p(Rr.data_ptr() + o * e), ln, self.n, self.k, 0,
-            _native.ptr(SC), self.shift, ctypes.c_void_p(self.PQ.data_ptr() + self.blk0[i] * 8),
-            self.PQ.stride(0), s_))
-
-    def _update(self, i, X, Rr, D, Q, Bu, SC, s_):
-        o, ln = self.ranges[i]
-        e = 8
-        P = ctypes.c_void_p
-        _native._check(self.lib.nft_cg_update_seg_batched(
-            P(X.data_ptr() + o * e), P(Rr.data_ptr() + o * e), P(D.data_ptr() + o * e), P(Q.data_ptr() + o * e),
-            P(Bu.data_ptr() + o * e) if Bu is not None else P(0), ln, self.n, self.k, 0, self.shift,
-            _native.ptr(SC), _native.ptr(self.UP), self.nbtot, self.blk0[i], s_))
-
-    def __call__(self, X, Rr, D, Q, Bu, SC):
-        core, lib = self.core, self.lib
-        main = torch.cuda.current_stream()
-        side = _side_stream()
-        amp_i = [i for i in range(len(self.ranges)) if i != self.grid_i]
-        s_ = _native.stream_ptr()
-        for i in amp_i:
-            self._dir(i, D, Rr, SC, s_)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            da = core.mv_amp_jvp(D)
-        self._dir(self.grid_i, D, Rr, SC, s_)
-        main.wait_stream(side)
-        w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbtot:])
-        _native._check(lib.nft_fold_partials(_native.ptr(self.PQ), self.nbtot + self.nq, self.k,
-                                             ctypes.c_void_p(SC.data_ptr() + _native.CG_CURV * 8),
-                                             _native.CG_NSCALARS, s_))
-        # the mirror fold streams as much as the grid update: it stays on the
-        # main stream; the side stream gets the latency-bound rest
-        wf = core.mv_fold(w)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            core.mv_amp_vjp(D, w, Q, 0.0, folded=wf)
-            ss = _native.stream_ptr()
-            for i in amp_i:
-                self._update(i, X, Rr, D, Q, Bu, SC, ss)
-        self._update(self.grid_i, X, Rr, D, Q, Bu, SC, s_)
-        main.wait_stream(side)
-        _native._check(lib.nft_cg_finalize_batched(_native.ptr(self.UP), self.nbtot, self.k, _native.ptr(SC), s_))
-
-
 # The grid segment's CG update carried by the adjoint transform's epilogue
 # (data-space curvature: alpha is known before the adjoint): q's grid segment
 # is neither stored nor read back (NFT_CG_CARRY=0: separate update pass)
@@ -645,8 +550,6 @@ class FusedCGBatch(FusedCG):
                 st["PQ"] = torch.empty((k, st["nbd"] + nq), dtype=torch.float64, device=dev)
                 if carry:
                     st["split"] = _CarryIteration(lib, core, self.W, n, k, nq, sh)
-                elif _SPLIT and X.dtype == torch.float64 and hasattr(core, "mv_amp_jvp"):
-                    st["split"] = _SplitIteration(lib, core, self.W, n, k, nq, sh, st["Bu"] is not None)
         setup(k0)
 
         def record():
@@ -673,10 +576,6 @@ class FusedCGBatch(FusedCG):
                 split(X, Rr, D, Q, SC)
                 if st["xbdot"]:
                     chk(lib.nft_dot_batched(P(X), P(Bv), n, n, k, dt, P(SC[:, _native.CG_XB:]), NS, P(ws), s_))
-                record()
-                return
-            if with_dir and split is not None:
-                split(X, Rr, D, Q, Bu, SC)
                 record()
                 return
             if with_dir and nq:
@@ -734,8 +633,8 @@ class FusedCGBatch(FusedCG):
         # checks with their recorded scalars (HIST)
         chunkable = CHUNK and all(_count_silent(self.controllers[j]) for j in active)
         # which iteration this solve runs (diagnostics: tools/demo_profile.py)
-        self.path = ("carry" if isinstance(st["split"], _CarryIteration) else "split" if st["split"] is not None
-                     else "quad" if nq else "plain") + ("+chunk" if chunkable else "")
+        self.path = ("carry" if isinstance(st["split"], _CarryIteration) else "quad" if nq else "plain") + \
+            ("+chunk" if chunkable else "")
         self.compactions = 0
         iter_seen = np.zeros(k0)
         while active:

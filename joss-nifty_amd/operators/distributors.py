@@ -25,16 +25,11 @@ def _chunk_bins(offs, nbin, npix):
     return cb.astype(np.int32)
 
 
-class _SortedFold:
-    """fold_into's result in bin-sorted order (nf, pre): scatter_from sums
-    contiguous runs"""
+class _ILFold:
+    """fold_into's result in cell order with the items interleaved (nf, pre)"""
 
     def __init__(self, t):
         self.t = t
-
-
-class _ILFold(_SortedFold):
-    """fold_into's result in cell order with the items interleaved (nf, pre)"""
 
 
 class BinIndex:
@@ -82,10 +77,7 @@ class BinIndex:
         offs = np.zeros(self.nbin + 1, dtype=np.int64)
         np.cumsum(np.bincount(f, minlength=self.nbin), out=offs[1:])
         cb = _chunk_bins(offs, self.nbin, f.size)
-        cpos = np.empty(f.size, dtype=np.int32)
-        cpos[perm] = np.arange(f.size, dtype=np.int32)
         return dict(shape=tuple(int(n) for n in shp), nf=int(f.size),
-                    cpos=torch.from_numpy(cpos).to(device),                   # cell -> sorted position
                     pindex=torch.from_numpy(f.astype(np.int32)).to(device),   # cell -> bin
                     perm=torch.from_numpy(perm.astype(np.int32)).to(device),
                     offsets=torch.from_numpy(offs.astype(np.int32)).to(device),
@@ -115,12 +107,6 @@ class BinIndex:
         return _native.bin_scatter(wf, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
                                    order=f["order"])
 
-    # the half-grid fold written in bin-sorted order and contiguous bin sums
-    # (nft_bin_fold_half_sorted + nft_bin_sum_sorted, NFT_BIN_SORTED=1) --
-    # bitwise the fold in cell order + gathering scatter.  Measured at 4 x
-    # 2048^2: fold 27.5 -> 64 us (its stores scatter), sums 35 -> 32 us: off
-    SORTED = os.environ.get("NFT_BIN_SORTED", "0") == "1"
-
     # the half-grid fold with the items interleaved (bin_fold_half_sorted,
     # cpos None) + bin sums gathering all items of a cell at once
     # (nft_bin_scatter_il; NFT_BIN_IL=0: planar fold + per-item gathers) --
@@ -131,16 +117,14 @@ class BinIndex:
         """first half of scatter: the mirror fold of w into wf (pre, nf);
         returns the operand of scatter_from (wf, or w without a fold).
         half: w holds point-mirror pair sums on the half grid
-        (nft_hartley_fuse.epi_out2_pairs); then, for pre <= 8, wf receives
-        the fold in bin-sorted order (nf, pre) and the operand is tagged so"""
+        (nft_hartley_fuse.epi_out2_pairs); then, for pre in (2, 4, 8), wf
+        receives the fold with the items interleaved (nf, pre) and the operand
+        is tagged so"""
         f = self.fold
         if f is None:
             if half:
                 raise ValueError("pair sums need the folded bin index")
             return w
-        if half and self.SORTED and 1 <= pre <= 8:
-            _native.bin_fold_half_sorted(w, wf, f["cpos"], pre, f["shape"])
-            return _SortedFold(wf)
         if half and self.IL and pre in (2, 4, 8):
             _native.bin_fold_half_sorted(w, wf, None, pre, f["shape"])
             return _ILFold(wf)
@@ -155,38 +139,20 @@ class BinIndex:
                                        order=self.gather_order)
         if isinstance(src, _ILFold):
             return _native.bin_scatter_il(src.t, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin)
-        if isinstance(src, _SortedFold):
-            return _native.bin_sum_sorted(src.t, f["offsets"], out, pre, self.nbin)
         return _native.bin_scatter(src, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
                                    order=f["order"])
 
-    # pixel-ordered chunk gathers: measured no faster than the sorted ones at
-    # 2048^2 (the chunk kernel is bound by its per-bin phase, not by gather
-    # divergence), so only the precomputed chunk bounds are used by default
-    PIXEL_ORDER = False
-
     @property
     def gather_order(self):
-        """(gpix int32 | None, gslot uint16 as int16 storage | None, chunk_bins
-        int32) for nft_bin_scatter_ordered: within every chunk of
-        nft_bin_chunk() sorted positions the entries in ascending pixel order
-        and their position in the chunk; first bin owned by each chunk."""
+        """(None, None, chunk_bins int32) for nft_bin_scatter_ordered: the
+        first bin owned by each chunk of nft_bin_chunk() sorted positions
+        (pixel-ordered chunk gathers measured no faster at 2048^2: the chunk
+        kernel is bound by its per-bin phase, not by gather divergence)."""
         if self._order is None:
-            from .. import _native
-            ch = int(_native.load().nft_bin_chunk())
-            perm = self.perm.cpu().numpy().astype(np.int64)
-            dev = self.perm.device
-            nch = (perm.size + ch - 1) // ch
+            perm = self.perm
             offs = self.offsets.cpu().numpy().astype(np.int64)
-            cbt = torch.from_numpy(_chunk_bins(offs, self.nbin, perm.size)).to(dev)
-            if self.PIXEL_ORDER:
-                cid = np.arange(perm.size, dtype=np.int64) // ch
-                order = np.lexsort((perm, cid))
-                gslot = (order - cid * ch).astype(np.uint16)
-                self._order = (torch.from_numpy(perm[order].astype(np.int32)).to(dev),
-                               torch.from_numpy(gslot.view(np.int16)).to(dev), cbt)
-            else:
-                self._order = (None, None, cbt)
+            cbt = torch.from_numpy(_chunk_bins(offs, self.nbin, perm.numel())).to(perm.device)
+            self._order = (None, None, cbt)
         return self._order
 
     @classmethod

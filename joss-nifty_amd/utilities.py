@@ -193,7 +193,9 @@ class _Packed:
                 n = r.numel()
                 v = buf[off:off + n].reshape(r.shape).to(self.ts[i].device)
                 t = self.ts[i]
-                out[i] = torch.view_as_complex(v.contiguous()) if t.is_complex() else v.to(t.dtype)
+                # a complex run after an odd count of real elements starts at
+                # an odd storage offset, which view_as_complex rejects: clone
+                out[i] = torch.view_as_complex(v.clone()) if t.is_complex() else v.to(t.dtype)
                 off += n
         return self.rebuild(out)
 
@@ -236,6 +238,15 @@ def allreduce_sum(obj, comm, deterministic=None, counts=None, template=None):
     counts = [int(c) for c in counts]
     if sum(counts) == 0:
         raise ValueError("allreduce_sum over no items at all")
+    if min(counts) == 0:
+        # every rank must issue the same per-dtype collectives: a rank without
+        # items casts its template to the element dtypes of the ranks' items
+        mine = tuple(str(t.dtype) for t in _flatten(vals[0])[0]) if vals else None
+        lays = [x for x in comm.allgather(mine) if x is not None]
+        if any(x != lays[0] for x in lays):
+            raise RuntimeError("allreduce_sum: ranks hold items of different dtype layouts")
+        if not vals and template is not None:
+            template = _typed_template(template, lays[0])
     if deterministic:
         return _tree_sum(vals, comm, counts, template)
     if vals:
@@ -249,6 +260,16 @@ def allreduce_sum(obj, comm, deterministic=None, counts=None, template=None):
     for b in bufs:
         comm.allreduce_tensor_(b)
     return pk.unpack(bufs)
+
+
+def _typed_template(template, dtypes):
+    """template() with its tensors cast to `dtypes` (names as str(dtype))"""
+    def typed():
+        ts, rebuild = _flatten(template())
+        if len(ts) != len(dtypes):
+            raise RuntimeError("allreduce_sum: the template does not match the items' layout")
+        return rebuild([t.to(getattr(torch, d.split(".")[-1])) for t, d in zip(ts, dtypes)])
+    return typed
 
 
 def _tree_sum(vals, comm, counts, template):

@@ -50,9 +50,16 @@ def test_compacted_count_only_vs_sequential(ift, which):
     es = _energies(ift, cf, A, 3, 3)
     lims = [4, 11, 25]
     seq = [FusedCG(core, W, shift, ift.GradientNormController(iteration_limit=m)).run(e) for e, m in zip(es, lims)]
+    from nifty_amd.minimization import fused_cg
     cg = FusedCGBatch(core, W, shift, [ift.GradientNormController(iteration_limit=m) for m in lims])
+    n0 = fused_cg.STATS["carry_iters"]
     bat = cg.run(es)
     assert cg.compactions >= 1
+    if which == "los":
+        # the carried iteration (amplitude keys in the two-phase kernels) ran
+        # before and after the compaction
+        assert cg.path == "carry+chunk", cg.path
+        assert fused_cg.STATS["carry_iters"] - n0 >= 20
     for (e1, s1), (e2, s2) in zip(seq, bat):
         assert s1 == s2
         for key in cf.domain.keys():

@@ -246,6 +246,25 @@ def _worker_lists(rank, world, port, q, tmp):
         lo, hi = utilities.shareRange(7, world, rank)
         t = utilities.allreduce_sum(items[lo:hi], comm, deterministic=True)
         res["det32c"] = {k: np.asarray(t[k]) for k in d2.keys()}
+        # a complex field packed after an odd count of fp64 elements (energy
+        # value, complex field): odd storage offset in the shared buffer
+        tup = [(float(i) + 0.25, ift.makeField(d2["c"], np.asarray(items[i]["c"].val.cpu())))
+               for i in range(7)]
+        res["odd"] = {}
+        for det in (False, True):
+            v, f = utilities.allreduce_sum(tup[lo:hi], comm, deterministic=det)
+            res["odd"][det] = (v, np.asarray(f.val.cpu()))
+        # fp32 / complex samples on rank 0 only: rank 1's zero template takes
+        # the samples' dtypes (same collectives on both ranks)
+        sl2 = ift.SampleList(items[:1] if rank == 0 else [], comm=comm, domain=d2)
+        res["avg32c"] = {}
+        for det in (False, True):
+            utilities.DETERMINISTIC_ALLREDUCE, keep = det, utilities.DETERMINISTIC_ALLREDUCE
+            try:
+                a = sl2.average()
+            finally:
+                utilities.DETERMINISTIC_ALLREDUCE = keep
+            res["avg32c"][det] = {k: np.asarray(a[k].val.cpu()) for k in d2.keys()}
         comm.Barrier()
         dist.destroy_process_group()
         q.put((rank, res))
@@ -310,6 +329,42 @@ def test_deterministic_tree_fp32_complex(list_results):
             want = np.asarray(serial[k])
             assert got.dtype == want.dtype, (k, got.dtype)
             np.testing.assert_array_equal(got, want)
+
+
+def test_allreduce_complex_odd_offset(list_results):
+    """(scalar, complex field) tuples: the complex run starts at an odd offset
+    of the packed fp64 buffer; both reduction modes rebuild it"""
+    sys.path.insert(0, ROOT)
+    import nifty_amd as ift
+    from nifty_amd import utilities
+    d2 = ift.makeDomain({"f": ift.RGSpace(9), "c": ift.RGSpace((3, 4))})
+    rng = np.random.default_rng(3)
+    cs = []
+    for i in range(7):
+        rng.standard_normal(9), rng.integers(-4, 4, 9)
+        cs.append(rng.standard_normal((3, 4)) * 10.0 ** rng.integers(-6, 6, (3, 4)) + 1j * rng.standard_normal((3, 4)))
+    tup = [(float(i) + 0.25, ift.makeField(d2["c"], cs[i])) for i in range(7)]
+    sv, sf = utilities.pairwise_sum(tup)
+    for r in list_results:
+        for det in (False, True):
+            v, f = list_results[r]["odd"][det]
+            assert v == sv
+            assert f.dtype == np.complex128
+            if det:
+                np.testing.assert_array_equal(f, np.asarray(sf.val.cpu()))
+            else:
+                np.testing.assert_allclose(f, np.asarray(sf.val.cpu()), rtol=1e-14, atol=0)
+
+
+def test_average_empty_rank_dtypes(list_results):
+    """a rank without samples reduces with the samples' fp32 / complex dtypes"""
+    for r in list_results:
+        ref = list_results[0]["avg32c"][False]
+        for det in (False, True):
+            got = list_results[r]["avg32c"][det]
+            assert got["f"].dtype == np.float32 and got["c"].dtype == np.complex128
+            for k in ("f", "c"):
+                np.testing.assert_array_equal(got[k], ref[k])
 
 
 def _worker_desync(rank, world, port, q):

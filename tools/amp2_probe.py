@@ -32,7 +32,7 @@ def main():
     for _ in range(reps):
         bench.cg_iteration(lib, core, W, shift, bufs, k)
     torch.cuda.synchronize()
-    us, _ = bench.cg_iteration_wall(lib, core, W, shift, bufs, k)
+    us = bench.cg_iteration_wall(lib, core, W, shift, bufs, k)
     print("NFT_CG_AMP2=%s NFT_AMP2_DBG=%s iteration %.1f us" % (os.environ.get("NFT_CG_AMP2", "1"),
                                                                os.environ.get("NFT_AMP2_DBG", "0"), us), flush=True)
 
