@@ -14,7 +14,7 @@ from .domain_tuple import DomainTuple
 from .domains import DOFSpace, Domain, PowerSpace, RGSpace, StructuredDomain, UnstructuredDomain
 from .ducc_dispatch import nthreads, set_nthreads
 from .field import Field
-from .library.correlated_fields import _SlopeRemover, _SpecialSum, _TwoLogIntegrations
+from .library.correlated_fields import CorrelatedFieldMaker, _SlopeRemover, _SpecialSum, _TwoLogIntegrations
 from .library.correlated_fields_simple import CFJacobian, SimpleCorrelatedField
 from .library.los_response import LOSResponse
 from .linearization import Linearization

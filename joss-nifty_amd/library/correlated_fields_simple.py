@@ -119,14 +119,15 @@ class _AmplitudeModel:
     """Amplitude A(theta) on the PowerSpace, its JVP and VJP (B-sized math)."""
 
     def __init__(self, target, harmonic_partner, offset_std, fluctuations, flexibility, asperity,
-                 loglogavgslope, prefix):
+                 loglogavgslope, prefix, zm_prefix=None):
         self.pspace = PowerSpace(harmonic_partner)
         self.B = self.pspace.shape[0]
         self.prefix = prefix
         p = prefix
+        zp = prefix if zm_prefix is None else zm_prefix
         self.k_fl, self.k_sl = p + "fluctuations", p + "loglogavgslope"
         self.k_flex, self.k_asp = p + "flexibility", p + "asperity"
-        self.k_spec, self.k_zm = p + "spectrum", p + "zeromode"
+        self.k_spec, self.k_zm = p + "spectrum", zp + "zeromode"
         self.has_flex = flexibility is not None
         self.has_asp = asperity is not None
         self.has_zm = offset_std is not None
@@ -894,11 +895,17 @@ class CFJacobian(LinearOperator):
 
 
 class _CorrelatedFieldModel(Operator):
+    """The fused correlated field.  `prefix` names the amplitude keys;
+    `xi_prefix` (default: `prefix`) names 'xi' and 'zeromode', which the
+    CorrelatedFieldMaker keys by the maker's prefix alone
+    (correlated_fields.py:578-581,759,806)."""
+
     def __init__(self, target, harmonic_partner, offset_mean, offset_std, fluctuations, flexibility,
-                 asperity, loglogavgslope, prefix):
+                 asperity, loglogavgslope, prefix, xi_prefix=None):
+        xp = prefix if xi_prefix is None else xi_prefix
         self.amp = _AmplitudeModel(target, harmonic_partner, offset_std, fluctuations, flexibility,
-                                   asperity, loglogavgslope, prefix)
-        self.k_xi = prefix + "xi"
+                                   asperity, loglogavgslope, prefix, zm_prefix=xp)
+        self.k_xi = xp + "xi"
         dom = dict(self.amp.domain_dict)
         dom[self.k_xi] = DomainTuple.make(harmonic_partner)
         self._domain = MultiDomain.make(dom)

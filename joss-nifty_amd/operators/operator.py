@@ -70,6 +70,13 @@ class Operator:
         from .contraction_operator import ContractionOperator
         return ContractionOperator(self.target, spaces)(self)
 
+    def integrate(self, spaces=None):
+        from .contraction_operator import IntegrationOperator
+        return IntegrationOperator(self.target, spaces)(self)
+
+    def power(self, exponent):
+        return self.ptw("power", exponent)
+
     def vdot(self, other):
         from ..sugar import makeOp
         if other.jac is None and _is_fieldlike(other):

@@ -924,6 +924,71 @@ def gen_fftop():
     _save("fftop.npz", d)
 
 
+def _op_case(op, seed, d, tag):
+    """value, Jacobian and adjoint of `op` at a fixed random point"""
+    with ift.random.Context(seed):
+        x = ift.from_random(op.domain, "normal")
+        t = ift.from_random(op.domain, "normal")
+        g = ift.from_random(op.target, "normal")
+    lin = op(ift.Linearization.make_var(x))
+    for k, v in _flat(x).items():
+        d[f"{tag}x_" + k] = v
+    for k, v in _flat(t).items():
+        d[f"{tag}t_" + k] = v
+    d[tag + "g"] = g.val
+    d[tag + "val"] = lin.val.val
+    d[tag + "jt"] = lin.jac(t).val
+    for k, v in _flat(lin.jac.adjoint(g)).items():
+        d[f"{tag}ja_" + k] = v
+    return x
+
+
+def gen_cfm():
+    """CorrelatedFieldMaker (src/library/correlated_fields.py:388-1115):
+    a two-component product spectrum (2-D space x 1-D frequency, LogNormal
+    zero mode, offset), a single component with a maker prefix distinct from
+    the component prefix (the fused lowering), a unit zero mode and a Matern
+    component; values, Jacobians, adjoints and normalised amplitudes."""
+    d = {}
+    sp = ift.RGSpace((24, 20), distances=(0.05, 0.07))
+    fr = ift.RGSpace(18, distances=0.3)
+    cfm = ift.CorrelatedFieldMaker("pp_")
+    cfm.add_fluctuations(sp, (1., 0.4), (1.2, 0.5), (0.6, 0.3), (-3., 0.5), prefix="sp_")
+    cfm.add_fluctuations(fr, (0.7, 0.2), (0.9, 0.4), None, (-2., 0.4), prefix="fr_")
+    cfm.set_amplitude_total_offset(0.3, (0.8, 0.1))
+    op = cfm.finalize(prior_info=0)
+    x = _op_case(op, 41, d, "prod_")
+    for i, na in enumerate(cfm.get_normalized_amplitudes()):
+        d[f"prod_na{i}"] = na.force(x).val
+    d["prod_totfl"] = np.asarray(cfm.total_fluctuation.force(x).val)
+    for i in range(2):
+        d[f"prod_slfl{i}"] = np.asarray(cfm.slice_fluctuation(i).force(x).val)
+        d[f"prod_avfl{i}"] = np.asarray(cfm.average_fluctuation(i).force(x).val)
+
+    one = ift.RGSpace((40, 36), distances=(0.02, 0.03))
+    cfm = ift.CorrelatedFieldMaker("mk_")
+    cfm.add_fluctuations(one, (0.9, 0.3), (1.1, 0.4), (0.5, 0.2), (-2.5, 0.6), prefix="amp_")
+    cfm.set_amplitude_total_offset(-0.4, (1e-2, 1e-3))
+    op = cfm.finalize(prior_info=0)
+    x = _op_case(op, 42, d, "one_")
+    d["one_amp"] = cfm.amplitude.force(x).val
+
+    cfm = ift.CorrelatedFieldMaker("u_")
+    cfm.add_fluctuations(ift.RGSpace(64), (1., 0.5), None, None, (-3., 1.))
+    cfm.set_amplitude_total_offset(0., 1.)
+    op = cfm.finalize(prior_info=0)
+    x = _op_case(op, 43, d, "unit_")
+    d["unit_amp"] = cfm.amplitude.force(x).val
+
+    cfm = ift.CorrelatedFieldMaker("m_")
+    cfm.add_fluctuations_matern(ift.RGSpace((32, 32), distances=0.1), (1., 0.3), (2., 0.5), (-3., 0.5))
+    cfm.set_amplitude_total_offset(1., (1e-2, 1e-3))
+    op = cfm.finalize(prior_info=0)
+    x = _op_case(op, 44, d, "mat_")
+    d["mat_amp"] = cfm.amplitude.force(x).val
+    _save("cfm.npz", d)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -940,3 +1005,4 @@ if __name__ == "__main__":
     gen_random()
     gen_kl_constants()
     gen_napprox()
+    gen_cfm()
