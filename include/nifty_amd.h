@@ -275,6 +275,20 @@ typedef struct nft_hartley_fuse {
    * second output's bytes; nft_bin_fold_half completes the mirror fold from
    * it (engine-v2 strided unpack pass only). */
   int64_t epi_out2_pairs;
+  /* quadratic form of a pointwise weight carried by the epilogue
+   * (quad_part != NULL; batched, epi_a the only epilogue operand, no CG
+   * epilogue; the same geometries as the CG epilogue): out = epi_a * h is
+   * stored as usual and per transform tile of item b the fp64 sum of
+   * h * out over the tile's elements lands at quad_part[b * quad_pstride +
+   * quad_blk0 + tile], tile < nft_hartley_cg_blocks.  With epi_a = W this is
+   * the data-space curvature (J d).W(J d) of a sampling metric
+   * J^T W J with a pointwise W (Gaussian / Poisson likelihoods), formed
+   * while the forward transform writes W J d -- the partials that
+   * nft_fold_partials folds into the CG curvature (src/minimization/
+   * conjugate_gradient.py:96-101 computes it as d.(A d)). */
+  double* quad_part;
+  int64_t quad_pstride;
+  int32_t quad_blk0, quad_pad;
 } nft_hartley_fuse;
 
 /* Partial blocks per item of the CG-carrying epilogue for a batched
@@ -440,10 +454,6 @@ int nft_cg_finalize_batched(const double* part, int nbtot, int nrhs, double* sc,
 typedef struct nft_amp_const {
   const double *c0, *sf, *p0, *p1, *p2, *lv;
   const double *vslope, *sc, *Qf, *Qa, *mspec, *An;
-  /* tables of the two-phase kernels (nft_amp2_prepare; NULL until prepared):
-   * constant tile-local scans, constant tile sums and global sums of this
-   * linearisation point, nft_amp2_tab_len(B) doubles */
-  const double* tab;
   double fl, S, ls_f, sig_s, zm, ls_o, total_volume;
   int64_t B;
   int has_flex, has_asp, has_zm;
@@ -485,10 +495,6 @@ int nft_amp_vjp_batched(const nft_amp_const* c, const nft_amp_const* item_consts
  * first forms per-tile dot products of the tangent / cotangent with constant
  * vectors, the second the tile carries in a fixed order, the tile-local scans
  * and the outputs); the batched forms above take this path when it applies.
- * The constant sets must carry their tables (nft_amp_const.tab), made once
- * per linearisation point by nft_amp2_prepare: for the host set *c
- * (item_consts NULL, tables into tab) or for nrow DEVICE sets item_consts[r]
- * (tables into tab + r * tab_stride, item_consts[r].tab set on the device).
  * These kernels keep device-global arrival counters: do not run them on two
  * streams at once.  Key arrays are indexed fl, sl, flex, asp, zm, spec (NULL:
  * absent key), pointing at right-hand side 0, rows lat_stride elements apart.
@@ -522,18 +528,17 @@ int nft_amp2_enabled(void);
  * tests); on < 0: back to the environment (NFT_AMP2) */
 void nft_amp2_set_enabled(int on);
 int nft_amp2_tiles(int64_t B, int nrhs, int item_mode);
-int64_t nft_amp2_tab_len(int64_t B);
-int nft_amp2_prepare(const nft_amp_const* c, nft_amp_const* item_consts, int nrow, double* tab, int64_t tab_stride,
-                     hipStream_t stream);
-int nft_amp2_jvp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, double* const* t,
-                 const double* const* r, int64_t lat_stride, double* da, int64_t da_stride, int64_t da_elem_stride,
-                 double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift,
+/* dtype (0 fp64, 1 fp32): the element type of the key arrays, da and g
+ * (the fp32-storage CG); constants, workspace, sums, part and sc stay fp64 and
+ * every sum accumulates in fp64. */
+int nft_amp2_jvp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, void* const* t,
+                 const void* const* r, int64_t lat_stride, void* da, int64_t da_stride, int64_t da_elem_stride,
+                 double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift, int dtype,
                  hipStream_t stream);
-int nft_amp2_vjp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, const double* g,
-                 int64_t g_stride,
-                 double* const* out, double* const* out2, const double* const* d, int64_t lat_stride, double shift,
-                 double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
-                 int64_t gp_stride, int64_t gp_row, int ngp, hipStream_t stream);
+int nft_amp2_vjp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, const void* g,
+                 int64_t g_stride, void* const* out, void* const* out2, const void* const* d, int64_t lat_stride,
+                 double shift, double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
+                 int64_t gp_stride, int64_t gp_row, int ngp, int dtype, hipStream_t stream);
 
 
 

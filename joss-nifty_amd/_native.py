@@ -78,10 +78,9 @@ SIGNATURES = {
     "nft_amp2_enabled": (_i, []),
     "nft_amp2_set_enabled": (None, [_i]),
     "nft_amp2_tiles": (_i, [_i64, _i, _i]),
-    "nft_amp2_tab_len": (_i64, [_i64]),
-    "nft_amp2_prepare": (_i, [_p, _p, _i, _p, _i64, _p]),
-    "nft_amp2_jvp": (_i, [_p, _p, _i, _p, _p, _i64, _p, _i64, _i64, _p, _i, _p, _p, _i64, _d, _p]),
-    "nft_amp2_vjp": (_i, [_p, _p, _i, _p, _i64, _p, _p, _p, _i64, _d, _p, _i, _p, _p, _i64, _p, _i64, _i64, _i, _p]),
+    "nft_amp2_jvp": (_i, [_p, _p, _i, _p, _p, _i64, _p, _i64, _i64, _p, _i, _p, _p, _i64, _d, _i, _p]),
+    "nft_amp2_vjp": (_i, [_p, _p, _i, _p, _i64, _p, _p, _p, _i64, _d, _p, _i, _p, _p, _i64, _p, _i64, _i64, _i, _i,
+                          _p]),
     "nft_amp_forward_buf": (_i64, [_i64]),
     "nft_amp_forward_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _p, _i64, _p, _i64, _p, _p, _p]),
 }
@@ -98,7 +97,8 @@ class HartleyFuse(ctypes.Structure):
                [("cg_stride", _i64), ("cg_shift", _d), ("cg_nbtot", ctypes.c_int32), ("cg_blk0", ctypes.c_int32)] + \
                [(n, _p) for n in ("dir_r", "dir_sc", "dir_part")] + \
                [("dir_pstride", _i64), ("dir_shift", _d), ("dir_blk0", ctypes.c_int32), ("dir_pad", ctypes.c_int32)] + \
-               [("epi_out2_pairs", _i64)]
+               [("epi_out2_pairs", _i64)] + \
+               [("quad_part", _p), ("quad_pstride", _i64), ("quad_blk0", ctypes.c_int32), ("quad_pad", ctypes.c_int32)]
 
 
 class LosPlan(ctypes.Structure):
@@ -113,7 +113,7 @@ class LosPlan(ctypes.Structure):
 class AmpConst(ctypes.Structure):
     """nft_amp_const (include/nifty_amd.h)."""
     _fields_ = [(n, _p) for n in ("c0", "sf", "p0", "p1", "p2", "lv", "vslope", "sc", "Qf", "Qa",
-                                  "mspec", "An", "tab")] + \
+                                  "mspec", "An")] + \
                [(n, _d) for n in ("fl", "S", "ls_f", "sig_s", "zm", "ls_o", "total_volume")] + \
                [("B", _i64), ("has_flex", _i), ("has_asp", _i), ("has_zm", _i)]
 
@@ -383,7 +383,8 @@ def hartley_dir_blocks(grid):
     return int(load().nft_hartley_dir_blocks(len(grid), sh))
 
 
-def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None, cg=None):
+def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None, cg=None,
+                  quad=None):
     """out = epilogue(scale * Hartley(prologue)) with
     pro = dict(a=, x=, b=, c=, index=) (or fold=True and c per fundamental
     cell instead of index, nft_hartley_fuse.pro_folded) and
@@ -437,6 +438,14 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
         f.cg_shift = float(cg["shift"])
         f.cg_nbtot = int(cg["nbtot"])
         f.cg_blk0 = int(cg["blk0"])
+    if quad:
+        # per-tile partials of h * (epi_a * h) (nft_hartley_fuse.quad_*)
+        qp = quad["part"]
+        if not (qp.is_cuda and qp.dtype == torch.float64 and qp.stride(-1) == 1):
+            raise NativeError("quad part: fp64 device rows with unit element stride")
+        f.quad_part = qp.data_ptr()
+        f.quad_pstride = int(quad["pstride"])
+        f.quad_blk0 = int(quad.get("blk0", 0))
     if batch:
         for t in tens:
             if t is not None and not t.is_cuda:

@@ -59,9 +59,12 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
       if constexpr (persist_ok<N, NT, KIND>())
         (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if constexpr (KIND == K_UNPACK && !ROWS)
-        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, true>,
+      if constexpr (KIND == K_UNPACK && !ROWS) {
+        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, 1>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, 2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      }
       attr_set = true;
     }
   }
@@ -73,10 +76,13 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     set_last_error("out2 pair sums: only the strided unpack pass stores them");
     return NFT_ERR_UNSUPPORTED;
   }
-  if (a.f.cg) {
-    // the CG update rides only in the strided unpack pass, one item per tile
-    if (KIND != K_UNPACK || ROWS || a.los != 0 || a.f.nb < 1 || a.g.O != a.f.nb || ntiles % a.g.O != 0) {
-      set_last_error("CG-carrying epilogue: needs the strided unpack pass with one item per tile");
+  if (a.f.cg || a.f.quad) {
+    // the CG update / the quadratic-form partials ride only in the strided
+    // unpack pass, one item per tile
+    if (KIND != K_UNPACK || ROWS || a.los != 0 || a.f.nb < 1 || a.g.O != a.f.nb || ntiles % a.g.O != 0 ||
+        (a.f.quad && (a.f.cg || !a.f.ea || a.f.ed || a.f.out2))) {
+      set_last_error("CG-carrying / quadratic-form epilogue: needs the strided unpack pass with one item per "
+                     "tile (quad: epi_a only)");
       return NFT_ERR_UNSUPPORTED;
     }
     b.f.ctr = ntiles / a.g.O;
@@ -89,7 +95,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     // plain epilogue (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us), faster
     // for the CG-carrying epilogue, which is bound by its HBM traffic (the
     // contiguous flavour, 231 -> 221 us): that pass only
-    const int mode = f.cg ? 2 : 0;
+    const int mode = (f.cg || f.quad) ? 2 : 0;
     if (mode > 0 && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) {
       b.bgroup = f.nb;
       b.bmode = mode;
@@ -108,7 +114,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   constexpr int per_cu = 8;
   static const char* const kind_name[4] = {"fft_c2c", "fft_r2c", "fft_h1d", "fft_unpack"};
   static const char* const kind_fused[4] = {"fft_c2c", "fft_r2c+pro", "fft_h1d+fused", "fft_unpack+epi"};
-  prof_mark(s, a.f.cg ? "fft_unpack+cg" : (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
+  prof_mark(s, a.f.cg ? "fft_unpack+cg" : a.f.quad ? "fft_unpack+quad" : (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
   bool launched = false;
   if constexpr (persist_ok<N, NT, KIND>()) {
     if (!launched && !a.f.pro) {
@@ -119,8 +125,11 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   }
   if constexpr (KIND == K_UNPACK && !ROWS) {
     if (!launched && a.f.cg) {
-      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, true>), dim3((unsigned)ntiles), dim3(NT), lds, s,
-                         b);
+      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 1>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
+      launched = true;
+    }
+    if (!launched && a.f.quad) {
+      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 2>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
       launched = true;
     }
   }

@@ -61,6 +61,13 @@ struct FuseArgs {
   long long dps;
   double dshift;
   int dblk0;
+  // quadratic form of a pointwise weight carried by the unpack epilogue
+  // (nft_hartley_fuse.quad_*): per tile the sum of h * (ea * h) over its
+  // elements at qpart[item * qps + qblk0 + tile] (one item per tile)
+  int quad;
+  double* qpart;
+  long long qps;
+  int qblk0;
 };
 
 // element index into pc of item-element j: its bin (pidx[j]) or, folded, the
@@ -240,9 +247,11 @@ constexpr size_t pass_lds_bytes() {
   return tw_lds_offset<T, N, NT, KIND, ROWS>() + (size_t)(N / 4) * sizeof(cplx_t<T>);
 }
 
-// CGE (unpack passes): the CG-carrying epilogue (a.f.cg) compiled alone; the
-// plain unpack instance carries none of its registers (occupancy)
-template <typename T, int N, int NT, int KIND, bool ROWS, bool PF, bool CGE = false>
+// EM (unpack passes): epilogue mode -- 0 plain, 1 the CG-carrying epilogue
+// (a.f.cg), 2 the plain epilogue plus the per-tile quadratic-form partials
+// (a.f.quad).  Each compiled alone: the plain unpack instance carries none of
+// their registers (occupancy)
+template <typename T, int N, int NT, int KIND, bool ROWS, bool PF, int EM = 0>
 __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   // Persistent: workgroup b processes tiles b, b + G, b + 2G, ...  The input
   // of tile t + G is loaded into registers while tile t is transformed and
@@ -442,7 +451,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       __syncthreads();
       const T sg = (T)a.sigma, sc = a.scale;
       const int Nf = a.Nfull;
-      if constexpr (!CGE) {
+      if constexpr (EM == 0) {
 #pragma unroll
         for (int r = 0; r < VPT; ++r) {
           int l, x;
@@ -463,6 +472,44 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
             fuse_store<T>(a.f, out, im, hm);
           }
           if (a.f.o2h) fuse_store_pair<T>(a.f, ib, hb, u.mirror != 0, im, hm);
+        }
+      } else if constexpr (EM == 2) {
+        // out = ea * h (shared weight, no shift / second output) and the
+        // tile's sum of h * out: the metric's data-space quadratic form
+        // (J d).W(J d) of a pointwise W, one item per tile (los = 0)
+        const long long item = o;
+        const T* __restrict__ ea = (const T*)a.f.ea;
+        double qs = 0.0;
+#pragma unroll
+        for (int r = 0; r < VPT; ++r) {
+          int l, x;
+          lx_of(r, l, x);
+          const UnpackLine u = lines[l];
+          if (!u.valid) continue;
+          const C f = lds[l * PITCH + padx<PS>(x)];
+          const int k = (int)m * a.km + x * a.kx;
+          const T hv[2] = {sc * (f.x + sg * f.y), sc * (f.x - sg * f.y)};
+          const int km = (k == 0) ? 0 : Nf - k;
+          const long long idx[2] = {u.base + (long long)k * a.rs, u.mbase + (long long)km * a.rs};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (h == 1 && !u.mirror) continue;
+            long long b, j;
+            fuse_split(a.f, idx[h], b, j);
+            const T q = ea[b * a.f.sea + j] * hv[h];
+            out[b * a.f.so + j] = q;
+            qs += (double)hv[h] * (double)q;
+          }
+        }
+        __shared__ double qsh[NT / 64];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) qs += __shfl_down(qs, off, 64);
+        if ((tid & 63) == 0) qsh[tid >> 6] = qs;
+        __syncthreads();
+        if (tid == 0) {
+          double s0 = 0.0;
+          for (int w = 0; w < NT / 64; ++w) s0 += qsh[w];
+          a.f.qpart[item * a.f.qps + a.f.qblk0 + (t - item * a.f.ctr)] = s0;
         }
       } else {
         // one item per tile (los = 0): its step length from its CG scalars

@@ -941,7 +941,6 @@ __global__ __launch_bounds__(AT) void amp_fwd_4(AmpModel m, FwdLat x, double* bu
     c.Qa = fx && m.has_asp ? w.Qa : nullptr;
     c.mspec = w.mspec;
     c.An = w.An;
-    c.tab = nullptr;  // nft_amp2_prepare fills it on first use
     c.fl = sc.fl;
     c.S = S;
     c.ls_f = m.ls_f;
@@ -983,10 +982,10 @@ int nft_amp_jvp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
   const int n7 = nblk(B, AT) < 1024 ? nblk(B, AT) : 1024;
   {
     // two-phase tiles (nft_amp2.hip) where they apply
-    double* t[6] = {const_cast<double*>(tfl), const_cast<double*>(tsl), const_cast<double*>(tflex),
-                    const_cast<double*>(tasp), const_cast<double*>(tzm), const_cast<double*>(tspec)};
-    const int st = nft_amp2_jvp(cst, dcs, dcs ? 1 : 0, t, nullptr, ls, da, vs, da_elem_stride, ws, nrhs, nullptr, nullptr, 0, 0.0,
-                                s);
+    void* t[6] = {const_cast<double*>(tfl), const_cast<double*>(tsl), const_cast<double*>(tflex),
+                  const_cast<double*>(tasp), const_cast<double*>(tzm), const_cast<double*>(tspec)};
+    const int st = nft_amp2_jvp(cst, dcs, dcs ? 1 : 0, t, nullptr, ls, da, vs, da_elem_stride, ws, nrhs, nullptr,
+                                nullptr, 0, 0.0, 0, s);
     if (st != NFT_AMP2_FALLBACK) return st;
   }
   const unsigned ny = (unsigned)nrhs;
@@ -1029,10 +1028,10 @@ int nft_amp_vjp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
   double* tot4 = tot3 + nbM + 1;
   double* part45 = tot4 + nbM + 1;
   {
-    double* out[6] = {o.fl, o.sl, o.flex, o.asp, o.zm, o.spec};
-    const double* d[6] = {o.dfl, o.dsl, o.dflex, o.dasp, o.dzm, o.dspec};
-    const int st = nft_amp2_vjp(cst, dcs, dcs ? 1 : 0, g, vs, out, nullptr, d, ls, o.shift, ws, nrhs, nullptr, nullptr, 0,
-                                nullptr, 0, 0, 0, s);
+    void* out[6] = {o.fl, o.sl, o.flex, o.asp, o.zm, o.spec};
+    const void* d[6] = {o.dfl, o.dsl, o.dflex, o.dasp, o.dzm, o.dspec};
+    const int st = nft_amp2_vjp(cst, dcs, dcs ? 1 : 0, g, vs, out, nullptr, d, ls, o.shift, ws, nrhs, nullptr, nullptr,
+                                0, nullptr, 0, 0, 0, 0, s);
     if (st != NFT_AMP2_FALLBACK) return st;
   }
   const unsigned ny = (unsigned)nrhs;

@@ -1,46 +1,40 @@
-// Correlated-field amplitude Jacobian, two launches per JVP / VJP, carrying
-// the amplitude keys' CG direction (JVP) and the CG update + finalize (VJP).
+// Correlated-field amplitude Jacobian in two launches per JVP / VJP ("two-phase
+// tiles"), optionally carrying the amplitude keys' CG direction (JVP) and the
+// CG update + finalize of the iteration (VJP).
 //
 // Same operator as nft_amp.hip (reference: src/library/correlated_fields.py
 // :105-212 -- _SlopeRemover, _TwoLogIntegrations, _Normalization --, and the
 // scalings of correlated_fields_simple.py:86-127), linearised at one
-// expansion point.  The JVP / VJP are linear in the tangent / cotangent; the
-// two cumulative sums of the integrated Wiener process and the normalisation
-// make every bin depend on global quantities (scan carries of earlier / later
-// bins, the slope remover's last value T, the normalisation sums), all of them
-// LINEAR in the tangent.  The bins are cut into tiles; then
+// expansion point.  The JVP / VJP are linear in the tangent / cotangent, and
+// every global quantity they need -- the two scan carries of each tile, the
+// slope-remover's last value T, the normalisation sums dS / R1 / R3 -- enters
+// LINEARLY.  So each workgroup (one scan tile of E*256 bins, all K right-hand
+// sides of its group) first computes everything tile-local: local scans
+// without carries, and the handful of per-tile sums the carries and globals
+// are made of (phase A, first launch); the second launch combines them in a
+// fixed order over the tiles and redoes the tile-local scans to form the
+// outputs (phase B):
 //
-//   JVP   c_j  = loc1_j + C1(i)                       C1(i) = sum_{t<i} a1(t)
-//         tl_j = loc2_j + C1(i) LVc_j + C2(i)         C2(i) = sum_{t<i} a2(t) + C1(t) LVt(t)
-//         dS   = sum_t m1(t) + C2(t) MS2(t) + C1(t) MS3(t)  + ssl KV + sflex KF + sasp KA - T M4
-//   VJP   y_j  = yG_j - k ym_j + beta(i)              beta(i) = SG(i) - k SM(i) - R3
+//   JVP   c_j  = loc1_j + C1(i)                       C1(i) = sum_{t<i} agg1(t)
+//         tl_j = loc2_j + C1(i) LVc_j + C2(i)         C2(i) = sum_{t<i} agg2(t) + C1(t) LVt(t)
+//         dS   = sum_t MS1(t) + C2(t) MS2(t) + C1(t) MS3(t) - T MS4
+//   VJP   gapre_b = G_b - k mspec_b,  k = fl R1 / (2 S),  R3 = R3G - k R3m
+//         y_j  = yG_j - k ym_j + beta(i)              beta(i) = SG(i) - k SM(i) - R3
 //         g1_j = g1G_j - k g1m_j + beta(i) g1l_j + S1(i)
 //
-// (loc*, yG, g1G: tile-local scans of the tangent / cotangent).  Everything
-// that involves the expansion point alone -- the constant scans ym, g1m, g1l,
-// LVc, the constant tile sums MS2, MS3, AWM, ... and the global sums M4, KV,
-// KF, KA -- is formed ONCE per linearisation point (nft_amp2_prepare, tables
-// at nft_amp_const.tab), and every tile sum the carries need from the
-// tangent is a DOT PRODUCT of the tangent with a constant vector ("sum_j y_j
-// c_j" with y a tile-local reverse scan of G is "sum_j G_j F(c)_j" with F(c)
-// the tile-local forward scan of c, and vice versa):
-//
-//   a1 = d1.sf      a2 = d0.c0 + d1.ka      m1 = d0.(c0 RM) + d1.kb      (JVP)
-//   aggG = G.1   AWG = G.k1   P0G = G.k2   Q2G = G.k3   P1G = G.k4        (VJP)
-//
-// so the first launch of each (phase A) is a pure streaming pass: no scans,
-// one workgroup per tile for a group of right-hand sides that share constants
-// (the constants are read once and held once in registers); the last
-// workgroup of a group to finish forms the carries of every tile (fixed-order
-// scans over the tile sums).  The second launch (phase B) reads its tile's
-// carries, redoes the tile-local scans of the tangent / cotangent and writes
-// the outputs (the VJP's: the CG update, and in the last workgroup of a group
-// the CG finalize).  All sums are fixed-order, so results are deterministic
-// and, per right-hand side, independent of how many share the launch.
-//
-// Concurrency: the finalize's arrival counters are one device-global set, so
-// these kernels must not run concurrently on two streams (the library's
-// contract: one stream per device, include/nifty_amd.h).
+// (loc*, yG, ym, g1*: tile-local scans; SG, SM, S1: sums over the tiles after
+// i).  Against the ten stream-ordered kernels of nft_amp.hip (four for the
+// JVP, six for the VJP, each a full pass per RHS over B-sized intermediates)
+// this reads the per-bin constants once for the K right-hand sides of a
+// workgroup, writes one B-sized intermediate (the JVP's pre-slope values) and
+// takes one kernel boundary per JVP / VJP.  A grid barrier in place of that
+// boundary would need the whole problem resident in registers at once
+// (measured: ~40 VGPRs per bin and RHS, beyond the 256 CUs at C3's 4 x 313k
+// bins), so phase B re-derives the tile-local scans from its inputs instead
+// (bitwise the values of phase A).  All sums are fixed-order (tile-local
+// striped scans, then scans / totals over the tiles in index order), so
+// results are deterministic and, per right-hand side, independent of how many
+// share the launch.
 #include <algorithm>
 #include <cstdlib>
 
@@ -51,85 +45,48 @@ namespace nft {
 namespace amp2 {
 
 using AmpConst = nft_amp_const;
-constexpr int NT = 512;   // threads per workgroup, one bin per thread per sub-chunk
+constexpr int NT = 256;
 constexpr int NW = NT / 64;
-constexpr int MAXNB = 640;  // tiles per right-hand side at most: the tile grows with B
-constexpr int MAXR = 256;   // right-hand sides per launch
+constexpr int E = 4;  // bins per thread: tile = E * 256 bins, whatever the batch size
+constexpr int TL = E * NT;
+constexpr int MAXR = 256;     // right-hand sides per launch (per-RHS arrival counters)
 constexpr int NS_ = NFT_CG_NSCALARS;
-constexpr int TPT = (MAXNB + NT - 1) / NT;  // tiles per thread in the carry scans
 
 enum { KFL = 0, KSL = 1, KFLEX = 2, KASP = 3, KZM = 4, KSPEC = 5 };
 
-// ---------------------------------------------------------------- tables
-// per-bin tables (M each, padded): JVP ka, c0RM, kb, LVc; VJP k1..k4, ym, g1m, g1l
-enum { T_KA = 0, T_C0RM, T_KB, T_LVC, T_K1, T_K2, T_K3, T_K4, T_YM, T_G1M, T_G1L, T_N };
-// constant tile rows (nb each, padded); P*: per-tile partials of the globals
-enum { R_LVT = 0, R_MS2, R_MS3, R_AWM, R_AWL, R_P0M, R_P0S, R_Q2M, R_Q2L, R_P2S, R_P1M, R_P1S, R_SM, R_PM4, R_PKV,
-       R_PKF, R_PKA, R_N };
-// globals: M4 = sum msv sc, KV = sum msv vslope, KF = sum msv Qf, KA = sum msv Qa (all bins)
-enum { G_M4 = 0, G_KV, G_KF, G_KA, G_N = 8 };
-
-struct Geo {
-  int M, sub, nb;         // spectrum bins, sub-chunks per tile, tiles
-  long long Mp, nbp;      // padded strides
-  __host__ __device__ long long tl() const { return (long long)sub * NT; }
-};
-__host__ __device__ inline Geo geo_of(long long B) {
-  Geo g;
-  const long long M = B - 2 > 0 ? B - 2 : 1;
-  int s = 1;
-  while ((M + (long long)s * NT - 1) / ((long long)s * NT) > MAXNB) s *= 2;
-  g.M = (int)(B - 2);
-  g.sub = s;
-  g.nb = (int)((M + (long long)s * NT - 1) / ((long long)s * NT));
-  g.Mp = (M + 63) & ~63LL;
-  g.nbp = ((long long)g.nb + 63) & ~63LL;
-  return g;
-}
-__host__ __device__ inline long long tab_len(const Geo& g) { return (long long)T_N * g.Mp + (long long)R_N * g.nbp + G_N; }
-__device__ __forceinline__ const double* tabv(const double* t, const Geo& g, int q) { return t + (long long)q * g.Mp; }
-__device__ __forceinline__ const double* tabr(const double* t, const Geo& g, int q) {
-  return t + (long long)T_N * g.Mp + (long long)q * g.nbp;
-}
-__device__ __forceinline__ const double* tabg(const double* t, const Geo& g) {
-  return t + (long long)T_N * g.Mp + (long long)R_N * g.nbp;
-}
-
-// the per-bin arrays are read through pointers loaded from a struct: cast
-// them to the global address space (else flat loads, waited on with LDS)
+// the per-bin constants are read through pointers loaded from a struct (the
+// device constant sets): cast them to the global address space, or every
+// read is a flat load waited on with the LDS traffic
 typedef __attribute__((address_space(1))) const double gdouble;
 __device__ __forceinline__ gdouble* G_(const double* p) { return (gdouble*)p; }
 
-// constant sets: by value (kernel argument) or from device memory through
-// the constant address space (pointers land in SGPRs)
-typedef __attribute__((address_space(4))) const unsigned long long cword;
-static_assert(sizeof(AmpConst) % 8 == 0, "nft_amp_const is read as 64-bit words");
-__device__ __forceinline__ AmpConst load_const(const AmpConst* p) {
-  AmpConst v;
-  unsigned long long* d = (unsigned long long*)&v;
-  cword* q = (cword*)p;
-#pragma unroll
-  for (int k = 0; k < (int)(sizeof(AmpConst) / 8); ++k) d[k] = q[k];
-  return v;
+// device-coherent scalar access for the values exchanged between workgroups
+__device__ __forceinline__ double cld(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// MODE 0: the host set (argument); 1: one device set per RHS; 2: one device set for all
-template <int MODE>
-__device__ __forceinline__ AmpConst const_of(const AmpConst& c, const AmpConst* dcs, const AmpConst* dc1, int r) {
-  if constexpr (MODE == 1) return load_const(dcs + r);
-  else if constexpr (MODE == 2) return load_const(dc1);
-  else return c;
+__device__ __forceinline__ void cst(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------ block helpers
-// NV block totals at once: per value the wave tree, then the waves in order
-// (value by value, so that the tree needs one temporary)
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+// NV block totals at once; per value the wave tree and the waves in order
 template <int NV>
 __device__ __forceinline__ void btot(double (&v)[NV], double* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave trees of the NV values step by step (one LDS round trip per step)
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
+  for (int off = 32; off > 0; off >>= 1) {
+    double y[NV];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_down(v[k], off, 64);
+    for (int k = 0; k < NV; ++k) y[k] = __shfl_down(v[k], off, 64);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += y[k];
   }
   __syncthreads();
   if (lane == 0) {
@@ -147,134 +104,112 @@ __device__ __forceinline__ void btot(double (&v)[NV], double* sh) {
   __syncthreads();
 }
 
-// NV block totals into LDS: after the call, total k is at sh[NV * NW + k]
-// (thread k sums the wave totals of value k in wave order; nobody holds all
-// NV * NW partials in registers).  sh: NV * (NW + 1) doubles.
-template <int NV>
-__device__ __forceinline__ void btot_sh(double (&v)[NV], double* sh) {
+// inclusive scans of NA independent arrays of EE values per thread in
+// STRIPED layout (v[a][e] is element e*NT + tid: every global access of a
+// tile is one coalesced run per e), forward or reversed: wave scans by
+// shuffles -- all NA*EE of a step issued together, one LDS round trip per
+// step --, then per element the fixed-order sum of the preceding (following)
+// wave segments, segment (e, w) in the order e*NW + w.  One barrier pair.
+// tot[a]: totals.
+template <int NA, int EE, bool REV>
+__device__ __forceinline__ void scan_arr(double (&v)[NA][EE], double (&tot)[NA], double* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_down(v[k], off, 64);
-  }
-  __syncthreads();
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) sh[k * NW + w] = v[k];
-  }
-  __syncthreads();
-  if (threadIdx.x < NV) {
-    const int k = threadIdx.x;
-    double t = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) t += sh[k * NW + i];
-    sh[NV * NW + k] = t;
-  }
-  __syncthreads();
-}
-
-// inclusive block scans of NA arrays (one value per thread, thread order),
-// forward or reversed: wave scans by shuffles; then thread (a, w) forms the
-// fixed-order sum of the waves before (after) wave w for array a, so every
-// thread reads one offset per array.  tot: the block totals.  sh: NA (2 NW
-// + 1) doubles.
-template <int NA, bool REV>
-__device__ __forceinline__ void bscan(double (&v)[NA], double (&tot)[NA], double* sh) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int NSEG = EE * NW;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    double y[NA];
+    double y[NA][EE];
 #pragma unroll
-    for (int a = 0; a < NA; ++a) y[a] = REV ? __shfl_down(v[a], off, 64) : __shfl_up(v[a], off, 64);
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int e = 0; e < EE; ++e) y[a][e] = REV ? __shfl_down(v[a][e], off, 64) : __shfl_up(v[a][e], off, 64);
     const bool take = REV ? (lane + off < 64) : (lane >= off);
 #pragma unroll
     for (int a = 0; a < NA; ++a)
-      if (take) v[a] += y[a];
+#pragma unroll
+      for (int e = 0; e < EE; ++e)
+        if (take) v[a][e] += y[a][e];
   }
   if (lane == (REV ? 0 : 63)) {
 #pragma unroll
-    for (int a = 0; a < NA; ++a) sh[a * NW + w] = v[a];
-  }
-  __syncthreads();
-  if (threadIdx.x < NA * NW) {
-    const int a = threadIdx.x / NW, w2 = threadIdx.x - a * NW;
-    double off = 0.0, run = 0.0;
-    if (!REV) {
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        if (q < w2) off += sh[a * NW + q];
-        run += sh[a * NW + q];
-      }
-    } else {
-#pragma unroll
-      for (int q = NW - 1; q >= 0; --q) {
-        if (q > w2) off += sh[a * NW + q];
-        run += sh[a * NW + q];
-      }
-    }
-    sh[NA * NW + a * NW + w2] = off;
-    if (w2 == 0) sh[2 * NA * NW + a] = run;
+      for (int e = 0; e < EE; ++e) sh[a * NSEG + e * NW + w] = v[a][e];
   }
   __syncthreads();
 #pragma unroll
   for (int a = 0; a < NA; ++a) {
-    v[a] += sh[NA * NW + a * NW + w];
-    tot[a] = sh[2 * NA * NW + a];
+    const double* s = sh + a * NSEG;
+    double run = 0.0;  // the segments of the elements before (after) e
+    if (!REV) {
+#pragma unroll
+      for (int e = 0; e < EE; ++e) {
+        double off = run;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          if (q < w) off += s[e * NW + q];
+          run += s[e * NW + q];
+        }
+        v[a][e] += off;
+      }
+    } else {
+#pragma unroll
+      for (int e = EE - 1; e >= 0; --e) {
+        double off = run;
+#pragma unroll
+        for (int q = NW - 1; q >= 0; --q) {
+          if (q > w) off += s[e * NW + q];
+          run += s[e * NW + q];
+        }
+        v[a][e] += off;
+      }
+    }
+    tot[a] = run;
   }
   __syncthreads();
 }
 
-// exclusive scans over the tiles (nb <= MAXNB values, TPT per thread in
-// chunks of NT, thread order within a chunk), forward or reversed, of NA rows
-// at once; x[a][c] is tile c * NT + tid (0 past nb)
-template <int NA, bool REV>
-__device__ __forceinline__ void tile_scan(const double (&x)[NA][TPT], double (&ex)[NA][TPT], double (&tot)[NA],
-                                          double* sh) {
-  double run[NA];
-#pragma unroll
-  for (int a = 0; a < NA; ++a) run[a] = 0.0;
-#pragma unroll
-  for (int cc = 0; cc < TPT; ++cc) {
-    const int c = REV ? TPT - 1 - cc : cc;
-    double v[NA], t[NA];
-#pragma unroll
-    for (int a = 0; a < NA; ++a) v[a] = x[a][c];
-    bscan<NA, REV>(v, t, sh);
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      ex[a][c] = run[a] + (v[a] - x[a][c]);
-      run[a] += t[a];
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < NA; ++a) tot[a] = run[a];
-}
-
 // ------------------------------------------------------------ arrival
-// Arrival counters of the VJP's finalize (per group of right-hand sides):
-// arrival i of n counts at group counter i % 16, the last arrival of a group
-// at the top counter (hundreds of atomics on one address serialise at the
-// memory-side atomic unit, sixteen lines do not); each counter is reset by
-// the arrival that completes it.  Release / acquire at agent scope: the
-// partials a workgroup stored before it arrives are visible to the last one.
+// Per-RHS arrival counters of the first launches (the last workgroup of a
+// RHS forms that RHS's tile carries) and the grid counter of the VJP's second
+// launch (its last workgroup runs the CG finalize).  Hierarchical: arrival i
+// of n counts at group counter i % 16, the last arrival of a group at the top
+// counter -- a few hundred atomics on ONE address serialise at the memory-side
+// atomic unit (tens of microseconds), sixteen lines do not.  Each counter is
+// reset by the arrival that completes it.
+//
+// Hand-over between the workgroups of ONE launch: the values the last
+// arrival reads are written with device-coherent stores (cst: agent-scope
+// atomic stores, written through the XCD's L2) and read with device-coherent
+// loads (cld: they bypass the reader's L2, which may hold lines of the
+// previous launch), and every thread waits for its stores (s_waitcnt) before
+// its workgroup's counter increment.  Agent-scope release / acquire fences
+// would formally order plain stores instead, but on gfx950 an agent-scope
+// release writes back the whole XCD L2 (the eight L2s are not coherent with
+// each other): one write-back per workgroup measured 2-3x slower here
+// (round 4: a VJP first launch 36 -> 131 us, second 116 -> 210 us at C3).
+// Values handed to a LATER launch need neither (kernel boundaries write back
+// and invalidate the L2s).  The counters are one device-global set: these
+// kernels must not run concurrently on two streams (nifty_amd.h).
 constexpr int NGRP = 16;
 struct Line {
   unsigned v[16];  // one 64-byte line per counter
 };
-__device__ Line g_arrive[3][MAXR][NGRP + 1];  // jvp_a, vjp_a, vjp_b
+__device__ Line g_arrive[3][MAXR][NGRP + 1];
 
+// true in exactly one of the n workgroups (arrival index idx) that call it
+// with the same counter set, after every caller's device-coherent stores
+// before the call are complete
 __device__ __forceinline__ bool last_arrival(Line* ctr, int idx, int n, int* lds_flag) {
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const int ng = n < NGRP ? n : NGRP;
     const int q = idx % ng;
     const unsigned gsz = (unsigned)(n / ng + (q < n % ng ? 1 : 0));
     bool last = false;
-    if (__hip_atomic_fetch_add(&ctr[q].v[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gsz - 1) {
+    if (__hip_atomic_fetch_add(&ctr[q].v[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsz - 1) {
       __hip_atomic_store(&ctr[q].v[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (__hip_atomic_fetch_add(&ctr[NGRP].v[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+      if (__hip_atomic_fetch_add(&ctr[NGRP].v[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
           (unsigned)ng - 1) {
         __hip_atomic_store(&ctr[NGRP].v[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = true;
@@ -283,10 +218,22 @@ __device__ __forceinline__ bool last_arrival(Line* ctr, int idx, int n, int* lds
     *lds_flag = last ? 1 : 0;
   }
   __syncthreads();
-  const bool last = *lds_flag != 0;
-  if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return last;
+  return *lds_flag != 0;
 }
+
+// Workgroup -> (tile, RHS): a 1-D grid of roundup(nb, 8) * k workgroups in
+// which the k right-hand sides of one tile are consecutive slots of one XCD
+// group (workgroups are dealt round-robin over the 8 XCDs: w and w + 8 share
+// one), so the per-bin constants the RHS share are read from HBM once and
+// from that XCD's L2 after; padding workgroups return at once.
+__device__ __forceinline__ bool place(int nb, int k, int& tile, int& r) {
+  const int w = blockIdx.x, xg = w & 7, slot = w >> 3;
+  const int bl = slot / k;
+  r = slot - bl * k;
+  tile = bl * 8 + xg;
+  return tile < nb;
+}
+static unsigned grid_of(int nb, int k) { return (unsigned)(((nb + 7) & ~7) * k); }
 
 __device__ __forceinline__ double beta_of(const double* scb) {
   double beta = scb[NFT_CG_GAMMA] / scb[NFT_CG_GPREV];
@@ -294,223 +241,37 @@ __device__ __forceinline__ double beta_of(const double* scb) {
   return beta;
 }
 
-// workgroup -> (tile, group of KG right-hand sides); RHS r = g * KG + q
-__device__ __forceinline__ void place(int nb, int& tile, int& grp) {
-  tile = (int)(blockIdx.x % (unsigned)nb);
-  grp = (int)(blockIdx.x / (unsigned)nb);
+// exclusive block scan of Q values per thread (striped: tile t0 + q*NT +
+// tid), forward or reversed, with a running carry across chunks: ex = the
+// exclusive values, run advanced by the chunk total
+template <bool REV, int Q>
+__device__ __forceinline__ void chunk_scan(const double (&x)[Q], double (&ex)[Q], double& run, double* sh) {
+  double v[1][Q], t[1];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) v[0][q] = x[q];
+  scan_arr<1, Q, REV>(v, t, sh);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) ex[q] = run + (v[0][q] - x[q]);
+  run += t[0];
 }
-
-// ================================================================= PREPARE
-struct PrepArgs {
-  AmpConst c;              // host set (item_consts NULL) or B + flags
-  AmpConst* dcs;           // device sets (one per row) or null
-  double* tab;             // row r's tables at tab + r * ts
-  long long ts;
-  int nrow;
-};
-
-// one workgroup per (tile, row): the constant tile-local scans -> tables,
-// the constant tile sums -> rows
-template <bool DEV>
-__global__ __launch_bounds__(NT) void prep_tiles(PrepArgs a) {
-#pragma clang fp contract(off)
-  __shared__ double sh[(R_P1S + 5) * (NW + 1)];
-  const Geo g = geo_of(a.c.B);
-  const int i = (int)(blockIdx.x % (unsigned)g.nb), r = (int)(blockIdx.x / (unsigned)g.nb);
-  const AmpConst c = DEV ? load_const(a.dcs + r) : a.c;
-  double* tab = a.tab + (long long)r * a.ts;
-  const int tid = threadIdx.x;
-  const bool flex = c.has_flex, asp = c.has_asp;
-  const long long j0 = (long long)i * g.tl();
-  auto T = [&](int q) { return tab + (long long)q * g.Mp; };
-  auto R = [&](int q) { return tab + (long long)T_N * g.Mp + (long long)q * g.nbp; };
-  // globals' partials over the tile's bins (+ bins 0, 1 in tile 0)
-  double pg[4] = {0.0, 0.0, 0.0, 0.0};  // msv sc, msv vsl, msv Qf, msv Qa
-  // row sums
-  double rs[R_P1S + 1];
-#pragma unroll
-  for (int q = 0; q <= R_P1S; ++q) rs[q] = 0.0;
-  // forward pass over the sub-chunks: LVc, k1 = F(l1) - l2, k2 = F(p0),
-  // k3 = F(l1 p2c) - l2 p2c with p2c = F(p2), k4 = F(p1)
-  double cf[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // running carries: lv, l1, p2, l1 p2c, p0 (p1 below)
-  double cp1 = 0.0;
-  for (int s = 0; s < g.sub; ++s) {
-    const long long j = j0 + (long long)s * NT + tid;
-    const bool ok = j < g.M;
-    const long long b = j + 2;
-    const double msv = ok ? G_(c.mspec)[b] : 0.0;
-    const double scv = ok ? G_(c.sc)[b] : 0.0;
-    const double vsl = ok ? G_(c.vslope)[b] : 0.0;
-    pg[0] += msv * scv;
-    pg[1] += msv * vsl;
-    if (flex) pg[2] += msv * (ok ? G_(c.Qf)[b] : 0.0);
-    if (asp) pg[3] += msv * (ok ? G_(c.Qa)[b] : 0.0);
-    if (!flex) continue;
-    const bool okf = ok;
-    const double lv = okf ? G_(c.lv)[j] : 0.0;
-    const double lvn = (okf && j + 1 < g.M) ? G_(c.lv)[j + 1] : 0.0;
-    const double l1 = lv / 2. + lvn / 2., l2 = lvn / 2.;
-    const double p0 = okf ? G_(c.p0)[j] : 0.0;
-    const double p1 = (okf && asp) ? G_(c.p1)[j] : 0.0;
-    const double p2 = okf ? G_(c.p2)[j] : 0.0;
-    double v[6] = {lv, l1, p2, 0.0, p0, p1}, t[6];
-    // p2c first (l1 p2c needs it): scan lv, l1, p2, p0, p1 together
-    {
-      double u[5] = {lv, l1, p2, p0, p1}, tu[5];
-      bscan<5, false>(u, tu, sh);
-      v[0] = u[0] + cf[0];
-      v[1] = u[1] + cf[1];
-      v[2] = u[2] + cf[2];
-      v[4] = u[3] + cf[4];
-      v[5] = u[4] + cp1;
-      cf[0] += tu[0];
-      cf[1] += tu[1];
-      cf[2] += tu[2];
-      cf[4] += tu[3];
-      cp1 += tu[4];
-    }
-    const double p2c = v[2];
-    double w3[1] = {l1 * p2c}, t3[1];
-    bscan<1, false>(w3, t3, sh);
-    const double f3 = w3[0] + cf[3];
-    cf[3] += t3[0];
-    (void)t;
-    const double LVc = v[0];
-    const double k1 = v[1] - l2, k2 = v[4], k3 = f3 - l2 * p2c, k4 = v[5];
-    if (ok) {
-      T(T_LVC)[j] = LVc;
-      T(T_K1)[j] = k1;
-      T(T_K2)[j] = k2;
-      T(T_K3)[j] = k3;
-      T(T_K4)[j] = asp ? k4 : 0.0;
-    }
-    rs[R_LVT] += lv;
-    rs[R_MS2] += msv;
-    rs[R_MS3] += msv * LVc;
-    rs[R_AWL] += l1;
-    rs[R_P0M] += msv * k2;
-    rs[R_P0S] += p0;
-    rs[R_Q2M] += msv * k3;
-    rs[R_Q2L] += l1 * p2c;
-    rs[R_P2S] += p2;
-    rs[R_P1M] += msv * (asp ? k4 : 0.0);
-    rs[R_P1S] += p1;
-  }
-  // reverse pass: RL = R(lv), RM = R(msv) = ym, RLM = R(lv RM), g1m = R(RM l1 - msv l2),
-  // g1l = R(l1); ka = sf (RL - lv/2), c0RM = c0 RM, kb = sf (RLM - lv RM/2); AWM
-  if (flex) {
-    double cr[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // lv, msv, lv RM, w(msv), l1
-    for (int s = g.sub - 1; s >= 0; --s) {
-      const long long j = j0 + (long long)s * NT + tid;
-      const bool ok = j < g.M;
-      const long long b = j + 2;
-      const double msv = ok ? G_(c.mspec)[b] : 0.0;
-      const double lv = ok ? G_(c.lv)[j] : 0.0;
-      const double lvn = (ok && j + 1 < g.M) ? G_(c.lv)[j + 1] : 0.0;
-      const double l1 = lv / 2. + lvn / 2., l2 = lvn / 2.;
-      const double sf = ok ? G_(c.sf)[j] : 0.0, c0 = ok ? G_(c.c0)[j] : 0.0;
-      double u[3] = {lv, msv, l1}, tu[3];
-      bscan<3, true>(u, tu, sh);
-      const double RL = u[0] + cr[0], RM = u[1] + cr[1], G1L = u[2] + cr[4];
-      cr[0] += tu[0];
-      cr[1] += tu[1];
-      cr[4] += tu[2];
-      const double wm = RM * l1 - msv * l2;
-      double u2[2] = {lv * RM, wm}, tu2[2];
-      bscan<2, true>(u2, tu2, sh);
-      const double RLM = u2[0] + cr[2], G1M = u2[1] + cr[3];
-      cr[2] += tu2[0];
-      cr[3] += tu2[1];
-      if (ok) {
-        T(T_KA)[j] = sf * (RL - lv / 2.);
-        T(T_C0RM)[j] = c0 * RM;
-        T(T_KB)[j] = sf * (RLM - lv * RM / 2.);
-        T(T_YM)[j] = RM;
-        T(T_G1M)[j] = G1M;
-        T(T_G1L)[j] = G1L;
-      }
-      rs[R_AWM] += wm;
-    }
-  }
-  if (i == 0 && tid < 2) {  // bins 0 and 1: no integrated part
-    const int b = tid;
-    const double ms = G_(c.mspec)[b];
-    pg[0] += ms * G_(c.sc)[b];
-    pg[1] += ms * G_(c.vslope)[b];
-    if (flex) pg[2] += ms * G_(c.Qf)[b];
-    if (asp) pg[3] += ms * G_(c.Qa)[b];
-  }
-  double all[R_P1S + 1 + 4];
-#pragma unroll
-  for (int q = 0; q <= R_P1S; ++q) all[q] = rs[q];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) all[R_P1S + 1 + q] = pg[q];
-  constexpr int NA = R_P1S + 1 + 4;
-  btot_sh<NA>(all, sh);
-  if (tid == 0) {
-    const double* tot = sh + NA * NW;
-#pragma unroll
-    for (int q = 0; q <= R_P1S; ++q) R(q)[i] = tot[q];
-    R(R_PM4)[i] = tot[R_P1S + 1];
-    R(R_PKV)[i] = tot[R_P1S + 2];
-    R(R_PKF)[i] = tot[R_P1S + 3];
-    R(R_PKA)[i] = tot[R_P1S + 4];
-  }
-}
-
-// one workgroup per row: SM (exclusive suffix of MS2 over the tiles) and the
-// globals (fixed-order sums of the tile partials); sets the row's tab pointer
-template <bool DEV>
-__global__ __launch_bounds__(NT) void prep_globals(PrepArgs a) {
-#pragma clang fp contract(off)
-  __shared__ double sh[8 * NW];
-  const Geo g = geo_of(a.c.B);
-  const int r = blockIdx.x;
-  double* tab = a.tab + (long long)r * a.ts;
-  auto R = [&](int q) { return tab + (long long)T_N * g.Mp + (long long)q * g.nbp; };
-  const int tid = threadIdx.x;
-  double x[1][TPT], ex[1][TPT], tot[1];
-  double p[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int cc = 0; cc < TPT; ++cc) {
-    const int t = cc * NT + tid;
-    const bool ok = t < g.nb;
-    x[0][cc] = ok ? R(R_MS2)[t] : 0.0;
-    p[0] += ok ? R(R_PM4)[t] : 0.0;
-    p[1] += ok ? R(R_PKV)[t] : 0.0;
-    p[2] += ok ? R(R_PKF)[t] : 0.0;
-    p[3] += ok ? R(R_PKA)[t] : 0.0;
-  }
-  tile_scan<1, true>(x, ex, tot, sh);
-#pragma unroll
-  for (int cc = 0; cc < TPT; ++cc) {
-    const int t = cc * NT + tid;
-    if (t < g.nb) R(R_SM)[t] = ex[0][cc];
-  }
-  btot<4>(p, sh);
-  if (tid == 0) {
-    double* gl = tab + (long long)T_N * g.Mp + (long long)R_N * g.nbp;
-    gl[G_M4] = p[0];
-    gl[G_KV] = p[1];
-    gl[G_KF] = p[2];
-    gl[G_KA] = p[3];
-    if (DEV) a.dcs[r].tab = tab;
-  }
-}
+constexpr int CQ = 2;  // tiles per thread in the carry scans (chunks of 512 tiles)
 
 // ======================================================================= JVP
-struct JvpArgs {
+// VT: storage of the latent vectors, da and g (double, or float for the
+// fp32-storage CG); constants, workspace, sums and CG scalars stay double
+template <typename VT>
+struct Jvp2Args {
   AmpConst c;              // constants (shared by every RHS), B and flags
   const AmpConst* dcs;     // per-RHS constants (device) or null
   const AmpConst* dc1;     // one device constant set shared by every RHS, or null
-  double* t[6];            // tangent keys of RHS 0 (rows ls apart); with dir the CG direction, updated in place
-  const double* r[6];      // residual keys of RHS 0 (dir only)
+  VT* t[6];                // tangent keys of RHS 0 (rows ls apart); with dir the CG direction, updated in place
+  const VT* r[6];          // residual keys of RHS 0 (dir only)
   long long ls;
-  double* da;              // da[r * vs + b * des]
+  VT* da;                  // da[r * vs + b * des]
   long long vs, des;
   double* ws;              // per-RHS workspace, wsd doubles apart
   long long wsd;
-  int nrhs;
+  int nrhs, nb;
   int dir;                 // carry d = max(0, gamma/gprev) d + r on the amplitude keys
   const double* sc;        // CG scalar blocks (dir)
   double* part;            // d.d partials: part[r * pstride + tile] = shift * d.d (dir)
@@ -518,315 +279,308 @@ struct JvpArgs {
   double shift;
 };
 
-// workspace rows of one RHS (JVP): a1, a2, m1 (phase A) and the carries C1,
-// C2 (phase A's last workgroup) [nbp each], then the scalars: the scalar
-// keys' tangents after the direction update [5], T, ds
-enum { W_A1 = 0, W_A2, W_M1, W_C1, W_C2, W_JN };
-enum { J_T = 5, J_DS = 6 };
-__device__ __forceinline__ double* wrow(double* W, const Geo& g, int q) { return W + (long long)q * g.nbp; }
+// workspace of one RHS: Eh [M, padded], the tile sums (7 rows of nb: agg1,
+// agg2, MS1, LVt, MS2, MS3, MS4), 8 scalars (the 5 tangents after the
+// direction update), the carries C1 [nb], C2 [nb], then T, dS
+struct JWs {
+  long long rows, scal, c1, c2, glb;
+};
+__device__ __host__ __forceinline__ JWs jws(int M, int nb) {
+  JWs w;
+  w.rows = ((long long)M + 63) & ~63LL;
+  w.scal = w.rows + 7LL * nb;
+  w.c1 = w.scal + 8;
+  w.c2 = w.c1 + nb;
+  w.glb = w.c2 + nb;
+  return w;
+}
 
-// phase A: direction update and the tile's dot products a1, a2, m1 for each
-// RHS of the group (+ tile 0: the scalar keys, stashed in the workspace)
-template <int MODE, int KG>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void jvp_a(JvpArgs a) {
-#pragma clang fp contract(off)
-  __shared__ double sh[(4 * KG) * (NW + 1)];
+// the constant set of RHS r by item mode (a template parameter, so that a
+// device set is read with scalar loads from the constant address space: its
+// pointers land in SGPRs and the per-bin loads wait on nothing)
+typedef __attribute__((address_space(4))) const unsigned long long cword;
+static_assert(sizeof(AmpConst) % 8 == 0, "nft_amp_const is read as 64-bit words");
+__device__ __forceinline__ AmpConst load_const(const AmpConst* p) {
+  AmpConst v;
+  unsigned long long* d = (unsigned long long*)&v;
+  cword* q = (cword*)p;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(AmpConst) / 8); ++k) d[k] = q[k];
+  return v;
+}
+template <int MODE>
+__device__ __forceinline__ AmpConst const_of(const AmpConst& c, const AmpConst* dcs, const AmpConst* dc1, int r) {
+  if constexpr (MODE == 1) return load_const(dcs + r);
+  else if constexpr (MODE == 2) return load_const(dc1);
+  else return c;
+}
+
+// first launch: direction update, tile-local scans, Eh, the tile sums; the
+// last workgroup of each RHS then forms that RHS's tile carries
+template <typename VT, int MODE>
+__global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
+  __shared__ double sh[2 * E * NW + 8 * NW];
   __shared__ int lflag;
-  const Geo g = geo_of(a.c.B);
-  int i, grp;
-  place(g.nb, i, grp);
+  int i, r;
+  if (!place(a.nb, a.nrhs, i, r)) return;
   const int tid = threadIdx.x;
-  const AmpConst c = const_of<MODE>(a.c, a.dcs, a.dc1, grp * KG);
+  const AmpConst c = const_of<MODE>(a.c, a.dcs, a.dc1, r);  // by value: loaded once, no aliasing with the stores
+  const int M = (int)(a.c.B - 2);
   const bool flex = a.c.has_flex, asp = a.c.has_asp;
-  const double* tb = c.tab;
-  if (!tb) return;  // constants without tables (nft_amp2_prepare not run): no access
-  double bt[KG];
-  bool live[KG], upd[KG], has[KG];
-#pragma unroll
-  for (int q = 0; q < KG; ++q) {
-    const int r = grp * KG + q;
-    has[q] = r < a.nrhs;
-    bt[q] = 0.0;
-    live[q] = false;
-    if (a.dir && has[q]) {
-      const double* scb = a.sc + (long long)r * NS_;
-      live[q] = scb[NFT_CG_DONE] == 0.0;
-      bt[q] = beta_of(scb);
-    }
-    upd[q] = a.dir && live[q];
+  const int nb = a.nb;
+  const int j0 = i * TL + tid;  // striped: bin j0 + e * NT
+  const long long ro = (long long)r * a.ls;
+  double* __restrict__ W = a.ws + (long long)r * a.wsd;
+  const JWs L = jws(M, nb);
+  bool live = false;
+  double bt = 0.0;
+  if (a.dir) {
+    const double* scb = a.sc + (long long)r * NS_;
+    live = scb[NFT_CG_DONE] == 0.0;
+    bt = beta_of(scb);
   }
-  // a1, a2, m1, dd per RHS
-  double s[4 * KG];
+  const bool upd = a.dir && live;
+  // every load of the phase first (the direction's stores cannot be passed)
+  double sv[5];
 #pragma unroll
-  for (int k = 0; k < 4 * KG; ++k) s[k] = 0.0;
+  for (int q = 0; q < 5; ++q) {
+    sv[q] = 0.0;
+    if (!a.t[q] || (q == KFLEX && !flex) || (q == KASP && !asp) || (q == KZM && !c.has_zm)) continue;
+    sv[q] = a.t[q][ro];
+    if (upd) sv[q] = bt * sv[q] + a.r[q][ro];
+  }
+  double d0[E], d1[E], r0[E], r1[E], lvv[E], c0v[E], sfv[E], vsl[E], qf[E], qa[E], msv[E], scv[E];
+  VT* __restrict__ ts = a.t[KSPEC] ? a.t[KSPEC] + ro : nullptr;
+  const VT* __restrict__ rs = (upd && a.r[KSPEC]) ? a.r[KSPEC] + ro : nullptr;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    const bool ok = j < M;
+    const int b = j + 2;
+    const bool okf = ok && flex;
+    d0[e] = okf ? ts[j] : 0.0;
+    d1[e] = okf ? ts[M + j] : 0.0;
+    r0[e] = (okf && rs) ? rs[j] : 0.0;
+    r1[e] = (okf && rs) ? rs[M + j] : 0.0;
+    lvv[e] = okf ? G_(c.lv)[j] : 0.0;
+    c0v[e] = okf ? G_(c.c0)[j] : 0.0;
+    sfv[e] = okf ? G_(c.sf)[j] : 0.0;
+    vsl[e] = ok ? G_(c.vslope)[b] : 0.0;
+    qf[e] = okf ? G_(c.Qf)[b] : 0.0;
+    qa[e] = (ok && asp) ? G_(c.Qa)[b] : 0.0;
+    msv[e] = ok ? G_(c.mspec)[b] : 0.0;
+    scv[e] = ok ? G_(c.sc)[b] : 0.0;
+  }
+  double dd = 0.0;
+  double u[1][E], th[2][E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    if (rs && j < M) {
+      d0[e] = bt * d0[e] + r0[e];
+      d1[e] = bt * d1[e] + r1[e];
+      ts[j] = d0[e];
+      ts[M + j] = d1[e];
+      dd += d0[e] * d0[e] + d1[e] * d1[e];
+    }
+    // t = (c + c_prev)/2 lv + t0 c0 with c_prev = c - u (amp_jvp_3) is
+    // loc1 lv + pre on the carry-free local scan loc1
+    u[0][e] = d1[e] * sfv[e];
+    th[0][e] = d0[e] * c0v[e] - u[0][e] / 2 * lvv[e];
+    th[1][e] = lvv[e];
+  }
+  double agg1 = 0.0, agg2 = 0.0, LVt = 0.0;
   if (flex) {
-    const long long j0 = (long long)i * g.tl();
-    for (int sc_ = 0; sc_ < g.sub; ++sc_) {
-      const long long j = j0 + (long long)sc_ * NT + tid;
-      const bool ok = j < g.M;
-      double sf = 0, c0 = 0, ka = 0, c0rm = 0, kb = 0;
-      if (ok) {
-        sf = G_(c.sf)[j];
-        c0 = G_(c.c0)[j];
-        ka = G_(tabv(tb, g, T_KA))[j];
-        c0rm = G_(tabv(tb, g, T_C0RM))[j];
-        kb = G_(tabv(tb, g, T_KB))[j];
-      }
-      double d0[KG], d1[KG], r0[KG], r1[KG];
+    double t1[1], t2[2];
+    scan_arr<1, E, false>(u, t1, sh);  // u -> loc1
+    agg1 = t1[0];
 #pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        const long long ro = (long long)(grp * KG + q) * a.ls;
-        const bool okq = ok && has[q];
-        d0[q] = okq ? a.t[KSPEC][ro + j] : 0.0;
-        d1[q] = okq ? a.t[KSPEC][ro + g.M + j] : 0.0;
-        r0[q] = (okq && upd[q]) ? a.r[KSPEC][ro + j] : 0.0;
-        r1[q] = (okq && upd[q]) ? a.r[KSPEC][ro + g.M + j] : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        if (ok && upd[q] && has[q]) {
-          const long long ro = (long long)(grp * KG + q) * a.ls;
-          d0[q] = bt[q] * d0[q] + r0[q];
-          d1[q] = bt[q] * d1[q] + r1[q];
-          a.t[KSPEC][ro + j] = d0[q];
-          a.t[KSPEC][ro + g.M + j] = d1[q];
-          s[4 * q + 3] += d0[q] * d0[q] + d1[q] * d1[q];
-        }
-        s[4 * q + 0] += d1[q] * sf;
-        s[4 * q + 1] += d0[q] * c0 + d1[q] * ka;
-        s[4 * q + 2] += d0[q] * c0rm + d1[q] * kb;
-      }
-    }
+    for (int e = 0; e < E; ++e) th[0][e] += u[0][e] * lvv[e];
+    scan_arr<2, E, false>(th, t2, sh);  // -> loc2, LVc
+    agg2 = t2[0];
+    LVt = t2[1];
   }
-  btot_sh<4 * KG>(s, sh);
-  const double* tot = sh + 4 * KG * NW;
+  // Eh = vslope ssl + loc2 + sf Qf + sa Qa (stored); tile sums MS1..MS4, d.d
+  const double ssl = c.sig_s * sv[KSL];
+  double s[5] = {0.0, 0.0, 0.0, 0.0, dd};
 #pragma unroll
-  for (int q = 0; q < KG; ++q) if (tid == q) {
-    const int r = grp * KG + q;
-    if (has[q]) {
-      double* W = a.ws + (long long)r * a.wsd;
-      wrow(W, g, W_A1)[i] = tot[4 * q + 0];
-      wrow(W, g, W_A2)[i] = tot[4 * q + 1];
-      wrow(W, g, W_M1)[i] = tot[4 * q + 2];
-      double v = tot[4 * q + 3];
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    if (j >= M) continue;
+    double d = vsl[e] * ssl + (flex ? th[0][e] : 0.0);
+    if (flex) d += sv[KFLEX] * qf[e];
+    if (asp) d += sv[KASP] * qa[e];
+    W[j] = d;
+    s[0] += msv[e] * d;
+    s[1] += msv[e];
+    s[2] += msv[e] * (flex ? th[1][e] : 0.0);
+    s[3] += msv[e] * scv[e];
+  }
+  if (i == 0 && tid < 2) {  // bins 0 and 1: no integrated part
+    const int b = tid;
+    const double ms = G_(c.mspec)[b];
+    double d = G_(c.vslope)[b] * ssl;
+    if (flex) d += sv[KFLEX] * G_(c.Qf)[b];
+    if (asp) d += sv[KASP] * G_(c.Qa)[b];
+    s[0] += ms * d;
+    s[3] += ms * G_(c.sc)[b];
+  }
+  btot<5>(s, sh);
+  if (tid == 0) {
+    double* R = W + L.rows;
+    cst(R + 0 * nb + i, agg1);
+    cst(R + 1 * nb + i, agg2);
+    cst(R + 2 * nb + i, s[0]);
+    cst(R + 3 * nb + i, LVt);
+    cst(R + 4 * nb + i, s[1]);
+    cst(R + 5 * nb + i, s[2]);
+    cst(R + 6 * nb + i, s[3]);
+    if (i == 0) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) W[L.scal + q] = sv[q];
+    }
+    if (a.dir) {
+      double v = s[4];
       if (i == 0) {
-        // the scalar keys: new direction stashed (phase B writes it back: the
-        // other workgroups of this launch still read the old one)
-        const long long ro = (long long)r * a.ls;
-        double* stash = wrow(W, g, W_JN);
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          double sv = 0.0;
-          if (a.t[k] && !(k == KFLEX && !flex) && !(k == KASP && !asp) && !(k == KZM && !a.c.has_zm)) {
-            sv = a.t[k][ro];
-            if (upd[q]) sv = bt[q] * sv + a.r[k][ro];
-          }
-          stash[k] = sv;
-          if (a.dir) v += sv * sv;
-        }
+        for (int q = 0; q < 5; ++q) v += sv[q] * sv[q];
       }
-      if (a.dir) a.part[(long long)r * a.pstride + i] = live[q] ? a.shift * v : 0.0;
+      a.part[(long long)r * a.pstride + i] = live ? a.shift * v : 0.0;
     }
   }
-  // the carries of every tile (the group's last workgroup): C1 = exclusive
-  // scan of a1, C2 = exclusive scan of a2 + C1 LVt, T = its total, ds = sum
-  // m1 + C2 MS2 + C1 MS3; right-hand sides one after the other
-  if (!flex) return;
-  if (!last_arrival(g_arrive[0][grp], i, g.nb, &lflag)) return;
-  double LT[1][TPT], M2[TPT], M3[TPT];
+  // the tile carries of this RHS (its last workgroup): chunks of 256 tiles
+  // in order, C1 = exclusive scan of agg1, C2 = exclusive scan of
+  // agg2 + C1 LVt, T = their total, dS = sum MS1 + C2 MS2 + C1 MS3 - T MS4
+  if (!last_arrival(g_arrive[0][r], i, nb, &lflag)) return;
+  const double* R = W + L.rows;
+  double run1 = 0.0, run2 = 0.0, ds = 0.0, m4 = 0.0;
+  for (int t0 = 0; t0 < nb; t0 += CQ * NT) {
+    // every row of the chunk loaded first
+    double A1[CQ], A2[CQ], M1[CQ], LT[CQ], M2[CQ], M3[CQ], M4[CQ];
 #pragma unroll
-  for (int cc = 0; cc < TPT; ++cc) {
-    const int t = cc * NT + tid;
-    const bool ok = t < g.nb;
-    LT[0][cc] = ok ? G_(tabr(tb, g, R_LVT))[t] : 0.0;
-    M2[cc] = ok ? G_(tabr(tb, g, R_MS2))[t] : 0.0;
-    M3[cc] = ok ? G_(tabr(tb, g, R_MS3))[t] : 0.0;
+    for (int q = 0; q < CQ; ++q) {
+      const int t = t0 + q * NT + tid;
+      const bool ok = t < nb;
+      A1[q] = ok ? cld(R + 0 * nb + t) : 0.0;
+      A2[q] = ok ? cld(R + 1 * nb + t) : 0.0;
+      M1[q] = ok ? cld(R + 2 * nb + t) : 0.0;
+      LT[q] = ok ? cld(R + 3 * nb + t) : 0.0;
+      M2[q] = ok ? cld(R + 4 * nb + t) : 0.0;
+      M3[q] = ok ? cld(R + 5 * nb + t) : 0.0;
+      M4[q] = ok ? cld(R + 6 * nb + t) : 0.0;
+    }
+    double C1[CQ], C2[CQ], y2[CQ];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) C1[q] = C2[q] = 0.0;
+    if (flex) {
+      chunk_scan<false, CQ>(A1, C1, run1, sh);
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) y2[q] = A2[q] + C1[q] * LT[q];
+      chunk_scan<false, CQ>(y2, C2, run2, sh);
+    }
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) {
+      const int t = t0 + q * NT + tid;
+      if (t >= nb) continue;
+      W[L.c1 + t] = C1[q];
+      W[L.c2 + t] = C2[q];
+      ds += M1[q] + C2[q] * M2[q] + C1[q] * M3[q];
+      m4 += M4[q];
+    }
   }
-#pragma unroll 1
-  for (int q = 0; q < KG; ++q) {
-    if (!has[q]) break;
-    double* W = a.ws + (long long)(grp * KG + q) * a.wsd;
-    double A1[1][TPT], A2[TPT], M1[TPT], C1[1][TPT], C2[1][TPT], y2[1][TPT], tt[1];
-#pragma unroll
-    for (int cc = 0; cc < TPT; ++cc) {
-      const int t = cc * NT + tid;
-      const bool ok = t < g.nb;
-      A1[0][cc] = ok ? wrow(W, g, W_A1)[t] : 0.0;
-      A2[cc] = ok ? wrow(W, g, W_A2)[t] : 0.0;
-      M1[cc] = ok ? wrow(W, g, W_M1)[t] : 0.0;
-    }
-    tile_scan<1, false>(A1, C1, tt, sh);
-#pragma unroll
-    for (int cc = 0; cc < TPT; ++cc) y2[0][cc] = A2[cc] + C1[0][cc] * LT[0][cc];
-    double T[1];
-    tile_scan<1, false>(y2, C2, T, sh);
-    double ds[1] = {0.0};
-#pragma unroll
-    for (int cc = 0; cc < TPT; ++cc) {
-      const int t = cc * NT + tid;
-      if (t < g.nb) {
-        ds[0] += M1[cc] + C2[0][cc] * M2[cc] + C1[0][cc] * M3[cc];
-        wrow(W, g, W_C1)[t] = C1[0][cc];
-        wrow(W, g, W_C2)[t] = C2[0][cc];
-      }
-    }
-    btot<1>(ds, sh);
-    if (tid == 0) {
-      wrow(W, g, W_JN)[J_T] = T[0];
-      wrow(W, g, W_JN)[J_DS] = ds[0];
-    }
+  double v[2] = {ds, m4};
+  btot<2>(v, sh);
+  if (tid == 0) {
+    const double T = flex ? run2 : 0.0;
+    W[L.glb] = T;
+    W[L.glb + 1] = v[0] - T * v[1];
   }
 }
 
-// phase B: the carries of this tile from every tile's a1, a2, m1, the
-// tile-local scans of the (updated) tangent, da; tile 0 also bins 0, 1 and
-// the scalar keys' new direction
-template <int MODE, int KG>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void jvp_b(JvpArgs a) {
-#pragma clang fp contract(off)
-  __shared__ double sh[KG * (2 * NW + 1)];
-  const Geo g = geo_of(a.c.B);
-  int i, grp;
-  place(g.nb, i, grp);
+// second launch: da from Eh and the carries; tile 0 writes the scalar keys'
+// new direction
+template <typename VT, int MODE>
+__global__ __launch_bounds__(NT) void jvp2b_kernel(Jvp2Args<VT> a) {
+  __shared__ double sh[E * NW + 8];
+  int i, r;
+  if (!place(a.nb, a.nrhs, i, r)) return;
   const int tid = threadIdx.x;
-  const AmpConst c = const_of<MODE>(a.c, a.dcs, a.dc1, grp * KG);
+  const AmpConst c = const_of<MODE>(a.c, a.dcs, a.dc1, r);  // by value: loaded once, no aliasing with the stores
+  const int M = (int)(a.c.B - 2);
   const bool flex = a.c.has_flex, asp = a.c.has_asp;
-  const double* tb = c.tab;
-  if (!tb) return;  // constants without tables (nft_amp2_prepare not run): no access
-  const double* gl = tabg(tb, g);
-  bool has[KG];
-  const double* sv[KG];
+  const int nb = a.nb;
+  const int j0 = i * TL + tid;  // striped: bin j0 + e * NT
+  const double* __restrict__ W = a.ws + (long long)r * a.wsd;
+  const JWs L = jws(M, nb);
+  double eh[E], anv[E], scv[E], lvc[1][E];
 #pragma unroll
-  for (int q = 0; q < KG; ++q) {
-    const int r = grp * KG + q;
-    has[q] = r < a.nrhs;
-    sv[q] = wrow(a.ws + (long long)(has[q] ? r : grp * KG) * a.wsd, g, W_JN);
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    const bool ok = j < M;
+    eh[e] = ok ? W[j] : 0.0;
+    anv[e] = ok ? G_(c.An)[j + 2] : 0.0;
+    scv[e] = ok ? G_(c.sc)[j + 2] : 0.0;
+    lvc[0][e] = (ok && flex) ? G_(c.lv)[j] : 0.0;
   }
-  const long long j0 = (long long)i * g.tl();
-  // ---- this tile's carries (phase A's last workgroup formed them)
-  double C1v[KG], C2v[KG], Tv[KG], dSv[KG];
-#pragma unroll
-  for (int q = 0; q < KG; ++q) {
-    const double* W = a.ws + (long long)(grp * KG + (has[q] ? q : 0)) * a.wsd;
-    C1v[q] = flex ? wrow((double*)W, g, W_C1)[i] : 0.0;
-    C2v[q] = flex ? wrow((double*)W, g, W_C2)[i] : 0.0;
-    Tv[q] = flex ? sv[q][J_T] : 0.0;
-    const double ssl = c.sig_s * sv[q][KSL];
-    double d = (flex ? sv[q][J_DS] : 0.0) + ssl * gl[G_KV];
-    if (flex) d += sv[q][KFLEX] * gl[G_KF];
-    if (asp) d += sv[q][KASP] * gl[G_KA];
-    dSv[q] = d - Tv[q] * gl[G_M4];
+  const double C1 = W[L.c1 + i], C2 = W[L.c2 + i], T = W[L.glb], dS = W[L.glb + 1];
+  const double* sv = W + L.scal;
+  const double sfl = sv[KFL];
+  if (flex) {
+    double t[1];
+    scan_arr<1, E, false>(lvc, t, sh);
   }
-  // ---- per bin: the tile-local scans and da
-  double run1[KG], run2[KG];
+  const double dfl = c.fl * c.ls_f * sfl;
+  VT* __restrict__ dr = a.da + (long long)r * a.vs;
+  const int des = (int)a.des;
 #pragma unroll
-  for (int q = 0; q < KG; ++q) run1[q] = run2[q] = 0.0;
-  for (int s = 0; s < g.sub; ++s) {
-    const long long j = j0 + (long long)s * NT + tid;
-    const bool ok = j < g.M;
-    const long long b = j + 2;
-    double sf = 0, c0 = 0, lv = 0, lvc = 0, vsl = 0, qf = 0, qa = 0, scv = 0, an = 0;
-    if (ok) {
-      vsl = G_(c.vslope)[b];
-      scv = G_(c.sc)[b];
-      an = G_(c.An)[b];
-      if (flex) {
-        sf = G_(c.sf)[j];
-        c0 = G_(c.c0)[j];
-        lv = G_(c.lv)[j];
-        lvc = G_(tabv(tb, g, T_LVC))[j];
-        qf = G_(c.Qf)[b];
-        if (asp) qa = G_(c.Qa)[b];
-      }
-    }
-    double th[KG], u[KG];
-    if (flex) {
-      double d0[KG], d1[KG];
-#pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        const long long ro = (long long)(grp * KG + q) * a.ls;
-        const bool okq = ok && has[q];
-        d0[q] = okq ? a.t[KSPEC][ro + j] : 0.0;
-        d1[q] = okq ? a.t[KSPEC][ro + g.M + j] : 0.0;
-        u[q] = d1[q] * sf;
-      }
-      double tu[KG];
-#pragma unroll
-      for (int q = 0; q < KG; ++q) th[q] = u[q];
-      bscan<KG, false>(th, tu, sh);  // th = loc1 (within the sub-chunk)
-#pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        const double loc1 = th[q] + run1[q];
-        run1[q] += tu[q];
-        th[q] = (d0[q] * c0 - u[q] / 2 * lv) + loc1 * lv;
-      }
-      bscan<KG, false>(th, tu, sh);  // th = loc2
-#pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        th[q] += run2[q];
-        run2[q] += tu[q];
-      }
-    }
-    if (!ok) continue;
-#pragma unroll
-    for (int q = 0; q < KG; ++q) {
-      if (!has[q]) continue;
-      const int r = grp * KG + q;
-      const double ssl = c.sig_s * sv[q][KSL];
-      double d = vsl * ssl + (flex ? th[q] : 0.0);
-      if (flex) d += sv[q][KFLEX] * qf;
-      if (asp) d += sv[q][KASP] * qa;
-      const double dp = (d + (C2v[q] + C1v[q] * lvc)) - Tv[q] * scv;
-      const double dfl = c.fl * c.ls_f * sv[q][KFL];
-      a.da[(long long)r * a.vs + b * a.des] =
-          (dfl * an + c.fl * an * (dp / 2. - dSv[q] / (2. * c.S))) * c.total_volume;
-    }
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    if (j >= M) continue;
+    const double dp = (eh[e] + (C2 + C1 * lvc[0][e])) - T * scv[e];
+    const double An = anv[e];
+    dr[(j + 2) * des] = (dfl * An + c.fl * An * (dp / 2. - dS / (2. * c.S))) * c.total_volume;
   }
-  if (i == 0 && tid < 2 * KG) {
-    const int q = tid >> 1, b = tid & 1;
-    if (has[q]) {
-      const int r = grp * KG + q;
-      const double* s_ = sv[q];
-      const double dfl = c.fl * c.ls_f * s_[KFL];
-      double v;
-      if (b == 0) {
-        v = c.has_zm ? c.zm * c.ls_o * s_[KZM] : 0.0;
-      } else {
-        double d = G_(c.vslope)[b] * (c.sig_s * s_[KSL]);
-        if (flex) d += s_[KFLEX] * G_(c.Qf)[b];
-        if (asp) d += s_[KASP] * G_(c.Qa)[b];
-        const double dp = d - Tv[q] * G_(c.sc)[b];
-        const double An = G_(c.An)[b];
-        v = dfl * An + c.fl * An * (dp / 2. - dSv[q] / (2. * c.S));
-      }
-      a.da[(long long)r * a.vs + b * a.des] = v * c.total_volume;
-      if (b == 0 && a.dir && a.sc[(long long)r * NS_ + NFT_CG_DONE] == 0.0) {
-        const long long ro = (long long)r * a.ls;
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-          if (a.t[k] && !(k == KFLEX && !flex) && !(k == KASP && !asp) && !(k == KZM && !c.has_zm)) a.t[k][ro] = s_[k];
-      }
+  if (i == 0 && tid < 2) {
+    const int b = tid;
+    double v;
+    if (b == 0) {
+      v = c.has_zm ? c.zm * c.ls_o * sv[KZM] : 0.0;
+    } else {
+      double d = G_(c.vslope)[b] * (c.sig_s * sv[KSL]);
+      if (flex) d += sv[KFLEX] * G_(c.Qf)[b];
+      if (asp) d += sv[KASP] * G_(c.Qa)[b];
+      const double dp = d - T * G_(c.sc)[b];
+      const double An = G_(c.An)[b];
+      v = dfl * An + c.fl * An * (dp / 2. - dS / (2. * c.S));
     }
+    dr[b * des] = v * c.total_volume;
+  }
+  if (a.dir && i == 0 && tid == 0 && a.sc[(long long)r * NS_ + NFT_CG_DONE] == 0.0) {
+    const long long ro = (long long)r * a.ls;
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+      if (a.t[q] && !(q == KFLEX && !flex) && !(q == KASP && !asp) && !(q == KZM && !c.has_zm)) a.t[q][ro] = sv[q];
   }
 }
 
 // ======================================================================= VJP
-struct VjpArgs {
+template <typename VT>
+struct Vjp2Args {
   AmpConst c;
   const AmpConst* dcs;
   const AmpConst* dc1;
-  const double* g;         // g[r * gs + b]
+  const VT* g;             // g[r * gs + b]
   long long gs;
   // plain mode: out keys (= shift * d + J^T g) and the d keys for the shift
   // CG mode (cg): x, r, d keys, updated x -= alpha d, r -= alpha (q + shift d)
-  double* o[6];
-  double* o2[6];           // cg: r keys
-  const double* d[6];      // d keys (shift / cg)
+  VT* o[6];
+  VT* o2[6];               // cg: r keys
+  const VT* d[6];          // d keys (shift / cg)
   long long ls;
   double shift;
   double* ws;
   long long wsd;
-  int nrhs;
+  int nrhs, nb;
   int cg;
   double* sc;              // CG scalar blocks (cg: alpha read, finalized here)
   double* part;            // cg: rr / xr partials per tile, part[r * pstride + {0, nb} + tile]
@@ -836,391 +590,369 @@ struct VjpArgs {
   int ngp;
 };
 
-// workspace rows of one RHS (VJP)
-enum { V_R1 = 0, V_R2G, V_R3G, V_AGG, V_AWG, V_P0G, V_Q2G, V_P1G, V_CRR, V_CXR, V_N };
-// ... then the carries of phase A's last workgroup: beta(t), S1(t) [nbp
-// each], and the scalars k, R1, R2, u0 (flexibility), u1 (asperity)
-enum { V_BT = V_N, V_S1, V_SC };
-enum { S_K = 0, S_R1, S_R2, S_U0, S_U1 };
+// workspace of one RHS: the tile sums (V_NROWS rows of nb), then the carries
+// beta [nb], S1 [nb], then k, R1, R2, R4, R5
+enum { V_R1 = 0, V_R2G, V_R3G, V_R2M, V_R3M, V_AG, V_AM, V_AWG, V_AWM, V_AWL, V_P0G, V_P0M, V_P0S, V_Q2G, V_Q2M,
+       V_Q2L, V_P2S, V_P1G, V_P1M, V_P1S, V_CRR, V_CXR, V_NROWS };
+struct VWs {
+  long long bet, s1, glb;
+};
+__device__ __host__ __forceinline__ VWs vws(int nb) {
+  VWs w;
+  w.bet = (long long)V_NROWS * nb;
+  w.s1 = w.bet + nb;
+  w.glb = w.s1 + nb;
+  return w;
+}
 
-// phase A: the tile's dot products of G = An fl TV g / 2 with the constant
-// vectors (+ its slice of the grid segment's CG partials)
-template <int MODE, int KG>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void vjp_a(VjpArgs a) {
-#pragma clang fp contract(off)
-  __shared__ double sh[(V_N * KG) * (NW + 1)];
+// tile-local reverse scans of the VJP: y = [G, mspec] (yG, ym), then
+// w = y lv/2 + y_{j+1} lv_{j+1}/2 with y_{j+1} = y_j - (its own term) for
+// both and wl = lv/2 + lv_{j+1}/2; second: the reverse scans of w (g1G, g1m,
+// g1l).  Both launches run it on the same inputs (bitwise the same values).
+__device__ __forceinline__ void vjp_scans(const double (&G)[E], const double (&msv)[E], const double (&lvv)[E],
+                                          const double (&lvn)[E], double (&y)[2][E], double (&w)[3][E],
+                                          double (&ty)[2], double (&tw)[3], double* sh, bool second) {
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    y[0][e] = G[e];
+    y[1][e] = msv[e];
+  }
+  scan_arr<2, E, true>(y, ty, sh);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    w[0][e] = y[0][e] * lvv[e] / 2. + (y[0][e] - G[e]) * lvn[e] / 2.;
+    w[1][e] = y[1][e] * lvv[e] / 2. + (y[1][e] - msv[e]) * lvn[e] / 2.;
+    w[2][e] = lvv[e] / 2. + lvn[e] / 2.;
+  }
+  if (second) scan_arr<3, E, true>(w, tw, sh);
+}
+
+// first launch: the tile sums (and, cg, this tile's slice of the grid
+// segment's r.r / x.r partials); the last workgroup of each RHS then forms
+// that RHS's k, R1, R2, R4, R5 and the carries beta, S1 of every tile
+template <typename VT, int MODE>
+__global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
+  __shared__ double sh[3 * E * NW + 24 * NW];
   __shared__ int lflag;
-  const Geo g = geo_of(a.c.B);
-  int i, grp;
-  place(g.nb, i, grp);
+  int i, r;
+  if (!place(a.nb, a.nrhs, i, r)) return;
   const int tid = threadIdx.x;
-  const AmpConst c = const_of<MODE>(a.c, a.dcs, a.dc1, grp * KG);
+  const AmpConst c = const_of<MODE>(a.c, a.dcs, a.dc1, r);  // by value: loaded once, no aliasing with the stores
+  const int M = (int)(a.c.B - 2);
   const bool flex = a.c.has_flex, asp = a.c.has_asp;
-  const double* tb = c.tab;
-  if (!tb) return;  // constants without tables (nft_amp2_prepare not run): no access
+  const int nb = a.nb;
+  const int j0 = i * TL + tid;  // striped: bin j0 + e * NT
   const double TV = c.total_volume;
-  bool has[KG];
+  double* __restrict__ W = a.ws + (long long)r * a.wsd;
+  const VT* __restrict__ gr = a.g + (long long)r * a.gs;
+  double gb[E], anv[E], msv[E], vsl[E], scv[E], lvv[E], lvn[E], p0v[E], p1v[E], pc[1][E];
 #pragma unroll
-  for (int q = 0; q < KG; ++q) has[q] = grp * KG + q < a.nrhs;
-  double s[V_N * KG];
-#pragma unroll
-  for (int k = 0; k < V_N * KG; ++k) s[k] = 0.0;
-  const long long j0 = (long long)i * g.tl();
-  for (int sc_ = 0; sc_ < g.sub; ++sc_) {
-    const long long j = j0 + (long long)sc_ * NT + tid;
-    const bool ok = j < g.M;
-    const long long b = j + 2;
-    double an = 0, vsl = 0, scv = 0, k1 = 0, k2 = 0, k3 = 0, k4 = 0;
-    if (ok) {
-      an = G_(c.An)[b];
-      vsl = G_(c.vslope)[b];
-      scv = G_(c.sc)[b];
-      if (flex) {
-        k1 = G_(tabv(tb, g, T_K1))[j];
-        k2 = G_(tabv(tb, g, T_K2))[j];
-        k3 = G_(tabv(tb, g, T_K3))[j];
-        if (asp) k4 = G_(tabv(tb, g, T_K4))[j];
-      }
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    const bool ok = j < M, okf = ok && flex;
+    const int b = j + 2;
+    gb[e] = ok ? gr[b] : 0.0;
+    anv[e] = ok ? G_(c.An)[b] : 0.0;
+    msv[e] = ok ? G_(c.mspec)[b] : 0.0;
+    vsl[e] = ok ? G_(c.vslope)[b] : 0.0;
+    scv[e] = ok ? G_(c.sc)[b] : 0.0;
+    lvv[e] = okf ? G_(c.lv)[j] : 0.0;
+    lvn[e] = (okf && j + 1 < M) ? G_(c.lv)[j + 1] : 0.0;
+    p0v[e] = okf ? G_(c.p0)[j] : 0.0;
+    p1v[e] = (okf && asp) ? G_(c.p1)[j] : 0.0;
+    pc[0][e] = okf ? G_(c.p2)[j] : 0.0;
+  }
+  // grid partial slice (cg)
+  double crr = 0.0, cxr = 0.0;
+  if (a.cg) {
+    const int per = (a.ngp + nb - 1) / nb;
+    const int lo = i * per, hi = min(a.ngp, lo + per);
+    const double* gp = a.gpart + (long long)r * a.gps;
+    for (int t = lo + tid; t < hi; t += NT) {
+      crr += gp[t];
+      cxr += gp[a.gpr + t];
     }
-    double gb[KG];
+  }
+  // G_b = An_b (fl TV g_b) / 2 (gapre without its normalisation term)
+  double G[E];
+  constexpr int NV = V_NROWS - 3;  // every row but aggG / aggm (scan totals) and P2S
+  double s[NV + 1];
 #pragma unroll
-    for (int q = 0; q < KG; ++q) gb[q] = (ok && has[q]) ? a.g[(long long)(grp * KG + q) * a.gs + b] : 0.0;
+  for (int q = 0; q <= NV; ++q) s[q] = 0.0;
+  // s index of row q: q < V_AG -> q; V_AWG.. -> q - 2 (aggG, aggm skipped), P2S skipped
+  auto S = [&](int row) -> double& { return s[row < V_AG ? row : (row < V_P2S ? row - 2 : row - 3)]; };
 #pragma unroll
-    for (int q = 0; q < KG; ++q) {
-      const double G = an * (c.fl * (TV * gb[q])) / 2.;
-      double* S = s + V_N * q;
-      S[V_R1] += TV * gb[q] * an;
-      S[V_R2G] += vsl * G;
-      S[V_R3G] += G * scv;
-      S[V_AGG] += G;
-      S[V_AWG] += G * k1;
-      S[V_P0G] += G * k2;
-      S[V_Q2G] += G * k3;
-      S[V_P1G] += G * k4;
-    }
+  for (int e = 0; e < E; ++e) {
+    G[e] = anv[e] * (c.fl * (TV * gb[e])) / 2.;
+    S(V_R1) += TV * gb[e] * anv[e];
+    S(V_R2G) += vsl[e] * G[e];
+    S(V_R3G) += G[e] * scv[e];
+    S(V_R2M) += vsl[e] * msv[e];
+    S(V_R3M) += msv[e] * scv[e];
   }
   if (i == 0 && tid < 2) {  // bins 0 and 1
     const int b = tid;
-    const double an = G_(c.An)[b], vs = G_(c.vslope)[b], scb = G_(c.sc)[b];
+    const double an = G_(c.An)[b], ms = G_(c.mspec)[b], vs = G_(c.vslope)[b], scb = G_(c.sc)[b];
+    const double g_ = gr[b];
+    const double ga = an * (c.fl * (b > 0 ? TV * g_ : 0.0)) / 2.;
+    if (b > 0) S(V_R1) += TV * g_ * an;
+    S(V_R2G) += vs * ga;
+    S(V_R3G) += ga * scb;
+    S(V_R2M) += vs * ms;
+    S(V_R3M) += ms * scb;
+  }
+  double ty[2] = {0.0, 0.0}, tpc[1] = {0.0};
+  if (flex) {
+    double y[2][E], w[3][E], tw[3];
+    vjp_scans(G, msv, lvv, lvn, y, w, ty, tw, sh, false);
+    // p2c: tile-local forward scan of p2, so that sum_j g1_j p2_j (g1 the
+    // reverse scan of w) is sum_j w_j p2c_j without that second scan
+    scan_arr<1, E, false>(pc, tpc, sh);
 #pragma unroll
-    for (int q = 0; q < KG; ++q) {
-      if (!has[q]) continue;
-      const double g_ = a.g[(long long)(grp * KG + q) * a.gs + b];
-      const double ga = an * (c.fl * (b > 0 ? TV * g_ : 0.0)) / 2.;
-      double* S = s + V_N * q;
-      if (b > 0) S[V_R1] += TV * g_ * an;
-      S[V_R2G] += vs * ga;
-      S[V_R3G] += ga * scb;
+    for (int e = 0; e < E; ++e) {
+      S(V_AWG) += w[0][e];
+      S(V_AWM) += w[1][e];
+      S(V_AWL) += w[2][e];
+      S(V_P0G) += y[0][e] * p0v[e];
+      S(V_P0M) += y[1][e] * p0v[e];
+      S(V_P0S) += p0v[e];
+      S(V_Q2G) += w[0][e] * pc[0][e];
+      S(V_Q2M) += w[1][e] * pc[0][e];
+      S(V_Q2L) += w[2][e] * pc[0][e];
+      S(V_P1G) += y[0][e] * p1v[e];
+      S(V_P1M) += y[1][e] * p1v[e];
+      S(V_P1S) += p1v[e];
     }
   }
-  if (a.cg) {
-    const int per = (a.ngp + g.nb - 1) / g.nb;
-    const int lo = i * per, hi = min(a.ngp, lo + per);
+  S(V_CRR) += crr;
+  S(V_CXR) += cxr;
+  btot<NV + 1>(s, sh);
+  if (tid == 0) {
 #pragma unroll
-    for (int q = 0; q < KG; ++q) {
-      if (!has[q]) continue;
-      const double* gp = a.gpart + (long long)(grp * KG + q) * a.gps;
-      for (int t = lo + tid; t < hi; t += NT) {
-        s[V_N * q + V_CRR] += gp[t];
-        s[V_N * q + V_CXR] += gp[a.gpr + t];
+    for (int q = 0; q < V_NROWS; ++q) {
+      double v;
+      if (q == V_AG) v = ty[0];
+      else if (q == V_AM) v = ty[1];
+      else if (q == V_P2S) v = tpc[0];
+      else v = S(q);
+      cst(W + (long long)q * nb + i, v);
+    }
+  }
+  if (!last_arrival(g_arrive[1][r], i, nb, &lflag)) return;
+  // this RHS's globals (fixed-order sums over the tiles) ...
+  auto row = [&](int q, int t) { return cld(W + (long long)q * nb + t); };
+  double gsum[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int t = tid; t < nb; t += NT) {
+    gsum[0] += row(V_R1, t);
+    gsum[1] += row(V_R3G, t);
+    gsum[2] += row(V_R3M, t);
+    gsum[3] += row(V_R2G, t);
+    gsum[4] += row(V_R2M, t);
+  }
+  btot<5>(gsum, sh);
+  const double kv = c.fl * gsum[0] / (2. * c.S);
+  const double R3 = gsum[1] - kv * gsum[2];
+  const VWs L = vws(nb);
+  // ... and, from the last tile down in chunks of 512, the carries
+  // beta(t) = SG - k SM - R3 and S1(t) (exclusive reverse sums), R4, R5
+  double u[2] = {0.0, 0.0};
+  if (flex) {
+    double rg = 0.0, rm = 0.0, rz = 0.0;
+    const int nch = (nb + CQ * NT - 1) / (CQ * NT);
+    for (int ch = nch - 1; ch >= 0; --ch) {
+      // every row of the chunk loaded first
+      constexpr int NRW = 14;
+      const int rows_[NRW] = {V_AG, V_AM, V_AWG, V_AWM, V_AWL, V_P0G, V_P0M, V_P0S, V_Q2G, V_Q2M, V_Q2L, V_P2S,
+                              V_P1G, V_P1M};
+      double x[NRW][CQ], p1s[CQ];
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        const int t = ch * CQ * NT + q * NT + tid;
+        const bool ok = t < nb;
+#pragma unroll
+        for (int k = 0; k < NRW; ++k) x[k][q] = ok ? row(rows_[k], t) : 0.0;
+        p1s[q] = ok ? row(V_P1S, t) : 0.0;
+      }
+      double sg[CQ], sm[CQ], z[CQ], S1[CQ], bet[CQ];
+      chunk_scan<true, CQ>(x[0], sg, rg, sh);
+      chunk_scan<true, CQ>(x[1], sm, rm, sh);
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        const int t = ch * CQ * NT + q * NT + tid;
+        bet[q] = (sg[q] - kv * sm[q]) - R3;
+        z[q] = t < nb ? ((x[2][q] - kv * x[3][q]) + bet[q] * x[4][q]) : 0.0;
+      }
+      chunk_scan<true, CQ>(z, S1, rz, sh);
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        const int t = ch * CQ * NT + q * NT + tid;
+        if (t >= nb) continue;
+        W[L.bet + t] = bet[q];
+        W[L.s1 + t] = S1[q];
+        u[0] += ((x[5][q] - kv * x[6][q]) + bet[q] * x[7][q]) + ((x[8][q] - kv * x[9][q]) + bet[q] * x[10][q]) +
+                S1[q] * x[11][q];
+        u[1] += (x[12][q] - kv * x[13][q]) + bet[q] * p1s[q];
       }
     }
   }
-  btot_sh<V_N * KG>(s, sh);
-  const double* tot = sh + V_N * KG * NW;
-#pragma unroll
-  for (int q = 0; q < KG; ++q) if (tid == q && has[q]) {
-    double* W = a.ws + (long long)(grp * KG + q) * a.wsd;
-#pragma unroll
-    for (int k = 0; k < V_N; ++k) wrow(W, g, k)[i] = tot[V_N * q + k];
-  }
-  // the carries of every tile (the group's last workgroup), right-hand sides
-  // one after the other: k = fl R1 / (2 S), R3 = R3G - k R3M; beta(t) =
-  // SG(t) - k SM(t) - R3 (SG: sum of aggG over the tiles after t); S1 =
-  // exclusive reverse scan of (AWG - k AWM) + beta AWL; R2 = R2G - k R2M;
-  // u0, u1 = the flexibility / asperity cotangents
-  if (!last_arrival(g_arrive[1][grp], i, g.nb, &lflag)) return;
-  double SM[TPT], AWM[TPT], AWL[TPT];
-#pragma unroll
-  for (int cc = 0; cc < TPT; ++cc) {
-    const int t = cc * NT + tid;
-    const bool ok = flex && t < g.nb;
-    SM[cc] = ok ? G_(tabr(tb, g, R_SM))[t] : 0.0;
-    AWM[cc] = ok ? G_(tabr(tb, g, R_AWM))[t] : 0.0;
-    AWL[cc] = ok ? G_(tabr(tb, g, R_AWL))[t] : 0.0;
-  }
-#pragma unroll 1
-  for (int q = 0; q < KG; ++q) {
-    if (!has[q]) break;
-    double* W = a.ws + (long long)(grp * KG + q) * a.wsd;
-    double gs[3] = {0.0, 0.0, 0.0};
-    double AG[1][TPT], AW[TPT];
-#pragma unroll
-    for (int cc = 0; cc < TPT; ++cc) {
-      const int t = cc * NT + tid;
-      const bool ok = t < g.nb;
-      gs[0] += ok ? wrow(W, g, V_R1)[t] : 0.0;
-      gs[1] += ok ? wrow(W, g, V_R3G)[t] : 0.0;
-      gs[2] += ok ? wrow(W, g, V_R2G)[t] : 0.0;
-      AG[0][cc] = (ok && flex) ? wrow(W, g, V_AGG)[t] : 0.0;
-      AW[cc] = (ok && flex) ? wrow(W, g, V_AWG)[t] : 0.0;
-    }
-    btot<3>(gs, sh);
-    const double k_ = c.fl * gs[0] / (2. * c.S);
-    const double R3s = gs[1] - k_ * tabg(tb, g)[G_M4];
-    double u[2] = {0.0, 0.0};
-    if (flex) {
-      double SG[1][TPT], z[1][TPT], S1[1][TPT], tt[1], BT[TPT];
-      tile_scan<1, true>(AG, SG, tt, sh);
-#pragma unroll
-      for (int cc = 0; cc < TPT; ++cc) {
-        const int t = cc * NT + tid;
-        BT[cc] = (SG[0][cc] - k_ * SM[cc]) - R3s;
-        z[0][cc] = t < g.nb ? ((AW[cc] - k_ * AWM[cc]) + BT[cc] * AWL[cc]) : 0.0;
-      }
-      tile_scan<1, true>(z, S1, tt, sh);
-#pragma unroll
-      for (int cc = 0; cc < TPT; ++cc) {
-        const int t = cc * NT + tid;
-        if (t >= g.nb) continue;
-        wrow(W, g, V_BT)[t] = BT[cc];
-        wrow(W, g, V_S1)[t] = S1[0][cc];
-        u[0] += ((wrow(W, g, V_P0G)[t] - k_ * G_(tabr(tb, g, R_P0M))[t]) + BT[cc] * G_(tabr(tb, g, R_P0S))[t]) +
-                ((wrow(W, g, V_Q2G)[t] - k_ * G_(tabr(tb, g, R_Q2M))[t]) + BT[cc] * G_(tabr(tb, g, R_Q2L))[t]) +
-                S1[0][cc] * G_(tabr(tb, g, R_P2S))[t];
-        if (asp) u[1] += (wrow(W, g, V_P1G)[t] - k_ * G_(tabr(tb, g, R_P1M))[t]) + BT[cc] * G_(tabr(tb, g, R_P1S))[t];
-      }
-    }
-    btot<2>(u, sh);
-    if (tid == 0) {
-      double* sc_ = wrow(W, g, V_SC);
-      sc_[S_K] = k_;
-      sc_[S_R1] = gs[0];
-      sc_[S_R2] = gs[2] - k_ * tabg(tb, g)[G_KV];
-      sc_[S_U0] = u[0];
-      sc_[S_U1] = u[1];
-    }
+  btot<2>(u, sh);
+  if (tid == 0) {
+    W[L.glb + 0] = kv;
+    W[L.glb + 1] = gsum[0];
+    W[L.glb + 2] = gsum[3] - kv * gsum[4];
+    W[L.glb + 3] = u[0];
+    W[L.glb + 4] = u[1];
   }
 }
 
-// phase B: this tile's carries (k, beta, S1) from every tile's sums, the
-// tile-local reverse scans of G and w, the spectrum cotangents (plain: the
-// outputs; cg: the update); tile 0 the scalar cotangents; cg: the r.r / x.r
-// partials and, in the last workgroup of the group, the finalize
-template <int MODE, int KG>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void vjp_b(VjpArgs a) {
-#pragma clang fp contract(off)
-  __shared__ double sh[(2 * KG) * (NW + 1)];
+// second launch: the tile-local scans again and the spectrum cotangents
+// (plain: outputs; cg: the update), tile 0 the scalar cotangents; cg: the
+// r.r / x.r partials and the finalize by the last workgroup of the grid
+template <typename VT, int MODE>
+__global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
+  __shared__ double sh[3 * E * NW + 8];
   __shared__ int lflag;
-  const Geo g = geo_of(a.c.B);
-  int i, grp;
-  place(g.nb, i, grp);
+  int i, r;
+  const bool valid = place(a.nb, a.nrhs, i, r);
+  if (!valid) return;
   const int tid = threadIdx.x;
-  const AmpConst c = const_of<MODE>(a.c, a.dcs, a.dc1, grp * KG);
+  const AmpConst c = const_of<MODE>(a.c, a.dcs, a.dc1, r);  // by value: loaded once, no aliasing with the stores
+  const int M = (int)(a.c.B - 2);
   const bool flex = a.c.has_flex, asp = a.c.has_asp;
-  const double* tb = c.tab;
-  if (!tb) return;  // constants without tables (nft_amp2_prepare not run): no access
+  const int nb = a.nb;
+  const int j0 = i * TL + tid;  // striped: bin j0 + e * NT
   const double TV = c.total_volume;
-  bool has[KG];
+  const double* __restrict__ W = a.ws + (long long)r * a.wsd;
+  const VT* __restrict__ gr = a.g + (long long)r * a.gs;
+  const VWs L = vws(nb);
+  const long long ro = (long long)r * a.ls;
+  // every load first
+  double gb[E], anv[E], msv[E], lvv[E], lvn[E], c0v[E], sfv[E], x0[E], x1[E], r0[E], r1[E], d0[E], d1[E];
+  VT* __restrict__ os = a.o[KSPEC] ? a.o[KSPEC] + ro : nullptr;
+  VT* __restrict__ rsp = (a.cg && a.o2[KSPEC]) ? a.o2[KSPEC] + ro : nullptr;
+  const VT* __restrict__ ds = a.d[KSPEC] ? a.d[KSPEC] + ro : nullptr;
 #pragma unroll
-  for (int q = 0; q < KG; ++q) has[q] = grp * KG + q < a.nrhs;
-  // ---- this tile's carries (phase A's last workgroup formed them)
-  double kv[KG], bet[KG], S1v[KG];
-#pragma unroll
-  for (int q = 0; q < KG; ++q) {
-    const double* W = a.ws + (long long)(grp * KG + (has[q] ? q : 0)) * a.wsd;
-    kv[q] = wrow((double*)W, g, V_SC)[S_K];
-    bet[q] = flex ? wrow((double*)W, g, V_BT)[i] : 0.0;
-    S1v[q] = flex ? wrow((double*)W, g, V_S1)[i] : 0.0;
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    const bool ok = j < M, okf = ok && flex;
+    gb[e] = okf ? gr[j + 2] : 0.0;
+    anv[e] = okf ? G_(c.An)[j + 2] : 0.0;
+    msv[e] = okf ? G_(c.mspec)[j + 2] : 0.0;
+    lvv[e] = okf ? G_(c.lv)[j] : 0.0;
+    lvn[e] = (okf && j + 1 < M) ? G_(c.lv)[j + 1] : 0.0;
+    c0v[e] = okf ? G_(c.c0)[j] : 0.0;
+    sfv[e] = okf ? G_(c.sf)[j] : 0.0;
+    x0[e] = (okf && rsp) ? os[j] : 0.0;
+    x1[e] = (okf && rsp) ? os[M + j] : 0.0;
+    r0[e] = (okf && rsp) ? rsp[j] : 0.0;
+    r1[e] = (okf && rsp) ? rsp[M + j] : 0.0;
+    d0[e] = (okf && ds) ? ds[j] : 0.0;
+    d1[e] = (okf && ds) ? ds[M + j] : 0.0;
   }
-  double al[KG];
-  bool okc[KG];
-#pragma unroll
-  for (int q = 0; q < KG; ++q) {
-    al[q] = 0.0;
-    okc[q] = false;
-    if (a.cg && has[q]) {
-      const double* scb = a.sc + (long long)(grp * KG + q) * NS_;
-      const double curv = scb[NFT_CG_CURV], gprev = scb[NFT_CG_GAMMA];
-      al[q] = gprev / curv;
-      okc[q] = (curv == curv) && curv != 0.0 && (al[q] >= 0.0) && (al[q] == al[q]) && scb[NFT_CG_DONE] == 0.0;
-    }
+  const double kv = W[L.glb + 0];
+  const double bet = W[L.bet + i], S1 = W[L.s1 + i];
+  double al = 0.0;
+  bool okc = false;
+  if (a.cg) {
+    const double* scb = a.sc + (long long)r * NS_;
+    const double curv = scb[NFT_CG_CURV], gprev = scb[NFT_CG_GAMMA];
+    al = gprev / curv;
+    okc = (curv == curv) && curv != 0.0 && (al >= 0.0) && (al == al) && scb[NFT_CG_DONE] == 0.0;
   }
-  double rr[KG], xr[KG];
-#pragma unroll
-  for (int q = 0; q < KG; ++q) rr[q] = xr[q] = 0.0;
-  // ---- per bin, sub-chunks from the last (reverse scans)
+  double rr = 0.0, xr = 0.0;
   if (flex) {
-    double ry[KG], rw[KG];
+    double G[E];
 #pragma unroll
-    for (int q = 0; q < KG; ++q) ry[q] = rw[q] = 0.0;
-    const long long j0 = (long long)i * g.tl();
-    for (int s = g.sub - 1; s >= 0; --s) {
-      const long long j = j0 + (long long)s * NT + tid;
-      const bool ok = j < g.M;
-      const long long b = j + 2;
-      // the scans' operands first; the output operands after the scans (a
-      // second load round, fewer live registers through the scans)
-      double an = 0, lv = 0, lvn = 0;
-      if (ok) {
-        an = G_(c.An)[b];
-        lv = G_(c.lv)[j];
-        lvn = j + 1 < g.M ? G_(c.lv)[j + 1] : 0.0;
-      }
-      double G[KG], y[KG], w[KG], ty[KG];
+    for (int e = 0; e < E; ++e) G[e] = anv[e] * (c.fl * (TV * gb[e])) / 2.;
+    double y[2][E], w[3][E], ty[2], tw[3];
+    vjp_scans(G, msv, lvv, lvn, y, w, ty, tw, sh, true);
 #pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        const double gb = (ok && has[q]) ? a.g[(long long)(grp * KG + q) * a.gs + b] : 0.0;
-        G[q] = an * (c.fl * (TV * gb)) / 2.;
-        y[q] = G[q];
-      }
-      bscan<KG, true>(y, ty, sh);
-#pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        y[q] += ry[q];
-        ry[q] += ty[q];
-        w[q] = y[q] * lv / 2. + (y[q] - G[q]) * lvn / 2.;
-      }
-      bscan<KG, true>(w, ty, sh);
-#pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        w[q] += rw[q];
-        rw[q] += ty[q];
-      }
-      if (!ok) continue;
-      const double ym = G_(tabv(tb, g, T_YM))[j], g1m = G_(tabv(tb, g, T_G1M))[j];
-      const double g1l = G_(tabv(tb, g, T_G1L))[j], c0 = G_(c.c0)[j], sf = G_(c.sf)[j];
-      // every operand of the group first (the stores to x / r cannot be
-      // passed by later loads of the same arrays), then the arithmetic
-      double X0[KG], X1[KG], R0[KG], R1[KG], D0[KG], D1[KG];
-#pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        const long long ro = (long long)(grp * KG + q) * a.ls;
-        const double* ds = a.d[KSPEC] ? a.d[KSPEC] + ro : nullptr;
-        X0[q] = X1[q] = R0[q] = R1[q] = D0[q] = D1[q] = 0.0;
-        if (!has[q]) continue;
+    for (int e = 0; e < E; ++e) {
+      const int j = j0 + e * NT;
+      if (j >= M) continue;
+      const double yv = (y[0][e] - kv * y[1][e]) + bet;
+      const double g1 = ((w[0][e] - kv * w[1][e]) + bet * w[2][e]) + S1;
+      const double q0 = yv * c0v[e], q1 = g1 * sfv[e];
+      if (!a.cg) {
+        double v0 = q0, v1 = q1;
         if (ds) {
-          D0[q] = ds[j];
-          D1[q] = ds[g.M + j];
+          v0 += a.shift * d0[e];
+          v1 += a.shift * d1[e];
         }
-        if (a.cg) {
-          X0[q] = a.o[KSPEC][ro + j];
-          X1[q] = a.o[KSPEC][ro + g.M + j];
-          R0[q] = a.o2[KSPEC][ro + j];
-          R1[q] = a.o2[KSPEC][ro + g.M + j];
+        os[j] = v0;
+        os[M + j] = v1;
+      } else {
+        double xa = x0[e], xb = x1[e], ra = r0[e], rb = r1[e];
+        if (okc) {
+          xa = xa - al * d0[e];
+          ra = ra - al * (q0 + a.shift * d0[e]);
+          xb = xb - al * d1[e];
+          rb = rb - al * (q1 + a.shift * d1[e]);
+          os[j] = xa;
+          rsp[j] = ra;
+          os[M + j] = xb;
+          rsp[M + j] = rb;
         }
-      }
-#pragma unroll
-      for (int q = 0; q < KG; ++q) {
-        if (!has[q]) continue;
-        const long long ro = (long long)(grp * KG + q) * a.ls;
-        const double yv = (y[q] - kv[q] * ym) + bet[q];
-        const double g1 = ((w[q] - kv[q] * g1m) + bet[q] * g1l) + S1v[q];
-        const double q0 = yv * c0, q1 = g1 * sf;
-        double* os = a.o[KSPEC] + ro;
-        if (!a.cg) {
-          double v0 = q0, v1 = q1;
-          if (a.d[KSPEC]) {
-            v0 += a.shift * D0[q];
-            v1 += a.shift * D1[q];
-          }
-          os[j] = v0;
-          os[g.M + j] = v1;
-        } else {
-          double* rsp = a.o2[KSPEC] + ro;
-          double xa = X0[q], xb = X1[q], ra = R0[q], rb = R1[q];
-          const double d0 = D0[q], d1 = D1[q];
-          if (okc[q]) {
-            xa = xa - al[q] * d0;
-            ra = ra - al[q] * (q0 + a.shift * d0);
-            xb = xb - al[q] * d1;
-            rb = rb - al[q] * (q1 + a.shift * d1);
-            os[j] = xa;
-            rsp[j] = ra;
-            os[g.M + j] = xb;
-            rsp[g.M + j] = rb;
-          }
-          rr[q] += ra * ra + rb * rb;
-          xr[q] += xa * ra + xb * rb;
-        }
+        rr += ra * ra + rb * rb;
+        xr += xa * ra + xb * rb;
       }
     }
   }
-  // scalar cotangents (tile 0, thread q for RHS q): fl, sl, flex, asp, zm
-#pragma unroll
-  for (int q = 0; q < KG; ++q) if (i == 0 && tid == q && has[q]) {
-    const int r = grp * KG + q;
-    const long long ro = (long long)r * a.ls;
+  // scalar cotangents (tile 0, thread 0): fl, sl, flex, asp, zm
+  if (i == 0 && tid == 0) {
     double qv[5];
-    bool hs[5];
-    const double* scq = wrow(a.ws + (long long)r * a.wsd, g, V_SC);
-    qv[KFL] = c.fl * c.ls_f * scq[S_R1];
-    hs[KFL] = true;
-    qv[KSL] = c.sig_s * scq[S_R2];
-    hs[KSL] = true;
-    qv[KFLEX] = scq[S_U0];
-    hs[KFLEX] = flex;
-    qv[KASP] = scq[S_U1];
-    hs[KASP] = asp;
-    qv[KZM] = c.has_zm ? c.zm * c.ls_o * TV * a.g[(long long)r * a.gs] : 0.0;
-    hs[KZM] = c.has_zm;
+    bool has[5];
+    qv[KFL] = c.fl * c.ls_f * W[L.glb + 1];
+    has[KFL] = true;
+    qv[KSL] = c.sig_s * W[L.glb + 2];
+    has[KSL] = true;
+    qv[KFLEX] = W[L.glb + 3];
+    has[KFLEX] = flex;
+    qv[KASP] = W[L.glb + 4];
+    has[KASP] = asp;
+    qv[KZM] = c.has_zm ? c.zm * c.ls_o * TV * gr[0] : 0.0;
+    has[KZM] = c.has_zm;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      if (!hs[k] || !a.o[k]) continue;
+    for (int q = 0; q < 5; ++q) {
+      if (!has[q] || !a.o[q]) continue;
       if (!a.cg) {
-        a.o[k][ro] = qv[k] + (a.d[k] ? a.shift * a.d[k][ro] : 0.0);
+        a.o[q][ro] = qv[q] + (a.d[q] ? a.shift * a.d[q][ro] : 0.0);
       } else {
-        double x = a.o[k][ro], rv = a.o2[k][ro];
-        const double d = a.d[k][ro];
-        if (okc[q]) {
-          x = x - al[q] * d;
-          rv = rv - al[q] * (qv[k] + a.shift * d);
-          a.o[k][ro] = x;
-          a.o2[k][ro] = rv;
+        double x = a.o[q][ro], rv = a.o2[q][ro];
+        const double d = a.d[q][ro];
+        if (okc) {
+          x = x - al * d;
+          rv = rv - al * (qv[q] + a.shift * d);
+          a.o[q][ro] = x;
+          a.o2[q][ro] = rv;
         }
-        rr[q] += rv * rv;
-        xr[q] += x * rv;
+        rr += rv * rv;
+        xr += x * rv;
       }
     }
   }
   if (!a.cg) return;
-  double v[2 * KG];
-#pragma unroll
-  for (int q = 0; q < KG; ++q) {
-    v[2 * q] = rr[q];
-    v[2 * q + 1] = xr[q];
-  }
-  btot_sh<2 * KG>(v, sh);
-  const double* tot = sh + 2 * KG * NW;
-#pragma unroll
-  for (int q = 0; q < KG; ++q) if (tid == q && has[q]) {
-    const int r = grp * KG + q;
-    const double* W = a.ws + (long long)r * a.wsd;
+  double v[2] = {rr, xr};
+  btot<2>(v, sh);
+  if (tid == 0) {
     double* pp = a.part + (long long)r * a.pstride;
     // this tile's amplitude sums, then its slice of the grid partials
-    pp[i] = tot[2 * q] + wrow((double*)W, g, V_CRR)[i];
-    pp[g.nb + i] = tot[2 * q + 1] + wrow((double*)W, g, V_CXR)[i];
+    cst(pp + i, v[0] + W[(long long)V_CRR * nb + i]);
+    cst(pp + nb + i, v[1] + W[(long long)V_CXR * nb + i]);
   }
-  // finalize (the last workgroup of the group): each RHS's tile partials
-  // folded in index order, then cg_finalize_kernel's bookkeeping; one wave
-  // per right-hand side
-  if (!last_arrival(g_arrive[2][grp], i, g.nb, &lflag)) return;
-  const int lane = tid & 63, wv = tid >> 6;
-  if (wv < KG && has[wv]) {
-    const int r = grp * KG + wv;
-    const double* pp = a.part + (long long)r * a.pstride;
-    double f0 = 0.0, f1 = 0.0;
-    for (int t = lane; t < g.nb; t += 64) {
-      f0 += pp[t];
-      f1 += pp[g.nb + t];
+  // finalize (the last workgroup of the grid): the tile partials of every
+  // RHS folded in index order, then cg_finalize_kernel's bookkeeping
+  if (!last_arrival(g_arrive[2][0], i * a.nrhs + r, nb * a.nrhs, &lflag)) return;
+  for (int rr_ = 0; rr_ < a.nrhs; ++rr_) {
+    const double* pp = a.part + (long long)rr_ * a.pstride;
+    double f[2] = {0.0, 0.0};
+    for (int t = tid; t < nb; t += NT) {
+      f[0] += cld(pp + t);
+      f[1] += cld(pp + nb + t);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      f0 += __shfl_down(f0, off, 64);
-      f1 += __shfl_down(f1, off, 64);
-    }
-    if (lane == 0) {
-      double* scb = a.sc + (long long)r * NS_;
+    btot<2>(f, sh);
+    if (tid == 0) {
+      double* scb = a.sc + (long long)rr_ * NS_;
       if (scb[NFT_CG_DONE] == 0.0) {
         const double curv = scb[NFT_CG_CURV], gprev = scb[NFT_CG_GAMMA];
         const double alpha = gprev / curv;
@@ -1230,21 +962,35 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void vj
         scb[NFT_CG_ITER] += 1.0;
         if (ok) {
           scb[NFT_CG_GPREV] = gprev;
-          scb[NFT_CG_GAMMA] = f0;
-          scb[NFT_CG_XR] = f1;
+          scb[NFT_CG_GAMMA] = f[0];
+          scb[NFT_CG_XR] = f[1];
           scb[NFT_CG_XB] = 0.0;
         }
-        if (!ok || (scb[NFT_CG_AUTO] != 0.0 && !(f0 > 0.0))) scb[NFT_CG_DONE] = 2.0;
+        if (!ok || (scb[NFT_CG_AUTO] != 0.0 && !(f[0] > 0.0))) scb[NFT_CG_DONE] = 2.0;
       }
     }
   }
 }
 
 // ------------------------------------------------------------------ launch
+static int nblk(long long n, long long per) { return (int)std::max<long long>(1, (n + per - 1) / per); }
+
+// NFT_AMP2=0: off (the multi-kernel path); nft_amp2_set_enabled overrides
+// the environment (tests, A/B)
 static int g_override = -1;
 static bool enabled() {
   static const int on = getenv("NFT_AMP2") ? atoi(getenv("NFT_AMP2")) : 1;
   return g_override >= 0 ? g_override != 0 : on != 0;
+}
+
+// tile count (1024-bin tiles, the same for every batch size), 0: not
+// applicable (NFT_AMP2=0, B < 3, too many RHS, or the workspace too small)
+static int tiles_of(long long B, int nrhs) {
+  if (!enabled() || B < 3 || nrhs < 1 || nrhs > MAXR) return 0;
+  const long long wsd = (long long)(nft_amp_workspace(B) / sizeof(double));
+  const long long nb = nblk(B - 2, TL);
+  if ((V_NROWS + 2) * nb + 8 > wsd || ((B + 63) & ~63LL) + 9 * nb + 10 > wsd) return 0;
+  return (int)nb;
 }
 
 }  // namespace amp2
@@ -1252,45 +998,6 @@ static bool enabled() {
 
 using namespace nft;
 using namespace nft::amp2;
-
-namespace {
-// right-hand sides per workgroup (at most kmax: the register budget of the
-// kernel): the constant sets of MODE 1 differ per RHS
-int kg_of(int nrhs, int mode, int kmax) {
-  if (mode == 1 || nrhs <= 1 || kmax <= 1) return 1;
-  return (nrhs == 2 || kmax == 2) ? 2 : 4;
-}
-// tuning probe (NFT_AMP2_KA / _KB / _KV = 1, 2 or 4): RHS per workgroup of
-// the JVP's first / second launch and of the VJP's
-int kg_env(const char* name, int def) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : 0;
-  return (v == 1 || v == 2 || v == 4) ? v : def;
-}
-
-#define NFT_AMP2_LAUNCH(KERN, ARGS, MODE, KG, GRID, S)                                              \
-  do {                                                                                              \
-    if ((MODE) == 1) hipLaunchKernelGGL((KERN<1, 1>), GRID, dim3(NT), 0, S, ARGS);                  \
-    else if ((MODE) == 2) {                                                                         \
-      if ((KG) == 1) hipLaunchKernelGGL((KERN<2, 1>), GRID, dim3(NT), 0, S, ARGS);                  \
-      else if ((KG) == 2) hipLaunchKernelGGL((KERN<2, 2>), GRID, dim3(NT), 0, S, ARGS);             \
-      else hipLaunchKernelGGL((KERN<2, 4>), GRID, dim3(NT), 0, S, ARGS);                            \
-    } else {                                                                                        \
-      if ((KG) == 1) hipLaunchKernelGGL((KERN<0, 1>), GRID, dim3(NT), 0, S, ARGS);                  \
-      else if ((KG) == 2) hipLaunchKernelGGL((KERN<0, 2>), GRID, dim3(NT), 0, S, ARGS);             \
-      else hipLaunchKernelGGL((KERN<0, 4>), GRID, dim3(NT), 0, S, ARGS);                            \
-    }                                                                                               \
-  } while (0)
-
-// tiles per RHS (0: not applicable -- NFT_AMP2=0, B < 3, too many RHS)
-int tiles_of(long long B, int nrhs) {
-  if (!enabled() || B < 3 || nrhs < 1 || nrhs > MAXR) return 0;
-  const Geo g = geo_of(B);
-  const long long wsd = (long long)(nft_amp_workspace(B) / sizeof(double));
-  if ((long long)V_SC * g.nbp + 8 > wsd || (long long)W_JN * g.nbp + 8 > wsd) return 0;
-  return g.nb;
-}
-}  // namespace
 
 extern "C" {
 
@@ -1303,123 +1010,73 @@ int nft_amp2_tiles(int64_t B, int nrhs, int item_mode) {
   return tiles_of(B, nrhs);
 }
 
-int64_t nft_amp2_tab_len(int64_t B) { return B < 3 ? 0 : tab_len(geo_of(B)); }
+}  // extern "C"
 
-int nft_amp2_prepare(const nft_amp_const* c, nft_amp_const* item_consts, int nrow, double* tab, int64_t tab_stride,
-                     hipStream_t stream) {
-  if (!c || c->B < 3 || !tab || nrow < 1 || (nrow > 1 && !item_consts) ||
-      (item_consts && tab_stride < nft_amp2_tab_len(c->B)) || (c->has_asp && !c->has_flex)) {
-    set_last_error("nft_amp2_prepare: invalid arguments");
-    return NFT_ERR_ARG;
-  }
-  if (!item_consts && (!c->mspec || !c->sc || !c->vslope || !c->An ||
-                       (c->has_flex && (!c->lv || !c->sf || !c->c0 || !c->p0 || !c->p2 || !c->Qf)) ||
-                       (c->has_asp && (!c->p1 || !c->Qa)))) {
-    set_last_error("nft_amp2_prepare: a constant array the flags need is NULL");
-    return NFT_ERR_ARG;
-  }
-  PrepArgs a{};
-  a.c = *c;
-  a.dcs = item_consts;
-  a.tab = tab;
-  a.ts = tab_stride;
-  a.nrow = nrow;
-  const Geo g = geo_of(c->B);
-  prof_mark(stream, "amp2_prepare");
-  if (item_consts) {
-    hipLaunchKernelGGL((prep_tiles<true>), dim3((unsigned)(g.nb * nrow)), dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL((prep_globals<true>), dim3((unsigned)nrow), dim3(NT), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL((prep_tiles<false>), dim3((unsigned)g.nb), dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL((prep_globals<false>), dim3(1), dim3(NT), 0, stream, a);
-  }
-  NFT_HIP_CHECK(hipGetLastError());
-  return NFT_OK;
-}
+namespace {
+#define NFT_AMP2_LAUNCH(KERN, VT, MODE, GRID, S, ARGS)                                  \
+  do {                                                                                  \
+    if ((MODE) == 1) hipLaunchKernelGGL((KERN<VT, 1>), GRID, dim3(NT), 0, S, ARGS);     \
+    else if ((MODE) == 2) hipLaunchKernelGGL((KERN<VT, 2>), GRID, dim3(NT), 0, S, ARGS); \
+    else hipLaunchKernelGGL((KERN<VT, 0>), GRID, dim3(NT), 0, S, ARGS);                 \
+  } while (0)
 
-int nft_amp2_jvp(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, double* const* t,
-                 const double* const* r, int64_t lat_stride, double* da, int64_t da_stride, int64_t da_elem_stride,
-                 double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift,
-                 hipStream_t stream) {
-  if (!cst_ || !t || !da || !ws || nrhs < 1 || cst_->B < 3 || (cst_->has_flex && !t[KSPEC]) ||
-      (r && (!sc || !part))) {
-    set_last_error("nft_amp2_jvp: invalid arguments");
-    return NFT_ERR_ARG;
-  }
-  if (item_mode < 0 || item_mode > 2 || (item_mode != 0 && !item_consts) || (item_mode == 0 && !cst_->tab)) {
-    set_last_error("nft_amp2_jvp: invalid item_mode / item_consts, or constants without tables (nft_amp2_prepare)");
-    return NFT_ERR_ARG;
-  }
-  const int nb = tiles_of(cst_->B, nrhs);
-  if (!nb) return NFT_AMP2_FALLBACK;
-  JvpArgs a{};
+template <typename VT>
+int amp2_jvp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, void* const* t,
+                  const void* const* r, int64_t lat_stride, void* da, int64_t da_stride, int64_t da_elem_stride,
+                  double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift, int nb,
+                  hipStream_t stream) {
+  Jvp2Args<VT> a{};
   a.c = *cst_;
   a.dcs = item_mode == 1 ? item_consts : nullptr;
   a.dc1 = item_mode == 2 ? item_consts : nullptr;
   for (int q = 0; q < 6; ++q) {
-    a.t[q] = t[q];
-    a.r[q] = r ? r[q] : nullptr;
-    if (r && t[q] && !r[q]) {
-      set_last_error("nft_amp2_jvp: a direction key without its residual");
-      return NFT_ERR_ARG;
-    }
+    a.t[q] = (VT*)t[q];
+    a.r[q] = r ? (const VT*)r[q] : nullptr;
   }
   a.ls = lat_stride;
-  a.da = da;
+  a.da = (VT*)da;
   a.vs = da_stride;
   a.des = da_elem_stride > 0 ? da_elem_stride : 1;
   a.ws = ws;
   a.wsd = (long long)(nft_amp_workspace(cst_->B) / sizeof(double));
   a.nrhs = nrhs;
+  a.nb = nb;
   a.dir = r != nullptr;
   a.sc = sc;
   a.part = part;
   a.pstride = pstride;
   a.shift = shift;
-  const int ka = kg_of(nrhs, item_mode, kg_env("NFT_AMP2_KA", 4)), kb = kg_of(nrhs, item_mode, kg_env("NFT_AMP2_KB", 2));
-  prof_mark(stream, a.dir ? "amp_jvp_a+dir" : "amp_jvp_a");
-  NFT_AMP2_LAUNCH(jvp_a, a, item_mode, ka, dim3((unsigned)(nb * ((nrhs + ka - 1) / ka))), stream);
-  prof_mark(stream, "amp_jvp_b");
-  NFT_AMP2_LAUNCH(jvp_b, a, item_mode, kb, dim3((unsigned)(nb * ((nrhs + kb - 1) / kb))), stream);
+  const dim3 grid(grid_of(nb, nrhs));
+  prof_mark(stream, a.dir ? "amp_jvp2a+dir" : "amp_jvp2a");
+  NFT_AMP2_LAUNCH(jvp2a_kernel, VT, item_mode, grid, stream, a);
+  prof_mark(stream, "amp_jvp2b");
+  NFT_AMP2_LAUNCH(jvp2b_kernel, VT, item_mode, grid, stream, a);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
 
-int nft_amp2_vjp(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, const double* g,
-                 int64_t g_stride, double* const* out, double* const* out2, const double* const* d,
-                 int64_t lat_stride, double shift, double* ws, int nrhs, double* sc, double* part, int64_t pstride,
-                 const double* gpart, int64_t gp_stride, int64_t gp_row, int ngp, hipStream_t stream) {
-  if (!cst_ || !g || !out || !ws || nrhs < 1 || cst_->B < 3 || (cst_->has_flex && !out[KSPEC]) ||
-      (out2 && (!d || !sc || !part || (ngp > 0 && !gpart)))) {
-    set_last_error("nft_amp2_vjp: invalid arguments");
-    return NFT_ERR_ARG;
-  }
-  if (item_mode < 0 || item_mode > 2 || (item_mode != 0 && !item_consts) || (item_mode == 0 && !cst_->tab)) {
-    set_last_error("nft_amp2_vjp: invalid item_mode / item_consts, or constants without tables (nft_amp2_prepare)");
-    return NFT_ERR_ARG;
-  }
-  const int nb = tiles_of(cst_->B, nrhs);
-  if (!nb) return NFT_AMP2_FALLBACK;
-  VjpArgs a{};
+template <typename VT>
+int amp2_vjp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, const void* g,
+                  int64_t g_stride, void* const* out, void* const* out2, const void* const* d, int64_t lat_stride,
+                  double shift, double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
+                  int64_t gp_stride, int64_t gp_row, int ngp, int nb, hipStream_t stream) {
+  Vjp2Args<VT> a{};
   a.c = *cst_;
   a.dcs = item_mode == 1 ? item_consts : nullptr;
   a.dc1 = item_mode == 2 ? item_consts : nullptr;
-  a.g = g;
+  a.g = (const VT*)g;
   a.gs = g_stride;
   for (int q = 0; q < 6; ++q) {
-    a.o[q] = out[q];
-    a.o2[q] = out2 ? out2[q] : nullptr;
-    a.d[q] = d ? d[q] : nullptr;
-    if (out2 && out[q] && (!out2[q] || !d[q])) {
-      set_last_error("nft_amp2_vjp: a CG key without its residual / direction");
-      return NFT_ERR_ARG;
-    }
+    a.o[q] = (VT*)out[q];
+    a.o2[q] = out2 ? (VT*)out2[q] : nullptr;
+    a.d[q] = d ? (const VT*)d[q] : nullptr;
   }
   a.ls = lat_stride;
   a.shift = shift;
   a.ws = ws;
   a.wsd = (long long)(nft_amp_workspace(cst_->B) / sizeof(double));
   a.nrhs = nrhs;
+  a.nb = nb;
   a.cg = out2 != nullptr;
   a.sc = sc;
   a.part = part;
@@ -1428,14 +1085,70 @@ int nft_amp2_vjp(const nft_amp_const* cst_, const nft_amp_const* item_consts, in
   a.gps = gp_stride;
   a.gpr = gp_row;
   a.ngp = a.cg ? ngp : 0;
-  const int kg = kg_of(nrhs, item_mode, kg_env("NFT_AMP2_KV", 1));
-  const dim3 grid((unsigned)(nb * ((nrhs + kg - 1) / kg)));
-  prof_mark(stream, a.cg ? "amp_vjp_a+cg" : "amp_vjp_a");
-  NFT_AMP2_LAUNCH(vjp_a, a, item_mode, kg, grid, stream);
-  prof_mark(stream, a.cg ? "amp_vjp_b+cg" : "amp_vjp_b");
-  NFT_AMP2_LAUNCH(vjp_b, a, item_mode, kg, grid, stream);
+  const dim3 grid(grid_of(nb, nrhs));
+  prof_mark(stream, a.cg ? "amp_vjp2a+cg" : "amp_vjp2a");
+  NFT_AMP2_LAUNCH(vjp2a_kernel, VT, item_mode, grid, stream, a);
+  prof_mark(stream, a.cg ? "amp_vjp2b+cg" : "amp_vjp2b");
+  NFT_AMP2_LAUNCH(vjp2b_kernel, VT, item_mode, grid, stream, a);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int nft_amp2_jvp(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, void* const* t,
+                 const void* const* r, int64_t lat_stride, void* da, int64_t da_stride, int64_t da_elem_stride,
+                 double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift, int dtype,
+                 hipStream_t stream) {
+  if (!cst_ || !t || !da || !ws || nrhs < 1 || cst_->B < 3 || (cst_->has_flex && !t[KSPEC]) ||
+      (r && (!sc || !part)) || (dtype != 0 && dtype != 1)) {
+    set_last_error("nft_amp2_jvp: invalid arguments");
+    return NFT_ERR_ARG;
+  }
+  if (item_mode < 0 || item_mode > 2 || (item_mode != 0 && !item_consts)) {
+    set_last_error("nft_amp2_jvp: invalid item_mode / item_consts");
+    return NFT_ERR_ARG;
+  }
+  for (int q = 0; q < 6; ++q)
+    if (r && t[q] && !r[q]) {
+      set_last_error("nft_amp2_jvp: a direction key without its residual");
+      return NFT_ERR_ARG;
+    }
+  const int nb = tiles_of(cst_->B, nrhs);
+  if (!nb) return NFT_AMP2_FALLBACK;
+  if (dtype == 1)
+    return amp2_jvp_impl<float>(cst_, item_consts, item_mode, t, r, lat_stride, da, da_stride, da_elem_stride, ws,
+                                nrhs, sc, part, pstride, shift, nb, stream);
+  return amp2_jvp_impl<double>(cst_, item_consts, item_mode, t, r, lat_stride, da, da_stride, da_elem_stride, ws,
+                               nrhs, sc, part, pstride, shift, nb, stream);
+}
+
+int nft_amp2_vjp(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, const void* g,
+                 int64_t g_stride, void* const* out, void* const* out2, const void* const* d, int64_t lat_stride,
+                 double shift, double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
+                 int64_t gp_stride, int64_t gp_row, int ngp, int dtype, hipStream_t stream) {
+  if (!cst_ || !g || !out || !ws || nrhs < 1 || cst_->B < 3 || (cst_->has_flex && !out[KSPEC]) ||
+      (out2 && (!d || !sc || !part || (ngp > 0 && !gpart))) || (dtype != 0 && dtype != 1)) {
+    set_last_error("nft_amp2_vjp: invalid arguments");
+    return NFT_ERR_ARG;
+  }
+  if (item_mode < 0 || item_mode > 2 || (item_mode != 0 && !item_consts)) {
+    set_last_error("nft_amp2_vjp: invalid item_mode / item_consts");
+    return NFT_ERR_ARG;
+  }
+  for (int q = 0; q < 6; ++q)
+    if (out2 && out[q] && (!out2[q] || !d[q])) {
+      set_last_error("nft_amp2_vjp: a CG key without its residual / direction");
+      return NFT_ERR_ARG;
+    }
+  const int nb = tiles_of(cst_->B, nrhs);
+  if (!nb) return NFT_AMP2_FALLBACK;
+  if (dtype == 1)
+    return amp2_vjp_impl<float>(cst_, item_consts, item_mode, g, g_stride, out, out2, d, lat_stride, shift, ws, nrhs,
+                                sc, part, pstride, gpart, gp_stride, gp_row, ngp, nb, stream);
+  return amp2_vjp_impl<double>(cst_, item_consts, item_mode, g, g_stride, out, out2, d, lat_stride, shift, ws, nrhs,
+                               sc, part, pstride, gpart, gp_stride, gp_row, ngp, nb, stream);
 }
 
 }  // extern "C"

@@ -533,6 +533,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
       a.f = *fz;
       a.f.epi = 0;
       a.f.cg = 0;
+      a.f.quad = 0;
     }
     if ((st = launch<T>(K_R2C, true, N, a, s)) != NFT_OK) return st;
   }
@@ -983,8 +984,9 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     int st = hartley_v2<T>(in, out, g, ax, sigma, scale, ws, ws_bytes, s, &f);
     if (st != NFT_FALLBACK) return st;
   }
-  if (f.cg || f.o2h) {
-    set_last_error("nft_hartley_fused: the CG-carrying epilogue / out2 pair sums need the engine-v2 unpack pass "
+  if (f.cg || f.o2h || f.quad) {
+    set_last_error("nft_hartley_fused: the CG-carrying / quadratic-form epilogue / out2 pair sums need the "
+                   "engine-v2 unpack pass "
                    "(nft_hartley_cg_blocks == 0 for this geometry)");
     return NFT_ERR_UNSUPPORTED;
   }
@@ -1219,6 +1221,19 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
       f.cshift = fz->cg_shift;
       f.cnbtot = fz->cg_nbtot;
       f.cblk0 = fz->cg_blk0;
+    }
+    f.quad = 0;
+    if (fz->quad_part) {
+      if (f.cg || !f.ea || f.ed || f.out2 || f.P <= 0 || f.nb < 1 || fz->quad_blk0 < 0 ||
+          fz->quad_pstride < fz->quad_blk0 + nft_hartley_cg_blocks(ndim, shape, naxes, axes, dtype)) {
+        set_last_error("nft_hartley_fused: the quadratic-form epilogue needs a batch, epi_a alone and "
+                       "quad_pstride >= quad_blk0 + nft_hartley_cg_blocks");
+        return NFT_ERR_ARG;
+      }
+      f.quad = 1;
+      f.qpart = fz->quad_part;
+      f.qps = fz->quad_pstride;
+      f.qblk0 = fz->quad_blk0;
     }
   }
   const int sigma = convention == 0 ? 1 : -1;

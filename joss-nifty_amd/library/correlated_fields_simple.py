@@ -80,33 +80,17 @@ class AmpLin:
         h.has_flex, h.has_asp, h.has_zm = int(amp.has_flex), int(amp.has_asp), int(amp.has_zm)
         self.host = h
         self._rep = {}
-        self.tab = None
 
     @property
     def B(self):
         return self.host.B
 
-    def prepare(self):
-        """the two-phase kernels' tables of every row (nft_amp2_prepare: once
-        per linearisation point, on first use; sets the device structs' tab)"""
-        if self.tab is None and self.B >= 3:
-            import ctypes
-            lib = _native.load()
-            n = int(lib.nft_amp2_tab_len(self.B))
-            self.tab = torch.empty((self.k, n), dtype=torch.float64, device=self.dconst.device)
-            _native._check(lib.nft_amp2_prepare(ctypes.byref(self.host), ctypes.c_void_p(self.dconst.data_ptr()),
-                                                 self.k, ctypes.c_void_p(self.tab.data_ptr()), n,
-                                                 _native.stream_ptr()))
-        return self
-
     def row_bytes(self, r):
-        self.prepare()
         return self.dconst[r * self.size:(r + 1) * self.size]
 
     def items(self, k, row=0):
         """device pointer of k consecutive structs: row `row` shared by k
         right-hand sides"""
-        self.prepare()
         if self.k == 1 and k == 1:
             return self.dconst.data_ptr()
         key = (k, row)
@@ -273,15 +257,6 @@ class _AmplitudeModel:
         k.total_volume = self.total_vol
         k.B = self.B
         k.has_flex, k.has_asp, k.has_zm = int(self.has_flex), int(self.has_asp), int(self.has_zm)
-        if self.B >= 3:
-            # the two-phase kernels' tables of this linearisation point
-            import ctypes
-            lib = _native.load()
-            n = int(lib.nft_amp2_tab_len(self.B))
-            keep["tab"] = torch.empty(n, dtype=torch.float64, device=keep["An"].device)
-            k.tab = keep["tab"].data_ptr()
-            _native._check(lib.nft_amp2_prepare(ctypes.byref(k), None, 1, ctypes.c_void_p(k.tab), n,
-                                                 _native.stream_ptr()))
         return k, keep
 
     # ------------------------------------------------- native forward
@@ -363,7 +338,6 @@ class _AmplitudeModel:
         without per-item constants is ONE device constant set shared by every
         right-hand side (mode 2)"""
         if isinstance(const, AmpLin):
-            const.prepare()
             if item_consts is None:
                 return const.host, const.items(1), 2
             return const.host, item_consts, 1
@@ -378,12 +352,16 @@ class _AmplitudeModel:
         ws = _native.workspace(k * lib.nft_amp_workspace(self.B), D.device, "amp")
         P = ctypes.c_void_p
         host, ic, mode = self._item_mode(const, item_consts)
+        if da.dtype != D.dtype:
+            raise _native.NativeError("native_jvp_batched: da and D dtypes differ")
         st = lib.nft_amp2_jvp(ctypes.byref(host), P(ic), mode, self._key_ptrs(D, off), None, size, P(da.data_ptr()),
                               1 if interleave else self.B, k if interleave else 1, P(ws.data_ptr()), k, None, None,
-                              0, 0.0, _native.stream_ptr())
+                              0, 0.0, _native.dtype_code(D.dtype), _native.stream_ptr())
         if st != _native.AMP2_FALLBACK:
             _native._check(st)
             return da
+        if D.dtype != torch.float64:
+            raise _native.NativeError("the multi-kernel amplitude JVP is fp64 only (NFT_AMP2=0 with fp32 storage)")
         at = self._ptrs(D, off)
         if mode == 2:
             ic = const.items(k)
@@ -402,12 +380,16 @@ class _AmplitudeModel:
         P = ctypes.c_void_p
         host, ic, mode = self._item_mode(const, item_consts)
         dk = self._key_ptrs(D, off) if (D is not None and shift != 0.0) else None
+        if g.dtype != Q.dtype or (D is not None and D.dtype != Q.dtype):
+            raise _native.NativeError("native_vjp_batched: g, Q and D dtypes differ")
         st = lib.nft_amp2_vjp(ctypes.byref(host), P(ic), mode, P(g.data_ptr()), self.B, self._key_ptrs(Q, off), None,
                               dk, size, float(shift), P(ws.data_ptr()), k, None, None, 0, None, 0, 0, 0,
-                              _native.stream_ptr())
+                              _native.dtype_code(Q.dtype), _native.stream_ptr())
         if st != _native.AMP2_FALLBACK:
             _native._check(st)
             return Q
+        if Q.dtype != torch.float64:
+            raise _native.NativeError("the multi-kernel amplitude VJP is fp64 only (NFT_AMP2=0 with fp32 storage)")
         if mode == 2:
             ic = const.items(k)
         atq = self._ptrs(Q, off)
@@ -443,7 +425,7 @@ class _AmplitudeModel:
         _native._check(lib.nft_amp2_jvp(ctypes.byref(host), P(ic), mode, self._key_ptrs(D, off),
                                         self._key_ptrs(R, off), size, P(da.data_ptr()), 1, k, P(ws.data_ptr()), k,
                                         P(SC.data_ptr()), P(part.data_ptr()), int(pstride), float(shift),
-                                        _native.stream_ptr()))
+                                        _native.dtype_code(D.dtype), _native.stream_ptr()))
         return da
 
     def native_vjp_cg(self, const, g, X, R, D, off, SC, part, pstride, gpart, gp_stride, gp_row, ngp, shift):
@@ -460,7 +442,7 @@ class _AmplitudeModel:
                                         self._key_ptrs(X, off), self._key_ptrs(R, off), self._key_ptrs(D, off), size,
                                         float(shift), P(ws.data_ptr()), k, P(SC.data_ptr()), P(part.data_ptr()),
                                         int(pstride), P(gpart.data_ptr()), int(gp_stride), int(gp_row), int(ngp),
-                                        _native.stream_ptr()))
+                                        _native.dtype_code(X.dtype), _native.stream_ptr()))
 
     def native_jvp(self, const, t, da):
         if isinstance(const, AmpLin):
@@ -667,9 +649,9 @@ class CFJacobian(LinearOperator):
         every stage launched once for the whole batch (nft_*_batched; the LOS
         matrix is streamed once for all rows).  Per row bitwise equal to
         metric_flat."""
-        if D.dtype == torch.float32:
+        if D.dtype == torch.float32 and not self.phases_fp32(D.shape[0]):
             if qpart is not None:
-                raise NotImplementedError("data-space curvature partials: fp64 only")
+                raise NotImplementedError("data-space curvature partials: fp32 needs the two-phase amplitude kernels")
             return self._metric_flat_batch32(D, Q, W, shift)
         da = self.mv_amp_jvp(D)
         w = self.mv_grid(D, da, Q, W, shift, qpart)
@@ -681,21 +663,47 @@ class CFJacobian(LinearOperator):
     # alone, so a caller may run them on a second stream next to the grid
     # segment's CG work (fused_cg.FusedCGBatch).  Their buffers persist per
     # batch size: no allocation is freed while another stream may use it.
-    def _mv_bufs(self, k):
+    def _mv_bufs(self, k, dtype=torch.float64):
+        """the phases' buffers for k rows of storage dtype (fp64, or fp32 for
+        the fp32-storage CG: every grid operand and dA in fp32)"""
         bufs = getattr(self, "_mvb", None)
-        if bufs is None or bufs["k"] != k:
+        if bufs is None or bufs["k"] != k or bufs["dt"] != dtype:
             grid = tuple(self._afull.shape)
-            dt = self._afull.dtype
+            dt = dtype
             B = self._m.amp.B
             fold = self._m.jbins.fold
             wshape = self._half(grid) if self._pairs(k) else grid
-            bufs = self._mvb = dict(k=k, da=torch.empty((B, k), dtype=torch.float64, device=self.device),
+            bufs = self._mvb = dict(k=k, dt=dtype, da=torch.empty((B, k), dtype=dt, device=self.device),
                                     s=torch.empty((k,) + grid, dtype=dt, device=self.device),
                                     w=torch.empty((k,) + wshape, dtype=dt, device=self.device),
                                     wf=torch.empty((k, fold["nf"]) if fold else (1,), dtype=dt,
                                                    device=self.device),
                                     ga=torch.empty((k, B), dtype=dt, device=self.device))
         return bufs
+
+    def _grid_ops(self, dtype):
+        """(A_full, xi0) in the storage dtype (fp32 copies made once)"""
+        if dtype == self._afull.dtype:
+            return self._afull, self._xi0
+        c = self.__dict__.setdefault("_g32", {})
+        if dtype not in c:
+            c[dtype] = (self._afull.to(dtype), self._xi0.to(dtype))
+        return c[dtype]
+
+    def _weight(self, W, dtype):
+        """a pointwise weight tensor in the storage dtype (cached per tensor)"""
+        if not torch.is_tensor(W) or W.dtype == dtype:
+            return W
+        c = self.__dict__.setdefault("_w32", {})
+        key = (W.data_ptr(), dtype)
+        if key not in c:
+            c[key] = W.to(dtype).contiguous()
+        return c[key]
+
+    def phases_fp32(self, k):
+        """True if the phase methods (mv_*) run on fp32 storage: the
+        two-phase amplitude kernels apply (nft_amp2_* with dtype 1)"""
+        return self.amp2_tiles(k) > 0
 
     @staticmethod
     def _half(grid):
@@ -713,7 +721,7 @@ class CFJacobian(LinearOperator):
         prologue's bin gather reads one contiguous run per pixel for all k"""
         m = self._m
         k = D.shape[0]
-        da = self._mv_bufs(k)["da"]
+        da = self._mv_bufs(k, D.dtype)["da"]
         m.amp.native_jvp_batched(self._const(), D, dict(zip(self.layout.keys, self.layout.offsets)), da,
                                  interleave=True)
         return da
@@ -728,7 +736,7 @@ class CFJacobian(LinearOperator):
         tile) and dA (B, k) of the updated D, bin-major interleaved"""
         m = self._m
         k = D.shape[0]
-        da = self._mv_bufs(k)["da"]
+        da = self._mv_bufs(k, D.dtype)["da"]
         return m.amp.native_jvp_dir(self._const(), D, R, dict(zip(self.layout.keys, self.layout.offsets)), da, SC,
                                     part, pstride, shift)
 
@@ -737,7 +745,7 @@ class CFJacobian(LinearOperator):
         the iteration's finalize (no q is stored)"""
         m = self._m
         k = X.shape[0]
-        ga = self._mv_bufs(k)["ga"]
+        ga = self._mv_bufs(k, X.dtype)["ga"]
         m.jbins.scatter_from(self.mv_fold(w), ga, k)
         m.amp.native_vjp_cg(self._const(), ga, X, R, D, dict(zip(self.layout.keys, self.layout.offsets)), SC, part,
                             pstride, gpart, gp_stride, gp_row, ngp, shift)
@@ -750,6 +758,15 @@ class CFJacobian(LinearOperator):
             grid = tuple(self._afull.shape)
             cache[k] = _native.hartley_cg_blocks((k,) + grid, tuple(range(1, 1 + len(grid))), self._afull.dtype)
         return cache[k]
+
+    def pointwise_quad_blocks(self, W):
+        """partials per RHS of (J d).W(J d) formed by the forward transform's
+        epilogue for a pointwise weight W (a grid-shaped tensor of the grid's
+        dtype), 0 where that epilogue does not apply"""
+        if not (torch.is_tensor(W) and W.dtype in (torch.float64, torch.float32)
+                and tuple(W.shape) == tuple(self._afull.shape) and W.is_contiguous() and W.device == self.device):
+            return 0
+        return self.cg_blocks(1)
 
     def dir_blocks(self, k):
         """d.d partial blocks of the CG direction carried by the folded
@@ -770,25 +787,34 @@ class CFJacobian(LinearOperator):
         m = self._m
         lay = self.layout
         k, size = D.shape
-        bufs = self._mv_bufs(k)
-        grid = tuple(self._afull.shape)
-        N = self._afull.numel()
+        bufs = self._mv_bufs(k, D.dtype)
+        afull, xi0 = self._grid_ops(D.dtype)
+        W = self._weight(W, D.dtype)
+        grid = tuple(afull.shape)
+        N = afull.numel()
         xo = dict(zip(lay.keys, lay.offsets))[m.k_xi]
         axes = tuple(range(1, 1 + len(grid)))
         conv = hartley_convention_code()
         s = bufs["s"]
-        pro = dict(a=self._afull, x=D[0, xo:], b=self._xi0, **self._pro_bins(da, k))
+        pro = dict(a=afull, x=D[0, xo:], b=xi0, **self._pro_bins(da, k))
         if pro_dir is not None:
             pro["dir"] = pro_dir
-        _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape,
-                              batch=dict(period=N, x=size, c=1, c_elem=k))
-        g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
-        g = g.contiguous()
+        bt = dict(period=N, x=size, c=1, c_elem=k)
+        if qpart is not None and torch.is_tensor(W):
+            # pointwise W inside the forward's last pass: s = W * (J d) and
+            # the per-tile partials of (J d).W(J d) (nft_hartley_fuse.quad_*)
+            _native.hartley_fused(s, axes, m.c_h, pro=pro, epi=dict(a=W), convention=conv, shape=s.shape,
+                                  batch=bt, quad=dict(part=qpart, pstride=qpart.stride(0)))
+            g = s
+        else:
+            _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape, batch=bt)
+            g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
+            g = g.contiguous()
         if after_w is not None:
             after_w()
         w = bufs["w"]
         pairs = self._pairs(k)
-        epi = dict(a=self._afull, b=self._xi0, out2=w, pairs=pairs)
+        epi = dict(a=afull, b=xi0, out2=w, pairs=pairs)
         bt = dict(period=N, out=size, out2=w[0].numel())
         if shift != 0.0:
             epi.update(d=D[0, xo:], shift=shift)
@@ -800,14 +826,14 @@ class CFJacobian(LinearOperator):
     def mv_fold(self, w):
         """the mirror fold of w (the bandwidth-bound half of the bin sums)"""
         k = w.shape[0]
-        return self._m.jbins.fold_into(w, self._mv_bufs(k)["wf"], k, half=self._pairs(k))
+        return self._m.jbins.fold_into(w, self._mv_bufs(k, w.dtype)["wf"], k, half=self._pairs(k))
 
     def mv_amp_vjp(self, D, w, Q, shift=0.0, folded=None):
         """bin sums of w (folded: mv_fold's result, if already formed) and the
         amplitude VJP into Q's amplitude keys"""
         m = self._m
         k = Q.shape[0]
-        ga = self._mv_bufs(k)["ga"]
+        ga = self._mv_bufs(k, Q.dtype)["ga"]
         m.jbins.scatter_from(self.mv_fold(w) if folded is None else folded, ga, k)
         m.amp.native_vjp_batched(self._const(), ga, Q, dict(zip(self.layout.keys, self.layout.offsets)), D, shift)
         return Q

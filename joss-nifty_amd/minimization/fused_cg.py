@@ -173,11 +173,21 @@ CHUNK = os.environ.get("NFT_CG_CHUNK", "1") != "0"
 
 def _quad_blocks(core, W, dtype, controllers=()):
     """partials per RHS of the metric's data-space quadratic form, or 0"""
-    if not CURV_DATA or dtype != torch.float64 or not callable(W):
+    if not CURV_DATA or dtype not in (torch.float64, torch.float32):
+        return 0
+    if dtype == torch.float32 and not (hasattr(core, "phases_fp32") and core.phases_fp32(1)):
+        # fp32 storage: the data-space curvature rides in the carried
+        # iteration only (its amplitude keys in the two-phase kernels)
         return 0
     if not CURV_DATA_VALUE and not all(_count_only(c) for c in controllers):
         return 0
     if not getattr(core, "supports_quad", False):
+        return 0
+    if torch.is_tensor(W):
+        # pointwise W (Gaussian / Poisson): the forward transform's epilogue
+        f = getattr(core, "pointwise_quad_blocks", None)
+        return int(f(W)) if f is not None else 0
+    if not callable(W):
         return 0
     return int(getattr(W, "quad_blocks", 0) or 0)
 
@@ -341,8 +351,15 @@ class _CarryIteration:
         self.UP = torch.empty((k, 3 * self.nbtot), dtype=torch.float64, device=dev)
 
     @staticmethod
-    def supported(core, k):
-        return _CARRY and hasattr(core, "cg_blocks") and core.cg_blocks(k) > 0
+    def supported(core, k, dtype=torch.float64):
+        if not (_CARRY and hasattr(core, "cg_blocks") and core.cg_blocks(k) > 0):
+            return False
+        if dtype == torch.float64:
+            return True
+        # fp32 storage: only the two-phase amplitude flavour (its segment
+        # kernels are dtype-generic; the separate segment passes are fp64)
+        return (dtype == torch.float32 and _AMP2 and _CARRY_DIR and hasattr(core, "amp2_tiles")
+                and core.amp2_tiles(k) > 0 and hasattr(core, "dir_blocks") and core.dir_blocks(k) > 0)
 
     def _call_amp2(self, X, Rr, D, Q, SC):
         core, lib = self.core, self.lib
@@ -540,7 +557,7 @@ class FusedCGBatch(FusedCG):
             st["Q"] = torch.zeros_like(X)
             st["AX"] = None
             st["split"] = None
-            carry = bool(nq) and X.dtype == torch.float64 and _CarryIteration.supported(core, k)
+            carry = bool(nq) and _CarryIteration.supported(core, k, X.dtype)
             # x.b from the update kernel (b streamed) or from a dot beside
             # the carried iteration
             st["Bu"] = Bv if (need_value and not carry) else None

@@ -99,8 +99,6 @@ from ..library.correlated_fields_simple import _O2_PAIRS, _PRO_FOLD  # noqa: E40
 def _items(st, k):
     """device nft_amp_const array for k right-hand sides: the state's own rows,
     or its single linearisation point shared by all k"""
-    for ln in st["lins"]:
-        ln.prepare()   # (stack() copied prepared rows; a fresh state's are prepared here)
     if st["k"] != 1 or k == 1:
         return st["dconst"].data_ptr()
     rep = st.setdefault("rep", {})

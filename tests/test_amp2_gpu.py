@@ -119,7 +119,6 @@ def test_amp2_per_item_constants(ift, restore):
     B = amp.B
     g = torch.randn((3, B), dtype=torch.float64, device=D.device)
     da = torch.empty((B, 3), dtype=torch.float64, device=D.device)
-    lb.prepare()   # the two-phase kernels' tables of every row (a raw item pointer bypasses AmpLin)
     amp.native_jvp_batched(lb.host, D, off, da, interleave=True, item_consts=lb.dconst.data_ptr())
     Q = torch.zeros_like(D)
     amp.native_vjp_batched(lb.host, g, Q, off, item_consts=lb.dconst.data_ptr())

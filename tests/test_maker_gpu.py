@@ -207,29 +207,67 @@ def test_unit_and_constant_zero_mode(ift, shape, flex_asp, matern):
     np.testing.assert_allclose(float(cf(r).s_integrate()), 0., atol=1e-8)
 
 
-def test_maker_statistics_and_realized(ift):
-    """statistics_summary draws prior samples through every fluctuation
-    operator; the *_realized estimators run on product-domain samples
-    (testAmplitudesInvariants, test_correlated_fields.py:151-210, at a size
-    the statistics settle)."""
-    sspace = ift.RGSpace((32, 32), distances=0.2)
-    fsspace = ift.RGSpace(24, distances=0.5)
-    astds = (0.2, 1.2)
+def _stats(ift, op, samples):
+    sc = ift.StatCalculator()
+    for s in samples:
+        sc.add(op(s.extract(op.domain)))
+    return sc.mean.val_np(), sc.var.ptw("sqrt").val_np()
+
+
+@pytest.mark.parametrize("sshape", [(8,), (12, 10)])
+def test_amplitudes_invariants(ift, sshape):
+    """testAmplitudesInvariants (test_correlated_fields.py:147-210, N = 0):
+    the prior statistics of total / average / slice fluctuation and offset
+    operators agree with the *_realized estimates on field samples, and
+    moment_slice_to_average recovers the slice fluctuation."""
+    sspace = ift.RGSpace(sshape, distances=0.3)
+    fsspace = ift.RGSpace((12,), (0.4,))
+    astds = 0.2, 1.2
+    offset_std_mean = 1.3
     fa = ift.CorrelatedFieldMaker('')
     fa.add_fluctuations(sspace, (astds[0], 1e-2), (1.1, 2.), (2.1, .5), (-2, 1.), 'spatial')
     fa.add_fluctuations(fsspace, (astds[1], 1e-2), (3.1, 1.), (.5, .1), (-4, 1.), 'freq')
-    fa.set_amplitude_total_offset(0., (1e-2, 1e-6))
-    op = fa.finalize(prior_info=3)
-    samples = [op(_rand_mf(ift, op.domain, 1000 + i)) for i in range(60)]
-    tot = fa.total_fluctuation_realized(samples)
-    sp = fa.average_fluctuation_realized(samples, 0)
-    fr = fa.average_fluctuation_realized(samples, 1)
-    np.testing.assert_allclose(sp, astds[0], rtol=0.5)
-    np.testing.assert_allclose(fr, astds[1], rtol=0.5)
-    np.testing.assert_allclose(tot, np.sqrt((1 + astds[0] ** 2) * (1 + astds[1] ** 2) - 1), rtol=0.5)
-    zm = fa.offset_amplitude_realized(samples)
-    assert np.all(np.isfinite(zm))
-    s0 = fa.slice_fluctuation_realized(samples, 0)
-    assert np.all(np.isfinite(s0))
-    m = fa.moment_slice_to_average(0.5, nsamples=50)
-    assert 0. < m < 0.5
+    fa.set_amplitude_total_offset(1.2, (offset_std_mean, 1e-2))
+    op = fa.finalize(prior_info=2)
+    samples = [_rand_mf(ift, op.domain, 500 + i) for i in range(100)]
+    tot_flm, _ = _stats(ift, fa.total_fluctuation, samples)
+    offset_amp_std, _ = _stats(ift, fa.amplitude_total_offset, samples)
+    fl0, _ = _stats(ift, fa.average_fluctuation(0), samples)
+    fl1, _ = _stats(ift, fa.average_fluctuation(1), samples)
+    sl0, _ = _stats(ift, fa.slice_fluctuation(0), samples)
+    sl1, _ = _stats(ift, fa.slice_fluctuation(1), samples)
+    sams = [op(s) for s in samples]
+    np.testing.assert_allclose(offset_amp_std, fa.offset_amplitude_realized(sams), rtol=0.5)
+    np.testing.assert_allclose(fl0, fa.average_fluctuation_realized(sams, 0), rtol=0.5)
+    np.testing.assert_allclose(fl1, fa.average_fluctuation_realized(sams, 1), rtol=0.5)
+    np.testing.assert_allclose(tot_flm, fa.total_fluctuation_realized(sams), rtol=0.5)
+    np.testing.assert_allclose(sl0, fa.slice_fluctuation_realized(sams, 0), rtol=0.5)
+    np.testing.assert_allclose(sl1, fa.slice_fluctuation_realized(sams, 1), rtol=0.5)
+
+    fa = ift.CorrelatedFieldMaker('')
+    fa.set_amplitude_total_offset(0., (offset_std_mean, .1))
+    fa.add_fluctuations(fsspace, (astds[1], 1.), (3.1, 1.), (.5, .1), (-4, 1.), 'freq')
+    m = 3.
+    x = fa.moment_slice_to_average(m, nsamples=300)
+    fa.add_fluctuations(sspace, (x, 1.5), (1.1, 2.), (2.1, .5), (-2, 1.), 'spatial', 0)
+    op = fa.finalize(prior_info=0)
+    em, _ = _stats(ift, fa.slice_fluctuation(0), samples)
+    np.testing.assert_allclose(m, em, rtol=0.5)
+    assert op.target[-2] == sspace
+    assert op.target[-1] == fsspace
+    # Jacobian consistency of the normalised amplitudes and the field
+    for ampl in list(fa.get_normalized_amplitudes()) + [op]:
+        x0 = _rand_mf(ift, ampl.domain, 9)
+        x0 = ift.MultiField.from_dict({k: x0[k] * 0.1 for k in x0.keys()})
+        lin = _lin(ift, ampl, x0)
+        t = _rand_mf(ift, ampl.domain, 10)
+        g = ift.makeField(ampl.target, np.random.default_rng(11).standard_normal(ampl.target.shape))
+        lhs = _vdot(lin.jac(t), g)
+        rhs = _vdot(t, lin.jac.adjoint(g))
+        assert abs(lhs - rhs) <= 1e-10 * max(abs(lhs), 1.)
+        eps = 1e-6
+        xp = ift.MultiField.from_dict({k: x0[k] + t[k] * eps for k in x0.keys()})
+        xm = ift.MultiField.from_dict({k: x0[k] - t[k] * eps for k in x0.keys()})
+        fd = (ampl(xp).val - ampl(xm).val) / (2 * eps)
+        jt = lin.jac(t).val
+        assert float(torch.linalg.norm(fd - jt)) <= 1e-5 * max(float(torch.linalg.norm(jt)), 1e-3)
