@@ -207,7 +207,7 @@ def cg_iteration(lib, core, W, shift, bufs, k):
     dt = _native.dtype_code(X.dtype)
     nq = _quad_blocks(core, W, X.dtype)
     from nifty_amd.minimization.fused_cg import _CarryIteration
-    if nq and X.dtype == torch.float64 and _CarryIteration.supported(core, k):
+    if nq and _CarryIteration.supported(core, k, X.dtype):
         # FusedCGBatch's iteration: the grid segment's update inside the
         # adjoint transform's epilogue (no b stream: count-only controllers)
         key = (id(core), k, n)

@@ -296,11 +296,14 @@ typedef struct nft_hartley_fuse {
  * or 0 when its last pass cannot carry the update. */
 int nft_hartley_cg_blocks(int ndim, const int64_t* shape, int naxes, const int* axes, int dtype);
 
-/* Blocks of the folded prologue over an item grid of ndim (1..3) axes: the
- * fundamental cell prod(n_a / 2 + 1) with its last axis padded to a multiple
- * of 64 (every wave starts a row chunk aligned), 256 cells per block -- the
+/* Blocks of the folded prologue over an item grid of ndim (1..3) axes -- the
  * number of dir_part entries per item of nft_hartley_fuse.dir_*; 0 for a bad
- * shape. */
+ * shape.  ndim >= 2 with n_last / 2 + 1 <= 2560: one block per group of
+ * mirror rows, prod over the first ndim - 1 axes of (n_a / 2 + 1) (the
+ * row-staged prologue: the cell row's dA runs in LDS, every row streamed
+ * with aligned loads and stores); otherwise the fundamental cell
+ * prod(n_a / 2 + 1) with its last axis padded to a multiple of 64, 256 cells
+ * per block. */
 int nft_hartley_dir_blocks(int ndim, const int64_t* shape);
 
 int nft_hartley_fused_workspace(int ndim, const int64_t* shape, int naxes, const int* axes,

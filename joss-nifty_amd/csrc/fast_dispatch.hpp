@@ -15,6 +15,8 @@ namespace fast {
 // threads per workgroup for a pass of length N
 constexpr int nt_rows(int N) { return N <= 2048 ? 256 : (N == 4096 ? 512 : 1024); }
 // strided: aim for >= 16 adjacent columns per tile
+// (N = 512 with 512 threads -- 8-line tiles, two workgroups per CU -- measured
+// slower at 512^3: C4 iteration 14.2 -> 15.1 ms)
 constexpr int nt_strided(int N) { return N <= 128 ? 256 : (N == 256 ? 512 : 1024); }
 
 inline bool is_pow2(long long n) { return n > 0 && (n & (n - 1)) == 0; }
@@ -95,7 +97,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     // plain epilogue (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us), faster
     // for the CG-carrying epilogue, which is bound by its HBM traffic (the
     // contiguous flavour, 231 -> 221 us): that pass only
-    const int mode = (f.cg || f.quad) ? 2 : 0;
+    const int mode = f.cg ? 2 : 0;
     if (mode > 0 && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) {
       b.bgroup = f.nb;
       b.bmode = mode;

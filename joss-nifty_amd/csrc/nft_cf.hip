@@ -410,8 +410,16 @@ __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, 
                                                       long long npix, long long nbins, int nchunks) {
   static_assert(CH % 256 == 0, "bin_scatter_il loads CH / 256 positions per thread");
   constexpr int PER = CH / 256;
+  // bins of more than LONGB positions (3-D grids: thousands of cells per
+  // |k| shell at high k) are summed by one wave each -- lane-strided
+  // partials, then a fixed shuffle tree -- instead of one thread's serial
+  // chain of gathers; shorter bins keep the sequential sum (2-D grids: no
+  // bin is that long, the sums are unchanged)
+  constexpr int LONGB = 256;
   __shared__ T vals[PRE][CH];
   __shared__ int bnd[2];
+  __shared__ int nlong;
+  __shared__ int longb[CH / LONGB + 1];
   const int per = (nchunks + NXCD - 1) / NXCD;
   const int c = (int)(blockIdx.x % NXCD) * per + (int)(blockIdx.x / NXCD);
   if (c >= nchunks) return;
@@ -429,6 +437,7 @@ __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, 
   for (int i = 0; i < PER; ++i)
 #pragma unroll
     for (int p = 0; p < PRE; ++p) v[i][p] = t + i * 256 < n ? in[(long long)pv[i] * PRE + p] : (T)0;
+  if (t == 0) nlong = 0;
   if (t < 2) {
     // first bin whose start offset is >= j0 (+ CH)
     const long long target = j0 + (t ? CH : 0);
@@ -449,6 +458,10 @@ __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, 
   const int b0 = bnd[0], b1 = bnd[1];
   for (int b = b0 + t; b < b1; b += 256) {
     const long long a = offs[b], e = offs[b + 1];
+    if (e - a > LONGB) {
+      longb[atomicAdd(&nlong, 1)] = b;  // list order is irrelevant: one bin per entry
+      continue;
+    }
     T acc[PRE];
 #pragma unroll
     for (int p = 0; p < PRE; ++p) acc[p] = (T)0;
@@ -464,6 +477,32 @@ __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, 
     }
 #pragma unroll
     for (int p = 0; p < PRE; ++p) out[p * nbins + b] = acc[p];
+  }
+  __syncthreads();
+  const int w = t >> 6, lane = t & 63;
+  for (int i = w; i < nlong; i += 4) {
+    const int b = longb[i];
+    const long long a = offs[b], e = offs[b + 1];
+    T acc[PRE];
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) acc[p] = (T)0;
+    for (long long j = a + lane; j < e; j += 64) {
+      if (j - j0 < CH) {
+#pragma unroll
+        for (int p = 0; p < PRE; ++p) acc[p] += vals[p][j - j0];
+      } else {
+        const long long q = (long long)perm[j] * PRE;
+#pragma unroll
+        for (int p = 0; p < PRE; ++p) acc[p] += in[q + p];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) {
+      T v = acc[p];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if (lane == 0) out[p * nbins + b] = v;
+    }
   }
 }
 

@@ -902,6 +902,207 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
   }
 }
 
+// Row-staged folded prologue (D >= 2): one workgroup per group of mirror
+// rows -- the 2^(D-1) rows (over the first D-1 axes) that share one row of
+// fundamental cells.  The dA runs of that cell row are gathered once into LDS
+// (one gather per cell, as pro_fold_kernel), then every row of the group is
+// streamed position by position: x, r, A, xi0 loads and d, u stores are
+// contiguous, cache-line-aligned runs (pro_fold_kernel's mirrored images
+// cross a line boundary in every wave, PMC 1.2x of the algorithmic bytes).
+// Same arithmetic per element (bitwise u and d); the d.d partials are per
+// row group (nft_hartley_dir_blocks).
+#ifndef NFT_PRO_ROWS
+#define NFT_PRO_ROWS 1  // A/B build knob (0: pro_fold_kernel everywhere)
+#endif
+__host__ __device__ inline bool pro_rows_ok(int D, long long nlast) { return D >= 2 && nlast / 2 + 1 <= 2560; }
+
+template <typename T, int D, int NBM, bool PI>
+__global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __restrict__ u, long long P, int nb) {
+  extern __shared__ __align__(16) unsigned char pro_smem[];
+  T* cvs = (T*)pro_smem;  // [hl][NBM]: the dA run of every cell of the row
+  const T* __restrict__ px = (const T*)f.px;
+  const T* __restrict__ pa = (const T*)f.pa;
+  const T* __restrict__ pb = (const T*)f.pb;
+  const T* __restrict__ pc = (const T*)f.pc;
+  using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
+  const bool vec = f.ce == nb && f.sc == 1 && (nb & 1) == 0 && nb <= NBM;
+  const bool dirc = f.dr != nullptr;
+  T* pd = const_cast<T*>(px);
+  const T* __restrict__ pr = (const T*)f.dr;
+  T bt[NBM];
+  bool live[NBM];
+  double dd[NBM];
+#pragma unroll
+  for (int b = 0; b < NBM; ++b) {
+    dd[b] = 0.0;
+    bt[b] = (T)0;
+    live[b] = false;
+    if (dirc && b < nb) {
+      const double* scb = f.dsc + b * NFT_CG_NSCALARS;
+      live[b] = scb[NFT_CG_DONE] == 0.0;
+      double beta = scb[NFT_CG_GAMMA] / scb[NFT_CG_GPREV];
+      if (!(beta > 0.0)) beta = 0.0;
+      bt[b] = (T)beta;
+    }
+  }
+  unsigned nn[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) nn[a] = (unsigned)f.fn[a];
+  const unsigned n = nn[D - 1], hl = n / 2 + 1;
+  unsigned cc[D];
+  {
+    unsigned rest = blockIdx.x;
+#pragma unroll
+    for (int a = D - 2; a >= 0; --a) {
+      const unsigned h = nn[a] / 2 + 1;
+      const unsigned q = rest / h;
+      cc[a] = rest - q * h;
+      rest = q;
+    }
+  }
+  unsigned cell0 = 0;
+#pragma unroll
+  for (int a = 0; a < D - 1; ++a) cell0 = cell0 * (nn[a] / 2 + 1) + cc[a];
+  cell0 *= hl;
+  const int tid = threadIdx.x;
+  for (unsigned c1 = tid; c1 < hl; c1 += 256) {
+    const long long ix = (long long)f.pidx[cell0 + c1] * f.ce;
+    T cv[NBM];
+#pragma unroll
+    for (int b = 0; b < NBM; ++b) cv[b] = (T)0;
+    if (vec) {
+      const V2* q = (const V2*)(pc + ix);
+#pragma unroll
+      for (int bp = 0; bp < NBM / 2; ++bp)
+        if (2 * bp < nb) {
+          const V2 c2 = q[bp];
+          cv[2 * bp] = c2.x;
+          cv[2 * bp + 1] = c2.y;
+        }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NBM; ++b)
+        if (b < nb) cv[b] = pc[b * f.sc + ix];
+    }
+#pragma unroll
+    for (int b = 0; b < NBM; ++b) cvs[c1 * NBM + b] = cv[b];
+  }
+  __syncthreads();
+  constexpr int NROW = 1 << (D - 1);
+  constexpr int NA = PI ? NBM : 1;
+  constexpr int PRO_RG = NBM <= 2 ? 4 : (NBM == 4 ? 2 : 1);  // positions per thread per load group
+#pragma unroll 1
+  for (int m = 0; m < NROW; ++m) {
+    // row m of the group: bit a of m flips axis a (skipped when self-mirror)
+    unsigned rb = 0;
+    bool dup = false;
+#pragma unroll
+    for (int a = 0; a < D - 1; ++a) {
+      unsigned k = cc[a];
+      if ((m >> a) & 1) {
+        const unsigned km = k == 0 ? 0 : nn[a] - k;
+        if (km == k) dup = true;
+        k = km;
+      }
+      rb = rb * nn[a] + k;
+    }
+    if (dup) continue;
+    rb *= n;
+#pragma unroll 1
+    for (unsigned p0 = 0; p0 < n; p0 += 256 * PRO_RG) {
+      // every load of the group before its first store (d is stored back
+      // into the array x is read from)
+      T av[PRO_RG][NA], bv[PRO_RG][NA], xv[PRO_RG][NBM], rv[PRO_RG][NBM];
+      bool ok[PRO_RG];
+#pragma unroll
+      for (int i = 0; i < PRO_RG; ++i) {
+        const unsigned pos = p0 + i * 256 + tid;
+        ok[i] = pos < n;
+        const unsigned j = rb + pos;
+#pragma unroll
+        for (int b = 0; b < NA; ++b) {
+          av[i][b] = (T)1;
+          bv[i][b] = (T)0;
+          if (ok[i] && b < nb) {
+            if (pa) av[i][b] = pa[b * f.sa + j];
+            bv[i][b] = pb[b * f.sb + j];
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < NBM; ++b) {
+          xv[i][b] = rv[i][b] = (T)0;
+          if (ok[i] && b < nb) {
+            xv[i][b] = px[b * f.sx + j];
+            if (dirc && live[b]) rv[i][b] = pr[b * f.sx + j];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < PRO_RG; ++i) {
+        if (!ok[i]) continue;
+        const unsigned pos = p0 + i * 256 + tid;
+        const unsigned j = rb + pos;
+        const unsigned c1 = pos == 0 ? 0 : (pos <= n - pos ? pos : n - pos);
+#pragma unroll
+        for (int b = 0; b < NBM; ++b) {
+          if (b >= nb) break;
+          T v = xv[i][b];
+          if (dirc && live[b]) {
+            v = bt[b] * v + rv[i][b];
+            pd[b * f.sx + j] = v;
+            dd[b] += (double)v * (double)v;
+          }
+          if (pa) v *= av[i][PI ? b : 0];
+          v += bv[i][PI ? b : 0] * cvs[c1 * NBM + b];
+          u[b * P + j] = v;
+        }
+      }
+    }
+  }
+  if (dirc) {
+    __shared__ double dsh[4][NBM];
+#pragma unroll
+    for (int b = 0; b < NBM; ++b) {
+      double v = dd[b];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if ((threadIdx.x & 63) == 0) dsh[threadIdx.x >> 6][b] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)nb && threadIdx.x < (unsigned)NBM) {
+      const int b = threadIdx.x;
+      const double t = ((dsh[0][b] + dsh[1][b]) + dsh[2][b]) + dsh[3][b];
+      f.dpart[b * f.dps + f.dblk0 + blockIdx.x] = live[b] ? f.dshift * t : 0.0;
+    }
+  }
+}
+
+template <typename T, int D, int NBM, bool PI>
+static void launch_pro_rows_n(const fast::FuseArgs& f, T* u, hipStream_t s) {
+  long long nrg = 1;
+  for (int a = 0; a < D - 1; ++a) nrg *= f.fn[a] / 2 + 1;
+  const size_t lds = (size_t)(f.fn[D - 1] / 2 + 1) * NBM * sizeof(T);
+  if (lds > 65536) {
+    static bool set = false;
+    if (!set) {
+      (void)hipFuncSetAttribute((const void*)pro_rows_kernel<T, D, NBM, PI>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      set = true;
+    }
+  }
+  hipLaunchKernelGGL((pro_rows_kernel<T, D, NBM, PI>), dim3((unsigned)nrg), dim3(256), lds, s, f, u, f.P, f.nb);
+}
+
+template <typename T, int D, bool PI>
+static void launch_pro_rows(const fast::FuseArgs& f, T* u, hipStream_t s) {
+  if (f.nb <= 2)
+    launch_pro_rows_n<T, D, 2, PI>(f, u, s);
+  else if (f.nb <= 4)
+    launch_pro_rows_n<T, D, 4, PI>(f, u, s);
+  else
+    launch_pro_rows_n<T, D, 8, PI>(f, u, s);
+}
+
 template <typename T, int D, bool PI>
 static void launch_pro_fold_pi(const fast::FuseArgs& f, T* u, long long ncell, hipStream_t s) {
   const dim3 grid((unsigned)((ncell + 255) / 256));
@@ -961,7 +1162,13 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
       long long ncell = 1;  // padded cell grid (pro_fold_kernel)
       for (int a = 0; a < f.fnd; ++a) ncell *= a == f.fnd - 1 ? ((f.fn[a] / 2 + 1 + 63) & ~63LL) : f.fn[a] / 2 + 1;
       prof_mark(s, f.dr ? "pro_fold+dir" : "pro_fold");
-      if (f.fnd == 1)
+      const bool rows = NFT_PRO_ROWS && pro_rows_ok(f.fnd, f.fn[f.fnd - 1]) && f.nb <= 8;
+      const bool pi = f.sa != 0 || f.sb != 0;
+      if (rows && f.fnd == 2)
+        pi ? launch_pro_rows<T, 2, true>(f, u, s) : launch_pro_rows<T, 2, false>(f, u, s);
+      else if (rows && f.fnd == 3)
+        pi ? launch_pro_rows<T, 3, true>(f, u, s) : launch_pro_rows<T, 3, false>(f, u, s);
+      else if (f.fnd == 1)
         launch_pro_fold<T, 1>(f, u, ncell, s);
       else if (f.fnd == 2)
         launch_pro_fold<T, 2>(f, u, ncell, s);
@@ -1245,6 +1452,14 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
 
 int nft_hartley_dir_blocks(int ndim, const int64_t* shape) {
   if (ndim < 1 || ndim > 3 || !shape) return 0;
+  for (int a = 0; a < ndim; ++a)
+    if (shape[a] < 1) return 0;
+  if (NFT_PRO_ROWS && pro_rows_ok(ndim, shape[ndim - 1])) {
+    // the row-staged prologue: one block per group of mirror rows
+    long long nrg = 1;
+    for (int a = 0; a < ndim - 1; ++a) nrg *= shape[a] / 2 + 1;
+    return (int)nrg;
+  }
   long long ncell = 1;
   for (int a = 0; a < ndim; ++a) {
     if (shape[a] < 1) return 0;
