@@ -31,12 +31,16 @@ def test_library_exports_every_header_symbol():
 
 
 def test_folded_prologue_block_count():
-    """nft_hartley_dir_blocks: cell grid prod(n/2+1), last axis padded to 64,
-    256 cells per block (pure host arithmetic)"""
+    """nft_hartley_dir_blocks (pure host arithmetic): 2-D / 3-D grids with
+    n_last/2+1 <= 2560 take the row-staged prologue, one block per group of
+    mirror rows (prod over the leading axes of n/2+1); 1-D and longer rows
+    the cell grid prod(n/2+1), last axis padded to 64, 256 cells per block"""
     from nifty_amd import _native
-    assert _native.hartley_dir_blocks((2048, 2048)) == (1025 * 1088 + 255) // 256
-    assert _native.hartley_dir_blocks((64, 30)) == (33 * 64 + 255) // 256
-    assert _native.hartley_dir_blocks((8, 8, 130)) == (5 * 5 * 128 + 255) // 256
+    assert _native.hartley_dir_blocks((2048, 2048)) == 1025
+    assert _native.hartley_dir_blocks((64, 30)) == 33
+    assert _native.hartley_dir_blocks((8, 8, 130)) == 5 * 5
+    assert _native.hartley_dir_blocks((512, 512, 512)) == 257 * 257
+    assert _native.hartley_dir_blocks((4, 8192)) == (3 * 4160 + 255) // 256
     assert _native.hartley_dir_blocks((100,)) == 1
     assert _native.hartley_dir_blocks((0, 4)) == 0
 
