@@ -386,11 +386,11 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
     return out, it
 
 
-def load_pmc(label):
-    """Per-launch HBM traffic of `label` from the committed PMC summary
-    (tools/pmc_probe.py under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE,
-    calibrated as MI355X_MICROARCH.md §HBM prescribes), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_pmc(label, config="C3"):
+    """Per-launch HBM traffic of `label` from the committed PMC summary of
+    the config (tools/pmc_probe.py under rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE, calibrated as MI355X_MICROARCH.md §HBM prescribes), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if config == "C3" else f"pmc_traffic_{config}.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -438,7 +438,7 @@ def roofline_of(kp, cgit, cf, R, config="C3"):
     ach = by / (us * 1e-6) / 1e9
     traffic = 0
     for lab, e in kp.items():
-        t = load_pmc(lab) if config == "C3" else None   # the PMC passes cover C3 only
+        t = load_pmc(lab, config)
         if t is None:
             traffic = None
             break

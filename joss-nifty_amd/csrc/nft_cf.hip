@@ -410,12 +410,12 @@ __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, 
                                                       long long npix, long long nbins, int nchunks) {
   static_assert(CH % 256 == 0, "bin_scatter_il loads CH / 256 positions per thread");
   constexpr int PER = CH / 256;
-  // bins of more than LONGB positions (3-D grids: thousands of cells per
-  // |k| shell at high k) are summed by one wave each -- lane-strided
-  // partials, then a fixed shuffle tree -- instead of one thread's serial
-  // chain of gathers; shorter bins keep the sequential sum (2-D grids: no
-  // bin is that long, the sums are unchanged)
-  constexpr int LONGB = 256;
+  // bins of more than LONGB positions (3-D grids: 512^3 has 87 k of its
+  // 141 k folded bins above 64 cells, up to 747) are summed by one wave each
+  // -- lane-strided partials, then a fixed shuffle tree -- instead of one
+  // thread's serial chain; shorter bins keep the sequential sum (2-D grids:
+  // at most 40 cells per folded bin up to 4096^2, so their sums are unchanged)
+  constexpr int LONGB = 64;
   __shared__ T vals[PRE][CH];
   __shared__ int bnd[2];
   __shared__ int nlong;

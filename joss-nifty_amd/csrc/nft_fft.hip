@@ -911,9 +911,6 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
 // cross a line boundary in every wave, PMC 1.2x of the algorithmic bytes).
 // Same arithmetic per element (bitwise u and d); the d.d partials are per
 // row group (nft_hartley_dir_blocks).
-#ifndef NFT_PRO_ROWS
-#define NFT_PRO_ROWS 1  // A/B build knob (0: pro_fold_kernel everywhere)
-#endif
 __host__ __device__ inline bool pro_rows_ok(int D, long long nlast) { return D >= 2 && nlast / 2 + 1 <= 2560; }
 
 template <typename T, int D, int NBM, bool PI>
@@ -1162,7 +1159,7 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
       long long ncell = 1;  // padded cell grid (pro_fold_kernel)
       for (int a = 0; a < f.fnd; ++a) ncell *= a == f.fnd - 1 ? ((f.fn[a] / 2 + 1 + 63) & ~63LL) : f.fn[a] / 2 + 1;
       prof_mark(s, f.dr ? "pro_fold+dir" : "pro_fold");
-      const bool rows = NFT_PRO_ROWS && pro_rows_ok(f.fnd, f.fn[f.fnd - 1]) && f.nb <= 8;
+      const bool rows = pro_rows_ok(f.fnd, f.fn[f.fnd - 1]) && f.nb <= 8;
       const bool pi = f.sa != 0 || f.sb != 0;
       if (rows && f.fnd == 2)
         pi ? launch_pro_rows<T, 2, true>(f, u, s) : launch_pro_rows<T, 2, false>(f, u, s);
@@ -1454,7 +1451,7 @@ int nft_hartley_dir_blocks(int ndim, const int64_t* shape) {
   if (ndim < 1 || ndim > 3 || !shape) return 0;
   for (int a = 0; a < ndim; ++a)
     if (shape[a] < 1) return 0;
-  if (NFT_PRO_ROWS && pro_rows_ok(ndim, shape[ndim - 1])) {
+  if (pro_rows_ok(ndim, shape[ndim - 1])) {
     // the row-staged prologue: one block per group of mirror rows
     long long nrg = 1;
     for (int a = 0; a < ndim - 1; ++a) nrg *= shape[a] / 2 + 1;

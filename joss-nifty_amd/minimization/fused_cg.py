@@ -654,6 +654,11 @@ class FusedCGBatch(FusedCG):
             ("+chunk" if chunkable else "")
         self.compactions = 0
         iter_seen = np.zeros(k0)
+        # value-driven controllers read the host every iteration and their
+        # solves are short (NewtonCG directions: ~7 iterations): the loop body
+        # stays eager (the one-off capture measured slower: demo step 858 ->
+        # 834 ms eager, Newton-direction CG 788 -> 747 us per RHS iteration)
+        eager_only = any(_reads_value(c) for c in self.controllers)
         while active:
             if chunkable and graph is not None and ii + 2 < self.nreset:
                 m = min(min(self.controllers[j]._iteration_limit - self.controllers[j]._itcount for j in active),
@@ -677,7 +682,7 @@ class FusedCGBatch(FusedCG):
             if ii < self.nreset:
                 if not first and isinstance(st["split"], _CarryIteration):
                     STATS["carry_iters"] += 1
-                if first or not USE_GRAPHS or self.niter <= GRAPH_AFTER or eager > 0:
+                if first or not USE_GRAPHS or eager_only or self.niter <= GRAPH_AFTER or eager > 0:
                     body(not first)
                     eager = max(0, eager - 1)
                 elif graph is None:

@@ -1,9 +1,13 @@
 """Short GPU program for the rocprofv3 PMC passes (HBM traffic of the CG
 iteration kernels, bench.py roofline `traffic`).
 
-    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 tools/pmc_probe.py
-    rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 tools/pmc_probe.py
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 tools/pmc_probe.py [C?]
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 tools/pmc_probe.py [C?]
     python tools/pmc_summary.py gpurun_out
+
+(C? = a bench.py config, default C3: its problem, RHS count and storage
+type; the summary goes to profiles/pmc_traffic.json for C3,
+profiles/pmc_traffic_C?.json otherwise.)
 
 Runs (1) a calibration: nft_scale over a 1 GiB fp64 buffer (known bytes: 1 GiB
 read + 1 GiB written, 8 B per lane, larger than the 256 MiB Infinity Cache),
@@ -21,12 +25,14 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def main(reps=3, k=4):
+def main(config="C3", reps=3):
     import nifty_amd as ift
     from nifty_amd import _native
     ift.config.set_device("cuda:0")
     lib = _native.load()
-    cf, R, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
+    cfg = bench.CONFIGS[config]
+    k = cfg["pairs"]
+    cf, R, lh, pos, _ = bench.build_problem(ift, cfg["shape"][0], 16384, config)
     ift.random.push_sseq_from_seed(5)
     core, W, shift, XS = bench.probe_setup(ift, lh, pos, k)
     n_lat = XS.shape[1]
@@ -49,13 +55,13 @@ def main(reps=3, k=4):
     torch.cuda.synchronize()
     from nifty_amd.minimization import fused_cg
     dcar = bool(fused_cg._CARRY and fused_cg._CARRY_DIR and core.dir_blocks(k) > 0 and bench._CARRY_CACHE)
-    model = bench.byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(core._pairs(k)))
+    model = bench.byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(core._pairs(k)), s=X.element_size())
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "pmc_labels.json"), "w") as f:
         json.dump({"labels": [lab for lab, _ in p.records], "calibration_bytes": 8 * cal_n,
-                   "calibration_launches": 2, "rhs": k, "model": model}, f)
+                   "calibration_launches": 2, "rhs": k, "model": model, "config": config}, f)
     print("pmc probe done:", len(p.records), "labelled launches")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "C3")

@@ -64,13 +64,14 @@ def main(out_dir):
         kernels[lab] = {"kernel": kn, "launches": cnt, "fetch_size_raw": round(f), "write_size_raw": round(w),
                         "traffic_bytes": round(tr), "algorithmic_bytes": alg,
                         "traffic_over_algorithmic": round(tr / alg, 3) if alg else None}
+    config = meta.get("config", "C3")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/pmc_probe.py, "
-                     f"batched CG iteration of the bench problem, {meta['rhs']} RHS",
+                     f"batched CG iteration of the bench problem ({config}), {meta['rhs']} RHS",
            "calibration": {"kernel": "nft::scale_kernel<double> over 1 GiB", "known_bytes_each_way": known,
                            "fetch_size_bytes": round(fcal), "write_size_bytes": round(wcal),
                            "fetch_correction": round(fcorr, 4), "write_correction": round(wcorr, 4)},
            "kernels": kernels}
-    dst = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    dst = os.path.join(ROOT, "profiles", "pmc_traffic.json" if config == "C3" else f"pmc_traffic_{config}.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
