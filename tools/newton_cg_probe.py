@@ -1,0 +1,71 @@
+"""Host overhead of the value-driven Newton-direction CG: one batched solve of
+k right-hand sides on the geoVI Newton metric (geovi_batch._MetricCore, the
+bench's C3 problem) with AbsDeltaEnergyController(iteration_limit=10) as
+NewtonCG's direction requests use it -- wall time per iteration from the
+host -- against the graph-replayed GPU time of the same iteration body
+(direction, matvec, curvature, update).  Usage: python tools/newton_cg_probe.py [k]"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    k = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    import nifty_amd as ift
+    from nifty_amd import _native
+    from nifty_amd.minimization import fused_cg, geovi_batch
+    ift.config.set_device("cuda:0")
+    lib = _native.load()
+    cf, R, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
+    _, f_lh = lh.get_transformation()
+    mini = ift.NewtonCG(ift.GradientNormController(iteration_limit=2))
+    gb = geovi_batch.plan(mini, f_lh, None, pos)
+    lay = gb.layout
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    X0 = gb.x0.repeat(k, 1) + 0.01 * torch.randn((k, lay.size), dtype=torch.float64, device="cuda", generator=g)
+    M = gb.tmean.unsqueeze(0).repeat(k, 1)
+    _, _, _, states = gb.evaluate(X0, M)
+    core = geovi_batch._MetricCore(gb.metric_batch(states), lay)
+    G = torch.randn((k, lay.size), dtype=torch.float64, device="cuda", generator=g)
+    for rep in range(3):
+        ctls = [ift.AbsDeltaEnergyController(1e-300, iteration_limit=10) for _ in range(k)]
+        cg = fused_cg.FusedCGBatch(core, None, 0.0, ctls, 20)
+        starts = [fused_cg._State(0.0, 1.0, lambda: None) for _ in range(k)]
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        cg.run_packed(torch.zeros_like(G), -G, G, starts)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t
+        print(f"solve {rep}: {cg.niter} iterations, {wall * 1e3:.1f} ms, {wall / cg.niter * 1e6:.0f} us per "
+              f"iteration (k={k}, path {cg.path})", flush=True)
+    n = lay.size
+    X, Rr, D = torch.zeros_like(G), -G.clone(), G.clone()
+    Q = torch.zeros_like(X)
+    SC = torch.zeros((k, _native.CG_NSCALARS), dtype=torch.float64, device=X.device)
+    SC[:, _native.CG_GAMMA] = 1.0
+    SC[:, _native.CG_GPREV] = 1.0
+    ws = _native.workspace(k * lib.nft_reduce_workspace(n), X.device, "cgb")
+    bufs = (X, Rr, D, Q, SC, ws)
+    for _ in range(2):
+        bench.cg_iteration(lib, core, None, 0.0, bufs, k)
+    torch.cuda.synchronize()
+    gr = fused_cg._capture(lambda: bench.cg_iteration(lib, core, None, 0.0, bufs, k))
+    gr.replay()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(10):
+        gr.replay()
+    ev[1].record()
+    torch.cuda.synchronize()
+    print(f"graph-replayed iteration body: {ev[0].elapsed_time(ev[1]) * 1e3 / 10:.0f} us (k={k})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
