@@ -32,6 +32,8 @@ def main(config="C3", reps=3):
     lib = _native.load()
     cfg = bench.CONFIGS[config]
     k = cfg["pairs"]
+    if cfg["cg"] == "fp32":
+        ift.config.set_cg_precision("fp32")   # as bench.py runs C5
     cf, R, lh, pos, _ = bench.build_problem(ift, cfg["shape"][0], 16384, config)
     ift.random.push_sseq_from_seed(5)
     core, W, shift, XS = bench.probe_setup(ift, lh, pos, k)
@@ -43,11 +45,14 @@ def main(config="C3", reps=3):
     SC[:, _native.CG_GPREV] = 1.0
     ws = _native.workspace(k * lib.nft_reduce_workspace(n_lat), X.device, "cgb")
     bufs = (X, Rr, D, Q, SC, ws)
-    cal_n = 1 << 27
-    cal = torch.ones(cal_n, dtype=torch.float64, device=X.device)
+    # calibration in the storage type of the run (fp32 loads are counted
+    # differently from fp64 ones): 1 GiB each way
+    cal_n = (1 << 30) // X.element_size()
+    cal = torch.ones(cal_n, dtype=X.dtype, device=X.device)
     torch.cuda.synchronize()
     for _ in range(2):
-        _native._check(lib.nft_scale(_native.ptr(cal), cal_n, 0, 1.0000001, _native.stream_ptr()))
+        _native._check(lib.nft_scale(_native.ptr(cal), cal_n, _native.dtype_code(X.dtype), 1.0000001,
+                                     _native.stream_ptr()))
     torch.cuda.synchronize()
     with _native.LaunchProfile(capacity=4096) as p:
         for _ in range(reps):
@@ -58,7 +63,7 @@ def main(config="C3", reps=3):
     model = bench.byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(core._pairs(k)), s=X.element_size())
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "pmc_labels.json"), "w") as f:
-        json.dump({"labels": [lab for lab, _ in p.records], "calibration_bytes": 8 * cal_n,
+        json.dump({"labels": [lab for lab, _ in p.records], "calibration_bytes": X.element_size() * cal_n,
                    "calibration_launches": 2, "rhs": k, "model": model, "config": config}, f)
     print("pmc probe done:", len(p.records), "labelled launches")
 

@@ -67,7 +67,8 @@ def main(out_dir):
     config = meta.get("config", "C3")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/pmc_probe.py, "
                      f"batched CG iteration of the bench problem ({config}), {meta['rhs']} RHS",
-           "calibration": {"kernel": "nft::scale_kernel<double> over 1 GiB", "known_bytes_each_way": known,
+           "calibration": {"kernel": "nft::scale_kernel over 1 GiB in the run's storage type",
+                           "known_bytes_each_way": known,
                            "fetch_size_bytes": round(fcal), "write_size_bytes": round(wcal),
                            "fetch_correction": round(fcorr, 4), "write_correction": round(wcorr, 4)},
            "kernels": kernels}
