@@ -275,11 +275,12 @@ typedef struct nft_hartley_fuse {
    * second output's bytes; nft_bin_fold_half completes the mirror fold from
    * it (engine-v2 strided unpack pass only). */
   int64_t epi_out2_pairs;
-  /* dot products carried by the epilogue (quad_part != NULL; batched, no
-   * CG epilogue; the same geometries as the CG epilogue): out is stored as
-   * usual and per transform tile of item b the fp64 sum of h * out over the
-   * tile's elements lands at quad_part[b * quad_pstride + quad_blk0 + tile],
-   * tile < nft_hartley_cg_blocks.  With epi_a = W this is
+  /* quadratic form of a pointwise weight carried by the epilogue
+   * (quad_part != NULL; batched, epi_a the only epilogue operand, no CG
+   * epilogue; the same geometries as the CG epilogue): out = epi_a * h is
+   * stored as usual and per transform tile of item b the fp64 sum of
+   * h * out over the tile's elements lands at quad_part[b * quad_pstride +
+   * quad_blk0 + tile], tile < nft_hartley_cg_blocks.  With epi_a = W this is
    * the data-space curvature (J d).W(J d) of a sampling metric
    * J^T W J with a pointwise W (Gaussian / Poisson likelihoods), formed
    * while the forward transform writes W J d -- the partials that
@@ -288,11 +289,6 @@ typedef struct nft_hartley_fuse {
   double* quad_part;
   int64_t quad_pstride;
   int32_t quad_blk0, quad_pad;
-  /* quad_d != NULL: the tile sums are of quad_d[j] * out[j] instead (quad_d
-   * with the per-item stride of out; any epilogue operands): the CG's
-   * curvature d.q with q the adjoint's stored output (value-driven
-   * controllers keep the reference's d.(A d), conjugate_gradient.py:96-101) */
-  const void* quad_d;
 } nft_hartley_fuse;
 
 /* Partial blocks per item of the CG-carrying epilogue for a batched
@@ -520,11 +516,7 @@ int nft_amp_vjp_batched(const nft_amp_const* c, const nft_amp_const* item_consts
  * includes the scalar keys; 0 for a finished RHS) -- the identity part of the
  * data-space curvature.
  *
- * nft_amp2_vjp: out[key] = shift * d[key] + J_amp^T g_r (d may be NULL; with
- * part != NULL and out2 == NULL, d is required and part[r * pstride + tile]
- * receives the tile's fp64 sum of d * out over the amplitude keys -- the
- * curvature d.q of value-driven CG controllers; tile 0 includes the scalar
- * keys), or,
+ * nft_amp2_vjp: out[key] = shift * d[key] + J_amp^T g_r (d may be NULL), or,
  * with out2 != NULL, the CG update of the amplitude keys carried instead:
  * out = x keys, out2 = r keys, d = direction keys, x -= alpha d,
  * r -= alpha (J_amp^T g + shift d) with alpha = sc[GAMMA] / sc[CURV] and the

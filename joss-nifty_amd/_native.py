@@ -98,8 +98,7 @@ class HartleyFuse(ctypes.Structure):
                [(n, _p) for n in ("dir_r", "dir_sc", "dir_part")] + \
                [("dir_pstride", _i64), ("dir_shift", _d), ("dir_blk0", ctypes.c_int32), ("dir_pad", ctypes.c_int32)] + \
                [("epi_out2_pairs", _i64)] + \
-               [("quad_part", _p), ("quad_pstride", _i64), ("quad_blk0", ctypes.c_int32), ("quad_pad", ctypes.c_int32),
-                ("quad_d", _p)]
+               [("quad_part", _p), ("quad_pstride", _i64), ("quad_blk0", ctypes.c_int32), ("quad_pad", ctypes.c_int32)]
 
 
 class LosPlan(ctypes.Structure):
@@ -447,11 +446,6 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
         f.quad_part = qp.data_ptr()
         f.quad_pstride = int(quad["pstride"])
         f.quad_blk0 = int(quad.get("blk0", 0))
-        qd = quad.get("d")
-        if qd is not None:
-            if not qd.is_cuda or qd.dtype != out.dtype:
-                raise NativeError("quad d: a device array of the output's dtype")
-            f.quad_d = qd.data_ptr()
     if batch:
         for t in tens:
             if t is not None and not t.is_cuda:

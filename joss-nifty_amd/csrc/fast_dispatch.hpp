@@ -82,9 +82,9 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     // the CG update / the quadratic-form partials ride only in the strided
     // unpack pass, one item per tile
     if (KIND != K_UNPACK || ROWS || a.los != 0 || a.f.nb < 1 || a.g.O != a.f.nb || ntiles % a.g.O != 0 ||
-        (a.f.quad && a.f.cg)) {
-      set_last_error("CG-carrying / dot-product epilogue: needs the strided unpack pass with one item per tile "
-                     "(not both at once)");
+        (a.f.quad && (a.f.cg || !a.f.ea || a.f.ed || a.f.out2))) {
+      set_last_error("CG-carrying / quadratic-form epilogue: needs the strided unpack pass with one item per "
+                     "tile (quad: epi_a only)");
       return NFT_ERR_UNSUPPORTED;
     }
     b.f.ctr = ntiles / a.g.O;

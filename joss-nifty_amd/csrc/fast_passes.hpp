@@ -61,16 +61,13 @@ struct FuseArgs {
   long long dps;
   double dshift;
   int dblk0;
-  // dot products carried by the unpack epilogue (nft_hartley_fuse.quad_*):
-  // per tile the sum over its elements of z * out, z = h (qd null: the
-  // quadratic form h * (ea * h) of a pointwise weight) or z = qd[b * so + j]
-  // (the CG's d.q with q the stored output), at qpart[item * qps + qblk0 +
-  // tile] (one item per tile)
+  // quadratic form of a pointwise weight carried by the unpack epilogue
+  // (nft_hartley_fuse.quad_*): per tile the sum of h * (ea * h) over its
+  // elements at qpart[item * qps + qblk0 + tile] (one item per tile)
   int quad;
   double* qpart;
   long long qps;
   int qblk0;
-  const void* qd;
 };
 
 // element index into pc of item-element j: its bin (pidx[j]) or, folded, the
@@ -124,20 +121,6 @@ __device__ __forceinline__ void fuse_store(const FuseArgs& f, T* out, long long 
   if (f.ed) r += (T)f.eshift * ((const T*)f.ed)[b * f.sd + j];
   out[b * f.so + j] = r;
   if (f.out2 && !f.o2h) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
-}
-
-// fuse_store that also accumulates z * out for the carried dot products
-// (epilogue mode 2: FuseArgs.quad)
-template <typename T>
-__device__ __forceinline__ void fuse_store_q(const FuseArgs& f, T* out, long long i, T h, double& qs) {
-  long long b, j;
-  fuse_split(f, i, b, j);
-  T r = f.ea ? ((const T*)f.ea)[b * f.sea + j] * h : h;
-  if (f.ed) r += (T)f.eshift * ((const T*)f.ed)[b * f.sd + j];
-  out[b * f.so + j] = r;
-  if (f.out2 && !f.o2h) ((T*)f.out2)[b * f.s2 + j] = ((const T*)f.eb)[b * f.seb + j] * h;
-  const T z = f.qd ? ((const T*)f.qd)[b * f.so + j] : h;
-  qs += (double)z * (double)r;
 }
 
 // point-mirror pair sum of the second epilogue output on the half grid: the
@@ -491,11 +474,11 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           if (a.f.o2h) fuse_store_pair<T>(a.f, ib, hb, u.mirror != 0, im, hm);
         }
       } else if constexpr (EM == 2) {
-        // the plain epilogue (as EM 0) and the tile's sum of z * out (z = h
-        // or qd): the data-space quadratic form (J d).W(J d) of a pointwise W
-        // (forward transform, out = W h) or the CG's d.q (adjoint transform,
-        // out = q); one item per tile (los = 0)
+        // out = ea * h (shared weight, no shift / second output) and the
+        // tile's sum of h * out: the metric's data-space quadratic form
+        // (J d).W(J d) of a pointwise W, one item per tile (los = 0)
         const long long item = o;
+        const T* __restrict__ ea = (const T*)a.f.ea;
         double qs = 0.0;
 #pragma unroll
         for (int r = 0; r < VPT; ++r) {
@@ -505,18 +488,18 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           if (!u.valid) continue;
           const C f = lds[l * PITCH + padx<PS>(x)];
           const int k = (int)m * a.km + x * a.kx;
-          const long long ib = u.base + (long long)k * a.rs;
-          const T hb = sc * (f.x + sg * f.y);
-          fuse_store_q<T>(a.f, out, ib, hb, qs);
-          long long im = 0;
-          T hm = (T)0;
-          if (u.mirror) {
-            const int km = (k == 0) ? 0 : Nf - k;
-            im = u.mbase + (long long)km * a.rs;
-            hm = sc * (f.x - sg * f.y);
-            fuse_store_q<T>(a.f, out, im, hm, qs);
+          const T hv[2] = {sc * (f.x + sg * f.y), sc * (f.x - sg * f.y)};
+          const int km = (k == 0) ? 0 : Nf - k;
+          const long long idx[2] = {u.base + (long long)k * a.rs, u.mbase + (long long)km * a.rs};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (h == 1 && !u.mirror) continue;
+            long long b, j;
+            fuse_split(a.f, idx[h], b, j);
+            const T q = ea[b * a.f.sea + j] * hv[h];
+            out[b * a.f.so + j] = q;
+            qs += (double)hv[h] * (double)q;
           }
-          if (a.f.o2h) fuse_store_pair<T>(a.f, ib, hb, u.mirror != 0, im, hm);
         }
         __shared__ double qsh[NT / 64];
 #pragma unroll

@@ -582,7 +582,6 @@ struct Vjp2Args {
   long long wsd;
   int nrhs, nb;
   int cg;
-  int dq;                  // plain mode: per-tile partials of d.out at part[r * pstride + tile]
   double* sc;              // CG scalar blocks (cg: alpha read, finalized here)
   double* part;            // cg: rr / xr partials per tile, part[r * pstride + {0, nb} + tile]
   long long pstride;
@@ -889,10 +888,8 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
           v0 += a.shift * d0[e];
           v1 += a.shift * d1[e];
         }
-        const VT s0 = (VT)v0, s1 = (VT)v1;
-        os[j] = s0;
-        os[M + j] = s1;
-        if (a.dq) rr += (double)d0[e] * (double)s0 + (double)d1[e] * (double)s1;
+        os[j] = v0;
+        os[M + j] = v1;
       } else {
         double xa = x0[e], xb = x1[e], ra = r0[e], rb = r1[e];
         if (okc) {
@@ -928,9 +925,7 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
     for (int q = 0; q < 5; ++q) {
       if (!has[q] || !a.o[q]) continue;
       if (!a.cg) {
-        const VT ov = (VT)(qv[q] + (a.d[q] ? a.shift * a.d[q][ro] : 0.0));
-        a.o[q][ro] = ov;
-        if (a.dq) rr += (double)a.d[q][ro] * (double)ov;
+        a.o[q][ro] = qv[q] + (a.d[q] ? a.shift * a.d[q][ro] : 0.0);
       } else {
         double x = a.o[q][ro], rv = a.o2[q][ro];
         const double d = a.d[q][ro];
@@ -945,15 +940,7 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
       }
     }
   }
-  if (!a.cg) {
-    if (a.dq) {
-      // this tile's d.out (the curvature d.q of the amplitude keys)
-      double v[1] = {rr};
-      btot<1>(v, sh);
-      if (tid == 0) a.part[(long long)r * a.pstride + i] = v[0];
-    }
-    return;
-  }
+  if (!a.cg) return;
   double v[2] = {rr, xr};
   btot<2>(v, sh);
   if (tid == 0) {
@@ -1100,7 +1087,6 @@ int amp2_vjp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, i
   a.nrhs = nrhs;
   a.nb = nb;
   a.cg = out2 != nullptr;
-  a.dq = (!a.cg && part != nullptr) ? 1 : 0;
   a.sc = sc;
   a.part = part;
   a.pstride = pstride;
@@ -1152,7 +1138,7 @@ int nft_amp2_vjp(const nft_amp_const* cst_, const nft_amp_const* item_consts, in
                  double shift, double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
                  int64_t gp_stride, int64_t gp_row, int ngp, int dtype, hipStream_t stream) {
   if (!cst_ || !g || !out || !ws || nrhs < 1 || cst_->B < 3 || (cst_->has_flex && !out[KSPEC]) ||
-      (out2 && (!d || !sc || !part || (ngp > 0 && !gpart))) || (!out2 && part && !d) || (dtype != 0 && dtype != 1)) {
+      (out2 && (!d || !sc || !part || (ngp > 0 && !gpart))) || (dtype != 0 && dtype != 1)) {
     set_last_error("nft_amp2_vjp: invalid arguments");
     return NFT_ERR_ARG;
   }

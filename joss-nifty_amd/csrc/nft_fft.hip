@@ -1428,17 +1428,16 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
     }
     f.quad = 0;
     if (fz->quad_part) {
-      if (f.cg || !f.epi || f.P <= 0 || f.nb < 1 || fz->quad_blk0 < 0 ||
+      if (f.cg || !f.ea || f.ed || f.out2 || f.P <= 0 || f.nb < 1 || fz->quad_blk0 < 0 ||
           fz->quad_pstride < fz->quad_blk0 + nft_hartley_cg_blocks(ndim, shape, naxes, axes, dtype)) {
-        set_last_error("nft_hartley_fused: the dot-product epilogue needs a batch, an epilogue, no CG epilogue "
-                       "and quad_pstride >= quad_blk0 + nft_hartley_cg_blocks");
+        set_last_error("nft_hartley_fused: the quadratic-form epilogue needs a batch, epi_a alone and "
+                       "quad_pstride >= quad_blk0 + nft_hartley_cg_blocks");
         return NFT_ERR_ARG;
       }
       f.quad = 1;
       f.qpart = fz->quad_part;
       f.qps = fz->quad_pstride;
       f.qblk0 = fz->quad_blk0;
-      f.qd = fz->quad_d;
     }
   }
   const int sigma = convention == 0 ? 1 : -1;

@@ -371,28 +371,23 @@ class _AmplitudeModel:
             1 if interleave else self.B, k if interleave else 1, _native.stream_ptr()))
         return da
 
-    def native_vjp_batched(self, const, g, Q, off, D=None, shift=0.0, item_consts=None, dq=None):
-        """Q[b] amplitude keys = shift * D[b] + J_amp^T g[b].  dq = (part,
-        pstride): per-tile partials of D.Q over the amplitude keys into
-        part[b * pstride + tile] (nft_amp2_tiles tiles; D required)."""
+    def native_vjp_batched(self, const, g, Q, off, D=None, shift=0.0, item_consts=None):
+        """Q[b] amplitude keys = shift * D[b] + J_amp^T g[b]."""
         import ctypes
         k, size = Q.shape
         lib = _native.load()
         ws = _native.workspace(k * lib.nft_amp_workspace(self.B), Q.device, "amp")
         P = ctypes.c_void_p
         host, ic, mode = self._item_mode(const, item_consts)
-        dk = self._key_ptrs(D, off) if (D is not None and (shift != 0.0 or dq is not None)) else None
-        part, pstride = (None, 0) if dq is None else (dq[0].data_ptr(), int(dq[1]))
+        dk = self._key_ptrs(D, off) if (D is not None and shift != 0.0) else None
         if g.dtype != Q.dtype or (D is not None and D.dtype != Q.dtype):
             raise _native.NativeError("native_vjp_batched: g, Q and D dtypes differ")
         st = lib.nft_amp2_vjp(ctypes.byref(host), P(ic), mode, P(g.data_ptr()), self.B, self._key_ptrs(Q, off), None,
-                              dk, size, float(shift), P(ws.data_ptr()), k, None, P(part), pstride, None, 0, 0, 0,
+                              dk, size, float(shift), P(ws.data_ptr()), k, None, None, 0, None, 0, 0, 0,
                               _native.dtype_code(Q.dtype), _native.stream_ptr())
         if st != _native.AMP2_FALLBACK:
             _native._check(st)
             return Q
-        if dq is not None:
-            raise _native.NativeError("d.q partials need the two-phase amplitude kernels (nft_amp2)")
         if Q.dtype != torch.float64:
             raise _native.NativeError("the multi-kernel amplitude VJP is fp64 only (NFT_AMP2=0 with fp32 storage)")
         if mode == 2:
@@ -781,16 +776,14 @@ class CFJacobian(LinearOperator):
             return 0
         return _native.hartley_dir_blocks(jb.fold["shape"])
 
-    def mv_grid(self, D, da, Q, W, shift=0.0, qpart=None, after_w=None, cg=None, pro_dir=None, dq=None):
+    def mv_grid(self, D, da, Q, W, shift=0.0, qpart=None, after_w=None, cg=None, pro_dir=None):
         """forward transform (with the prologue), W, adjoint transform: the
         grid segment of Q and w = xi0 * v for the amplitude VJP.
         after_w: called between W and the adjoint (the curvature fold);
         cg: the grid segment's CG update carried by the adjoint's epilogue
         (nft_hartley_fuse.cg_*) -- Q's grid segment is then not written.
         pro_dir: the grid segment's CG direction update carried by the folded
-        prologue (nft_hartley_fuse.dir_*): D's grid segment is updated in place.
-        dq: (k, >= cg_blocks) fp64 rows receiving the adjoint's per-tile
-        partials of d.q on the grid segment (nft_hartley_fuse.quad_d)."""
+        prologue (nft_hartley_fuse.dir_*): D's grid segment is updated in place."""
         m = self._m
         lay = self.layout
         k, size = D.shape
@@ -826,9 +819,8 @@ class CFJacobian(LinearOperator):
         if shift != 0.0:
             epi.update(d=D[0, xo:], shift=shift)
             bt["d"] = size
-        quad = None if dq is None else dict(part=dq, pstride=dq.stride(0), d=D[0, xo:])
         _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt,
-                              cg=cg, quad=quad)
+                              cg=cg)
         return w
 
     def mv_fold(self, w):
@@ -836,16 +828,14 @@ class CFJacobian(LinearOperator):
         k = w.shape[0]
         return self._m.jbins.fold_into(w, self._mv_bufs(k, w.dtype)["wf"], k, half=self._pairs(k))
 
-    def mv_amp_vjp(self, D, w, Q, shift=0.0, folded=None, dq=None):
+    def mv_amp_vjp(self, D, w, Q, shift=0.0, folded=None):
         """bin sums of w (folded: mv_fold's result, if already formed) and the
-        amplitude VJP into Q's amplitude keys; dq = (part, pstride): per-tile
-        partials of d.q over the amplitude keys (amp2_tiles per row)"""
+        amplitude VJP into Q's amplitude keys"""
         m = self._m
         k = Q.shape[0]
         ga = self._mv_bufs(k, Q.dtype)["ga"]
         m.jbins.scatter_from(self.mv_fold(w) if folded is None else folded, ga, k)
-        m.amp.native_vjp_batched(self._const(), ga, Q, dict(zip(self.layout.keys, self.layout.offsets)), D, shift,
-                                 dq=dq)
+        m.amp.native_vjp_batched(self._const(), ga, Q, dict(zip(self.layout.keys, self.layout.offsets)), D, shift)
         return Q
 
     def grid_segment(self):

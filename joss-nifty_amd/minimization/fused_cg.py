@@ -428,61 +428,6 @@ class _CarryIteration:
         _native._check(lib.nft_cg_finalize_batched(P(self.UP), self.nbtot, k, P(SC), s_))
 
 
-class _ValueIteration:
-    """One CG iteration (k RHS) for value-driven controllers, with the
-    reference's curvature d.(A d) (conjugate_gradient.py:96-101) formed where
-    q is written instead of in a pass over d and q:
-
-      direction of the amplitude keys (two-phase JVP) and of the grid
-      segment (folded prologue), with shift * d.d per tile | forward
-      transform, W | adjoint transform writing q's grid segment and its
-      per-tile d.q | bin sums, amplitude VJP writing q's amplitude keys and
-      their per-tile d.q | one fixed-order fold -> curv | the update pass
-      (x.b streamed for the energy value).
-
-    The direction and q are bitwise those of the separate passes; curv is
-    their dot product summed per tile instead of per block."""
-
-    def __init__(self, lib, core, W, n, k, shift):
-        self.lib, self.core, self.W, self.n, self.k, self.shift = lib, core, W, n, k, shift
-        g0, _ = core.grid_segment()
-        self.g0 = g0
-        self.na = int(core.amp2_tiles(k))
-        self.pb = int(core.dir_blocks(k))
-        self.tiles = int(core.cg_blocks(k))
-        self.nbtot = 2 * self.na + self.pb + self.tiles
-        self.PQ = torch.empty((k, self.nbtot), dtype=torch.float64, device=core.device)
-
-    @staticmethod
-    def supported(core, k, dtype):
-        if not (VALUE_FUSED and hasattr(core, "mv_grid") and hasattr(core, "amp2_tiles")
-                and hasattr(core, "dir_blocks") and hasattr(core, "cg_blocks")):
-            return False
-        if dtype == torch.float32 and not core.phases_fp32(k):
-            return False
-        return core.amp2_tiles(k) > 0 and core.dir_blocks(k) > 0 and core.cg_blocks(k) > 0
-
-    def __call__(self, X, Rr, D, Q, SC, Bu, ws):
-        core, lib, k, n, na, pb = self.core, self.lib, self.k, self.n, self.na, self.pb
-        PQ, P, s_ = self.PQ, _native.ptr, _native.stream_ptr()
-        stride = self.nbtot
-        da = core.mv_amp_jvp_dir(D, Rr, SC, PQ, stride, self.shift)
-        pro_dir = dict(r=Rr[0, self.g0:], sc=SC, part=PQ, pstride=stride, shift=self.shift, blk0=na)
-        w = core.mv_grid(D, da, Q, self.W, 0.0, pro_dir=pro_dir, dq=PQ[:, 2 * na + pb:])
-        core.mv_amp_vjp(D, w, Q, 0.0, dq=(PQ[:, na + pb:], stride))
-        _native._check(lib.nft_fold_partials(P(PQ), stride, k, ctypes.c_void_p(SC.data_ptr() + _native.CG_CURV * 8),
-                                             _native.CG_NSCALARS, s_))
-        dt = _native.dtype_code(X.dtype)
-        _native._check(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, self.shift, P(SC),
-                                                 P(ws), s_))
-
-
-# value-driven solves with the direction in the transform passes and d.q
-# summed where q is written (_ValueIteration; NFT_CG_VALUE_FUSED=0: the
-# separate direction / curvature passes)
-VALUE_FUSED = os.environ.get("NFT_CG_VALUE_FUSED", "1") != "0"
-
-
 class FusedCGBatch(FusedCG):
     """k independent conjugate-gradient solves with the same metric, run in
     lock step: every iteration is ONE batched matvec (the LOS matrix, the FFT
@@ -622,8 +567,6 @@ class FusedCGBatch(FusedCG):
                 st["PQ"] = torch.empty((k, st["nbd"] + nq), dtype=torch.float64, device=dev)
                 if carry:
                     st["split"] = _CarryIteration(lib, core, self.W, n, k, nq, sh)
-            elif _ValueIteration.supported(core, k, X.dtype):
-                st["value"] = _ValueIteration(lib, core, self.W, n, k, sh)
         setup(k0)
 
         def record():
@@ -650,10 +593,6 @@ class FusedCGBatch(FusedCG):
                 split(X, Rr, D, Q, SC)
                 if st["xbdot"]:
                     chk(lib.nft_dot_batched(P(X), P(Bv), n, n, k, dt, P(SC[:, _native.CG_XB:]), NS, P(ws), s_))
-                record()
-                return
-            if with_dir and st.get("value") is not None:
-                st["value"](X, Rr, D, Q, SC, Bu, ws)
                 record()
                 return
             if with_dir and nq:
@@ -711,8 +650,8 @@ class FusedCGBatch(FusedCG):
         # checks with their recorded scalars (HIST)
         chunkable = CHUNK and all(_count_silent(self.controllers[j]) for j in active)
         # which iteration this solve runs (diagnostics: tools/demo_profile.py)
-        self.path = ("carry" if isinstance(st["split"], _CarryIteration) else "quad" if nq else
-                     "value" if st.get("value") is not None else "plain") + ("+chunk" if chunkable else "")
+        self.path = ("carry" if isinstance(st["split"], _CarryIteration) else "quad" if nq else "plain") + \
+            ("+chunk" if chunkable else "")
         self.compactions = 0
         iter_seen = np.zeros(k0)
         # value-driven controllers read the host every iteration and their

@@ -132,36 +132,3 @@ def test_fp32_carried_vs_fp64(ift, which):
             a, b = e1.position[k].val, e2.position[k].val
             err = float(torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(b))
             assert err < 1e-4, (k, err)
-
-
-@pytest.mark.parametrize("which", ["gauss", "los"])
-def test_value_driven_fused_vs_separate(ift, which, monkeypatch):
-    """value-driven controllers (AbsDelta): the direction carried by the
-    transform / amplitude passes and d.q summed where q is written
-    (fused_cg._ValueIteration) against the separate direction / curvature
-    passes -- the same checks, iterates within rtol 1e-10"""
-    from nifty_amd.minimization import fused_cg
-    if which == "los":
-        from test_compact_gpu import _metric as _los_metric
-        cf, A, (core, W, shift) = _los_metric(ift, "los")
-    else:
-        cf, A, (core, W, shift) = _metric(ift, which)
-    with ift.random.Context(7):
-        es = [ift.QuadraticEnergy(0.1 * ift.from_random(cf.domain, "normal"), A,
-                                  ift.from_random(cf.domain, "normal")) for _ in range(3)]
-    out = {}
-    for fused in (True, False):
-        monkeypatch.setattr(fused_cg, "VALUE_FUSED", fused)
-        ctls = [ift.AbsDeltaEnergyController(d, iteration_limit=m) for d, m in ((1e-3, 12), (1e-6, 9), (1e-9, 15))]
-        cg = fused_cg.FusedCGBatch(core, W, shift, ctls)
-        out[fused] = (cg.run(es), [c._itcount for c in cg.controllers])
-        assert cg.path.startswith("value" if fused else "plain"), cg.path
-    (r1, it1), (r2, it2) = out[True], out[False]
-    assert it1 == it2
-    for (e1, s1), (e2, s2) in zip(r1, r2):
-        assert s1 == s2
-        assert abs(e1.value - e2.value) <= 1e-10 * abs(e2.value)
-        for k in cf.domain.keys():
-            a, b = e1.position[k].val, e2.position[k].val
-            err = float(torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(b))
-            assert err < 1e-10, (k, err)
