@@ -65,6 +65,26 @@ def main():
     ev[1].record()
     torch.cuda.synchronize()
     print(f"graph-replayed iteration body: {ev[0].elapsed_time(ev[1]) * 1e3 / 10:.0f} us (k={k})", flush=True)
+    # host enqueue time of one eager iteration body while the GPU is busy
+    torch.cuda._sleep(2_000_000_000)
+    ts = []
+    for _ in range(5):
+        t = time.perf_counter()
+        bench.cg_iteration(lib, core, None, 0.0, bufs, k)
+        ts.append(time.perf_counter() - t)
+    torch.cuda.synchronize()
+    print(f"host enqueue of one iteration body: {min(ts) * 1e6:.0f} us min, {sorted(ts)[2] * 1e6:.0f} us median",
+          flush=True)
+    # where the host time goes: the profile of one enqueue
+    import cProfile
+    import pstats
+    torch.cuda._sleep(2_000_000_000)
+    pr = cProfile.Profile()
+    pr.enable()
+    bench.cg_iteration(lib, core, None, 0.0, bufs, k)
+    pr.disable()
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(25)
 
 
 if __name__ == "__main__":
