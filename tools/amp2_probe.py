@@ -2,7 +2,8 @@
 problem): runs the iteration body (bench.cg_iteration, the timed loop's
 kernels and arguments) `PROBE_REPS` times -- for rocprofv3 --kernel-trace
 --stats -- and prints the HIP-event duration of the graph-replayed
-iteration.  NFT_CG_AMP2=0 gives the separate amplitude launches."""
+iteration.  NFT_CG_AMP2=0 gives the separate amplitude launches; PROBE_N sets
+the grid (default 2048), NFT_LIB another build of the library."""
 import os
 import sys
 
@@ -33,8 +34,7 @@ def main():
         bench.cg_iteration(lib, core, W, shift, bufs, k)
     torch.cuda.synchronize()
     us = bench.cg_iteration_wall(lib, core, W, shift, bufs, k)
-    print("NFT_CG_AMP2=%s NFT_AMP2_DBG=%s iteration %.1f us" % (os.environ.get("NFT_CG_AMP2", "1"),
-                                                               os.environ.get("NFT_AMP2_DBG", "0"), us), flush=True)
+    print("NFT_CG_AMP2=%s N=%d iteration %.1f us" % (os.environ.get("NFT_CG_AMP2", "1"), n, us), flush=True)
 
 
 if __name__ == "__main__":
