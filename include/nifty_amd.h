@@ -172,8 +172,13 @@ int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t
  * pre items interleaved, out[cell * pre + p]; nft_bin_scatter_il then sums
  * the bins of that layout (pre in {2, 4, 8}), one 8 pre-byte gather per
  * cell for all items -- bitwise nft_bin_fold_half + nft_bin_scatter. */
-int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void* out, int64_t pre, int64_t npix,
-                       int64_t nbins, int dtype, hipStream_t stream);
+/* It works in chunks of nft_bin_scatter_il_chunk(pre) sorted positions;
+ * chunk_bins (nchunks + 1 entries, or NULL: a binary search of offsets per
+ * workgroup): the first bin whose offset is >= c * chunk, last entry nbins
+ * -- a plan-time table as for nft_bin_scatter_ordered. */
+int nft_bin_scatter_il_chunk(int64_t pre);
+int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, const int* chunk_bins, void* out,
+                       int64_t pre, int64_t npix, int64_t nbins, int dtype, hipStream_t stream);
 int nft_bin_fold(const void* in, void* out, int64_t pre, int ndim, const int64_t* shape, int dtype,
                  hipStream_t stream);
 
@@ -531,17 +536,27 @@ int nft_amp2_enabled(void);
  * tests); on < 0: back to the environment (NFT_AMP2) */
 void nft_amp2_set_enabled(int on);
 int nft_amp2_tiles(int64_t B, int nrhs, int item_mode);
+/* Constant-scan table of one linearisation (item_mode 0: *c, 2: the device
+ * set item_consts; not per-RHS sets): the tile-local scans and tile sums that
+ * involve the constants only, formed once by nft_amp2_prepare
+ * (nft_amp2_tab_size(B) doubles, device) with the kernels' own scan and sum
+ * code, so that the JVP / VJP given `tab` skip them and produce bitwise the
+ * same results.  Valid while the constants it was made from are unchanged. */
+int64_t nft_amp2_tab_size(int64_t B);
+int nft_amp2_prepare(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, double* tab,
+                     hipStream_t stream);
 /* dtype (0 fp64, 1 fp32): the element type of the key arrays, da and g
  * (the fp32-storage CG); constants, workspace, sums, part and sc stay fp64 and
- * every sum accumulates in fp64. */
+ * every sum accumulates in fp64.  tab: NULL, or the table of nft_amp2_prepare
+ * for the same constants and item_mode (0 or 2). */
 int nft_amp2_jvp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, void* const* t,
                  const void* const* r, int64_t lat_stride, void* da, int64_t da_stride, int64_t da_elem_stride,
                  double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift, int dtype,
-                 hipStream_t stream);
+                 const double* tab, hipStream_t stream);
 int nft_amp2_vjp(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, const void* g,
                  int64_t g_stride, void* const* out, void* const* out2, const void* const* d, int64_t lat_stride,
                  double shift, double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
-                 int64_t gp_stride, int64_t gp_row, int ngp, int dtype, hipStream_t stream);
+                 int64_t gp_stride, int64_t gp_row, int ngp, int dtype, const double* tab, hipStream_t stream);
 
 
 

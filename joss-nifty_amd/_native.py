@@ -42,7 +42,8 @@ SIGNATURES = {
     "nft_bin_fold": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_fold_half": (_i, [_p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_fold_half_sorted": (_i, [_p, _p, _p, _i64, _i, _p, _i, _p]),
-    "nft_bin_scatter_il": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "nft_bin_scatter_il_chunk": (_i, [_i64]),
+    "nft_bin_scatter_il": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "nft_bin_scatter_ordered": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
     "nft_csr_rowblocks": (_i, [_p, _i64, _p, _i64, ctypes.POINTER(_i64)]),
@@ -78,9 +79,11 @@ SIGNATURES = {
     "nft_amp2_enabled": (_i, []),
     "nft_amp2_set_enabled": (None, [_i]),
     "nft_amp2_tiles": (_i, [_i64, _i, _i]),
-    "nft_amp2_jvp": (_i, [_p, _p, _i, _p, _p, _i64, _p, _i64, _i64, _p, _i, _p, _p, _i64, _d, _i, _p]),
+    "nft_amp2_tab_size": (_i64, [_i64]),
+    "nft_amp2_prepare": (_i, [_p, _p, _i, _p, _p]),
+    "nft_amp2_jvp": (_i, [_p, _p, _i, _p, _p, _i64, _p, _i64, _i64, _p, _i, _p, _p, _i64, _d, _i, _p, _p]),
     "nft_amp2_vjp": (_i, [_p, _p, _i, _p, _i64, _p, _p, _p, _i64, _d, _p, _i, _p, _p, _i64, _p, _i64, _i64, _i, _i,
-                          _p]),
+                          _p, _p]),
     "nft_amp_forward_buf": (_i64, [_i64]),
     "nft_amp_forward_batched": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _p, _i64, _p, _i64, _p, _p, _p]),
 }
@@ -326,13 +329,14 @@ def bin_fold_half_sorted(src, out, cpos, pre, shape):
     return out
 
 
-def bin_scatter_il(src, perm, offsets, out, pre, npix, nbins):
+def bin_scatter_il(src, perm, offsets, out, pre, npix, nbins, chunk_bins=None):
     """out[p, b] = sum over bin b's cells of src[cell * pre + p] (the
     interleaved fold of bin_fold_half_sorted with cpos None;
-    nft_bin_scatter_il)"""
+    nft_bin_scatter_il; chunk_bins: the plan's chunk -> first bin table for
+    nft_bin_scatter_il_chunk(pre) positions per chunk, or None)"""
     lib = load()
     require_device(src, perm, offsets, out)
-    _check(lib.nft_bin_scatter_il(ptr(src), ptr(perm), ptr(offsets), ptr(out), pre, npix, nbins,
+    _check(lib.nft_bin_scatter_il(ptr(src), ptr(perm), ptr(offsets), ptr(chunk_bins), ptr(out), pre, npix, nbins,
                                   dtype_code(src.dtype), stream_ptr()))
     return out
 

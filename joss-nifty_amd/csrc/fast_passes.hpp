@@ -226,6 +226,8 @@ constexpr int pass_pad() {
 // values per load group of the CG-carrying unpack epilogue (2 measured
 // 209 -> 219 us at 4 x 2048^2)
 constexpr int CG_CH_VALUES = 1;
+// values per load group of the quadratic-form epilogue (EM 2)
+constexpr int QUAD_CH_VALUES = 8;
 // line pitch in LDS: the (padded) length, +1 for strided passes so the L
 // lines' element x fall in different banks
 template <int N, bool ROWS>
@@ -477,28 +479,52 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         // out = ea * h (shared weight, no shift / second output) and the
         // tile's sum of h * out: the metric's data-space quadratic form
         // (J d).W(J d) of a pointwise W, one item per tile (los = 0)
+        // every weight load of a group of QCH values first, then the products,
+        // stores and sums in the element order (each load waited on before
+        // the next value's store otherwise: one round trip per value); the
+        // second phase re-derives the indices and values from LDS (registers)
         const long long item = o;
         const T* __restrict__ ea = (const T*)a.f.ea;
         double qs = 0.0;
-#pragma unroll
-        for (int r = 0; r < VPT; ++r) {
+        constexpr int QCH = QUAD_CH_VALUES;
+        auto elem = [&](int r, int h, bool& use, T& hv, long long& b, long long& j) {
           int l, x;
           lx_of(r, l, x);
           const UnpackLine u = lines[l];
-          if (!u.valid) continue;
           const C f = lds[l * PITCH + padx<PS>(x)];
           const int k = (int)m * a.km + x * a.kx;
-          const T hv[2] = {sc * (f.x + sg * f.y), sc * (f.x - sg * f.y)};
-          const int km = (k == 0) ? 0 : Nf - k;
-          const long long idx[2] = {u.base + (long long)k * a.rs, u.mbase + (long long)km * a.rs};
+          use = u.valid != 0 && (h == 0 || u.mirror != 0);
+          hv = h == 0 ? sc * (f.x + sg * f.y) : sc * (f.x - sg * f.y);
+          const long long idx = h == 0 ? u.base + (long long)k * a.rs : u.mbase + (long long)((k == 0) ? 0 : Nf - k) * a.rs;
+          fuse_split(a.f, idx, b, j);
+        };
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            if (h == 1 && !u.mirror) continue;
-            long long b, j;
-            fuse_split(a.f, idx[h], b, j);
-            const T q = ea[b * a.f.sea + j] * hv[h];
-            out[b * a.f.so + j] = q;
-            qs += (double)hv[h] * (double)q;
+        for (int r0 = 0; r0 < VPT; r0 += QCH) {
+          T wv[QCH][2];
+#pragma unroll
+          for (int c = 0; c < QCH; ++c) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              bool use;
+              T hv;
+              long long b, j;
+              elem(r0 + c, h, use, hv, b, j);
+              wv[c][h] = use ? ea[b * a.f.sea + j] : (T)0;
+            }
+          }
+#pragma unroll
+          for (int c = 0; c < QCH; ++c) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              bool use;
+              T hv;
+              long long b, j;
+              elem(r0 + c, h, use, hv, b, j);
+              if (!use) continue;
+              const T q = wv[c][h] * hv;
+              out[b * a.f.so + j] = q;
+              qs += (double)hv * (double)q;
+            }
           }
         }
         __shared__ double qsh[NT / 64];

@@ -985,7 +985,7 @@ int nft_amp_jvp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
     void* t[6] = {const_cast<double*>(tfl), const_cast<double*>(tsl), const_cast<double*>(tflex),
                   const_cast<double*>(tasp), const_cast<double*>(tzm), const_cast<double*>(tspec)};
     const int st = nft_amp2_jvp(cst, dcs, dcs ? 1 : 0, t, nullptr, ls, da, vs, da_elem_stride, ws, nrhs, nullptr,
-                                nullptr, 0, 0.0, 0, s);
+                                nullptr, 0, 0.0, 0, nullptr, s);
     if (st != NFT_AMP2_FALLBACK) return st;
   }
   const unsigned ny = (unsigned)nrhs;
@@ -1031,7 +1031,7 @@ int nft_amp_vjp_batched(const nft_amp_const* cst, const nft_amp_const* dcs, cons
     void* out[6] = {o.fl, o.sl, o.flex, o.asp, o.zm, o.spec};
     const void* d[6] = {o.dfl, o.dsl, o.dflex, o.dasp, o.dzm, o.dspec};
     const int st = nft_amp2_vjp(cst, dcs, dcs ? 1 : 0, g, vs, out, nullptr, d, ls, o.shift, ws, nrhs, nullptr, nullptr,
-                                0, nullptr, 0, 0, 0, 0, s);
+                                0, nullptr, 0, 0, 0, 0, nullptr, s);
     if (st != NFT_AMP2_FALLBACK) return st;
   }
   const unsigned ny = (unsigned)nrhs;

@@ -277,6 +277,7 @@ struct Jvp2Args {
   double* part;            // d.d partials: part[r * pstride + tile] = shift * d.d (dir)
   long long pstride;
   double shift;
+  const double* tab;       // constant-scan table (nft_amp2_prepare) or null
 };
 
 // workspace of one RHS: Eh [M, padded], the tile sums (7 rows of nb: agg1,
@@ -295,6 +296,34 @@ __device__ __host__ __forceinline__ JWs jws(int M, int nb) {
   return w;
 }
 
+// Constant-scan table of one constant set (nft_amp2_prepare, modes 0 / 2):
+// the tile-local scans and tile sums that involve the constants only -- the
+// forward scan of lv (LVc), the reverse scans of mspec (ym) and of the two
+// constant VJP weights (g1m, g1l), the forward scan of p2 (p2c), and the
+// constant tile-sum rows of the JVP (LVt, MS2..MS4) and the VJP -- formed
+// once per linearisation by the kernels' own scan and sum code on the same
+// operands, so the TB kernels read bitwise the values they would otherwise
+// form, with a third to a half of the scans.
+enum { TJ_LVT = 0, TJ_MS2, TJ_MS3, TJ_MS4, TV_R2M, TV_R3M, TV_AM, TV_AWM, TV_AWL, TV_P0M, TV_P0S, TV_Q2M, TV_Q2L,
+       TV_P2S, TV_P1M, TV_P1S, T_NROWS };
+struct Tab {
+  long long lvc, ym, g1m, g1l, p2c, rows;
+};
+__device__ __host__ __forceinline__ Tab tab_of(int M, int nb) {
+  const long long Mp = ((long long)M + 63) & ~63LL;
+  Tab t;
+  t.lvc = 0;
+  t.ym = Mp;
+  t.g1m = 2 * Mp;
+  t.g1l = 3 * Mp;
+  t.p2c = 4 * Mp;
+  t.rows = 5 * Mp;
+  (void)nb;
+  return t;
+}
+__host__ __forceinline__ long long tab_size(long long B, int nb) {
+  return tab_of((int)(B - 2), nb).rows + (long long)T_NROWS * nb;
+}
 // the constant set of RHS r by item mode (a template parameter, so that a
 // device set is read with scalar loads from the constant address space: its
 // pointers land in SGPRs and the per-bin loads wait on nothing)
@@ -316,8 +345,9 @@ __device__ __forceinline__ AmpConst const_of(const AmpConst& c, const AmpConst* 
 }
 
 // first launch: direction update, tile-local scans, Eh, the tile sums; the
-// last workgroup of each RHS then forms that RHS's tile carries
-template <typename VT, int MODE>
+// last workgroup of each RHS then forms that RHS's tile carries.  TB: the
+// constant scan (LVc) and sums (LVt, MS2..MS4) from the table
+template <typename VT, int MODE, bool TB>
 __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
   __shared__ double sh[2 * E * NW + 8 * NW];
   __shared__ int lflag;
@@ -369,10 +399,11 @@ __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
     qf[e] = okf ? G_(c.Qf)[b] : 0.0;
     qa[e] = (ok && asp) ? G_(c.Qa)[b] : 0.0;
     msv[e] = ok ? G_(c.mspec)[b] : 0.0;
-    scv[e] = ok ? G_(c.sc)[b] : 0.0;
+    scv[e] = (ok && !TB) ? G_(c.sc)[b] : 0.0;
   }
   double dd = 0.0;
-  double u[1][E], th[2][E];
+  constexpr int NTH = TB ? 1 : 2;
+  double u[1][E], th[NTH][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int j = j0 + e * NT;
@@ -387,22 +418,26 @@ __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
     // loc1 lv + pre on the carry-free local scan loc1
     u[0][e] = d1[e] * sfv[e];
     th[0][e] = d0[e] * c0v[e] - u[0][e] / 2 * lvv[e];
-    th[1][e] = lvv[e];
+    if constexpr (!TB) th[NTH - 1][e] = lvv[e];
   }
   double agg1 = 0.0, agg2 = 0.0, LVt = 0.0;
   if (flex) {
-    double t1[1], t2[2];
+    double t1[1], t2[NTH];
     scan_arr<1, E, false>(u, t1, sh);  // u -> loc1
     agg1 = t1[0];
 #pragma unroll
     for (int e = 0; e < E; ++e) th[0][e] += u[0][e] * lvv[e];
-    scan_arr<2, E, false>(th, t2, sh);  // -> loc2, LVc
+    scan_arr<NTH, E, false>(th, t2, sh);  // -> loc2 (, LVc)
     agg2 = t2[0];
-    LVt = t2[1];
+    LVt = t2[NTH - 1];
   }
   // Eh = vslope ssl + loc2 + sf Qf + sa Qa (stored); tile sums MS1..MS4, d.d
   const double ssl = c.sig_s * sv[KSL];
-  double s[5] = {0.0, 0.0, 0.0, 0.0, dd};
+  constexpr int KD = TB ? 1 : 4;  // the d.d slot
+  double s[KD + 1];
+#pragma unroll
+  for (int q = 0; q < KD; ++q) s[q] = 0.0;
+  s[KD] = dd;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int j = j0 + e * NT;
@@ -412,9 +447,11 @@ __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
     if (asp) d += sv[KASP] * qa[e];
     W[j] = d;
     s[0] += msv[e] * d;
-    s[1] += msv[e];
-    s[2] += msv[e] * (flex ? th[1][e] : 0.0);
-    s[3] += msv[e] * scv[e];
+    if constexpr (!TB) {
+      s[1] += msv[e];
+      s[2] += msv[e] * (flex ? th[NTH - 1][e] : 0.0);
+      s[3] += msv[e] * scv[e];
+    }
   }
   if (i == 0 && tid < 2) {  // bins 0 and 1: no integrated part
     const int b = tid;
@@ -423,24 +460,26 @@ __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
     if (flex) d += sv[KFLEX] * G_(c.Qf)[b];
     if (asp) d += sv[KASP] * G_(c.Qa)[b];
     s[0] += ms * d;
-    s[3] += ms * G_(c.sc)[b];
+    if constexpr (!TB) s[3] += ms * G_(c.sc)[b];
   }
-  btot<5>(s, sh);
+  btot<KD + 1>(s, sh);
   if (tid == 0) {
     double* R = W + L.rows;
     cst(R + 0 * nb + i, agg1);
     cst(R + 1 * nb + i, agg2);
     cst(R + 2 * nb + i, s[0]);
-    cst(R + 3 * nb + i, LVt);
-    cst(R + 4 * nb + i, s[1]);
-    cst(R + 5 * nb + i, s[2]);
-    cst(R + 6 * nb + i, s[3]);
+    if constexpr (!TB) {
+      cst(R + 3 * nb + i, LVt);
+      cst(R + 4 * nb + i, s[1]);
+      cst(R + 5 * nb + i, s[2]);
+      cst(R + 6 * nb + i, s[3]);
+    }
     if (i == 0) {
 #pragma unroll
       for (int q = 0; q < 5; ++q) W[L.scal + q] = sv[q];
     }
     if (a.dir) {
-      double v = s[4];
+      double v = s[KD];
       if (i == 0) {
 #pragma unroll
         for (int q = 0; q < 5; ++q) v += sv[q] * sv[q];
@@ -453,6 +492,7 @@ __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
   // agg2 + C1 LVt, T = their total, dS = sum MS1 + C2 MS2 + C1 MS3 - T MS4
   if (!last_arrival(g_arrive[0][r], i, nb, &lflag)) return;
   const double* R = W + L.rows;
+  const double* TR = TB ? a.tab + tab_of(M, nb).rows : nullptr;
   double run1 = 0.0, run2 = 0.0, ds = 0.0, m4 = 0.0;
   for (int t0 = 0; t0 < nb; t0 += CQ * NT) {
     // every row of the chunk loaded first
@@ -464,10 +504,17 @@ __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
       A1[q] = ok ? cld(R + 0 * nb + t) : 0.0;
       A2[q] = ok ? cld(R + 1 * nb + t) : 0.0;
       M1[q] = ok ? cld(R + 2 * nb + t) : 0.0;
-      LT[q] = ok ? cld(R + 3 * nb + t) : 0.0;
-      M2[q] = ok ? cld(R + 4 * nb + t) : 0.0;
-      M3[q] = ok ? cld(R + 5 * nb + t) : 0.0;
-      M4[q] = ok ? cld(R + 6 * nb + t) : 0.0;
+      if constexpr (TB) {
+        LT[q] = ok ? TR[TJ_LVT * nb + t] : 0.0;
+        M2[q] = ok ? TR[TJ_MS2 * nb + t] : 0.0;
+        M3[q] = ok ? TR[TJ_MS3 * nb + t] : 0.0;
+        M4[q] = ok ? TR[TJ_MS4 * nb + t] : 0.0;
+      } else {
+        LT[q] = ok ? cld(R + 3 * nb + t) : 0.0;
+        M2[q] = ok ? cld(R + 4 * nb + t) : 0.0;
+        M3[q] = ok ? cld(R + 5 * nb + t) : 0.0;
+        M4[q] = ok ? cld(R + 6 * nb + t) : 0.0;
+      }
     }
     double C1[CQ], C2[CQ], y2[CQ];
 #pragma unroll
@@ -498,8 +545,8 @@ __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
 }
 
 // second launch: da from Eh and the carries; tile 0 writes the scalar keys'
-// new direction
-template <typename VT, int MODE>
+// new direction.  TB: LVc from the table
+template <typename VT, int MODE, bool TB>
 __global__ __launch_bounds__(NT) void jvp2b_kernel(Jvp2Args<VT> a) {
   __shared__ double sh[E * NW + 8];
   int i, r;
@@ -520,12 +567,12 @@ __global__ __launch_bounds__(NT) void jvp2b_kernel(Jvp2Args<VT> a) {
     eh[e] = ok ? W[j] : 0.0;
     anv[e] = ok ? G_(c.An)[j + 2] : 0.0;
     scv[e] = ok ? G_(c.sc)[j + 2] : 0.0;
-    lvc[0][e] = (ok && flex) ? G_(c.lv)[j] : 0.0;
+    lvc[0][e] = (ok && flex) ? (TB ? a.tab[j] : G_(c.lv)[j]) : 0.0;  // table: lvc at offset 0
   }
   const double C1 = W[L.c1 + i], C2 = W[L.c2 + i], T = W[L.glb], dS = W[L.glb + 1];
   const double* sv = W + L.scal;
   const double sfl = sv[KFL];
-  if (flex) {
+  if (flex && !TB) {
     double t[1];
     scan_arr<1, E, false>(lvc, t, sh);
   }
@@ -588,6 +635,7 @@ struct Vjp2Args {
   const double* gpart;     // cg: the grid segment's partials (rows rr, xr at 0 and gpr) per RHS
   long long gps, gpr;
   int ngp;
+  const double* tab;       // constant-scan table (nft_amp2_prepare) or null
 };
 
 // workspace of one RHS: the tile sums (V_NROWS rows of nb), then the carries
@@ -603,6 +651,25 @@ __device__ __host__ __forceinline__ VWs vws(int nb) {
   w.s1 = w.bet + nb;
   w.glb = w.s1 + nb;
   return w;
+}
+
+// the table row of a VJP workspace row that is constant (-1: not constant)
+__device__ __forceinline__ int vtab_row(int q) {
+  switch (q) {
+    case V_R2M: return TV_R2M;
+    case V_R3M: return TV_R3M;
+    case V_AM: return TV_AM;
+    case V_AWM: return TV_AWM;
+    case V_AWL: return TV_AWL;
+    case V_P0M: return TV_P0M;
+    case V_P0S: return TV_P0S;
+    case V_Q2M: return TV_Q2M;
+    case V_Q2L: return TV_Q2L;
+    case V_P2S: return TV_P2S;
+    case V_P1M: return TV_P1M;
+    case V_P1S: return TV_P1S;
+    default: return -1;
+  }
 }
 
 // tile-local reverse scans of the VJP: y = [G, mspec] (yG, ym), then
@@ -627,10 +694,30 @@ __device__ __forceinline__ void vjp_scans(const double (&G)[E], const double (&m
   if (second) scan_arr<3, E, true>(w, tw, sh);
 }
 
+// the same for the cotangent terms only (the constant-scan table holds the
+// mspec / weight scans): y = reverse scan of G, w = its weight term and,
+// second, the reverse scan of w -- per array the operations of vjp_scans
+__device__ __forceinline__ void vjp_scans_g(const double (&G)[E], const double (&lvv)[E], const double (&lvn)[E],
+                                            double (&y)[1][E], double (&w)[1][E], double& ty, double* sh,
+                                            bool second) {
+#pragma unroll
+  for (int e = 0; e < E; ++e) y[0][e] = G[e];
+  double t[1];
+  scan_arr<1, E, true>(y, t, sh);
+  ty = t[0];
+#pragma unroll
+  for (int e = 0; e < E; ++e) w[0][e] = y[0][e] * lvv[e] / 2. + (y[0][e] - G[e]) * lvn[e] / 2.;
+  if (second) {
+    double t2[1];
+    scan_arr<1, E, true>(w, t2, sh);
+  }
+}
+
 // first launch: the tile sums (and, cg, this tile's slice of the grid
 // segment's r.r / x.r partials); the last workgroup of each RHS then forms
-// that RHS's k, R1, R2, R4, R5 and the carries beta, S1 of every tile
-template <typename VT, int MODE>
+// that RHS's k, R1, R2, R4, R5 and the carries beta, S1 of every tile.  TB:
+// the constant rows and scans from the table
+template <typename VT, int MODE, bool TB>
 __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
   __shared__ double sh[3 * E * NW + 24 * NW];
   __shared__ int lflag;
@@ -653,14 +740,14 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
     const int b = j + 2;
     gb[e] = ok ? gr[b] : 0.0;
     anv[e] = ok ? G_(c.An)[b] : 0.0;
-    msv[e] = ok ? G_(c.mspec)[b] : 0.0;
+    msv[e] = (ok && !TB) ? G_(c.mspec)[b] : 0.0;
     vsl[e] = ok ? G_(c.vslope)[b] : 0.0;
     scv[e] = ok ? G_(c.sc)[b] : 0.0;
     lvv[e] = okf ? G_(c.lv)[j] : 0.0;
     lvn[e] = (okf && j + 1 < M) ? G_(c.lv)[j + 1] : 0.0;
     p0v[e] = okf ? G_(c.p0)[j] : 0.0;
     p1v[e] = (okf && asp) ? G_(c.p1)[j] : 0.0;
-    pc[0][e] = okf ? G_(c.p2)[j] : 0.0;
+    pc[0][e] = okf ? (TB ? a.tab[tab_of(M, nb).p2c + j] : G_(c.p2)[j]) : 0.0;  // TB: already scanned
   }
   // grid partial slice (cg)
   double crr = 0.0, cxr = 0.0;
@@ -675,20 +762,40 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
   }
   // G_b = An_b (fl TV g_b) / 2 (gapre without its normalisation term)
   double G[E];
-  constexpr int NV = V_NROWS - 3;  // every row but aggG / aggm (scan totals) and P2S
+  // every row but aggG / aggm (scan totals) and P2S; TB: the cotangent rows
+  // R1, R2G, R3G, AWG, P0G, Q2G, P1G, CRR, CXR only
+  constexpr int NV = TB ? 8 : V_NROWS - 3;
   double s[NV + 1];
 #pragma unroll
   for (int q = 0; q <= NV; ++q) s[q] = 0.0;
   // s index of row q: q < V_AG -> q; V_AWG.. -> q - 2 (aggG, aggm skipped), P2S skipped
-  auto S = [&](int row) -> double& { return s[row < V_AG ? row : (row < V_P2S ? row - 2 : row - 3)]; };
+  auto S = [&](int row) -> double& {
+    if constexpr (TB) {
+      switch (row) {
+        case V_R1: return s[0];
+        case V_R2G: return s[1];
+        case V_R3G: return s[2];
+        case V_AWG: return s[3];
+        case V_P0G: return s[4];
+        case V_Q2G: return s[5];
+        case V_P1G: return s[6];
+        case V_CRR: return s[7];
+        default: return s[8];  // V_CXR
+      }
+    } else {
+      return s[row < V_AG ? row : (row < V_P2S ? row - 2 : row - 3)];
+    }
+  };
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     G[e] = anv[e] * (c.fl * (TV * gb[e])) / 2.;
     S(V_R1) += TV * gb[e] * anv[e];
     S(V_R2G) += vsl[e] * G[e];
     S(V_R3G) += G[e] * scv[e];
-    S(V_R2M) += vsl[e] * msv[e];
-    S(V_R3M) += msv[e] * scv[e];
+    if constexpr (!TB) {
+      S(V_R2M) += vsl[e] * msv[e];
+      S(V_R3M) += msv[e] * scv[e];
+    }
   }
   if (i == 0 && tid < 2) {  // bins 0 and 1
     const int b = tid;
@@ -698,11 +805,25 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
     if (b > 0) S(V_R1) += TV * g_ * an;
     S(V_R2G) += vs * ga;
     S(V_R3G) += ga * scb;
-    S(V_R2M) += vs * ms;
-    S(V_R3M) += ms * scb;
+    if constexpr (!TB) {
+      S(V_R2M) += vs * ms;
+      S(V_R3M) += ms * scb;
+    }
   }
   double ty[2] = {0.0, 0.0}, tpc[1] = {0.0};
-  if (flex) {
+  if constexpr (TB) {
+    if (flex) {
+      double y[1][E], w[1][E];
+      vjp_scans_g(G, lvv, lvn, y, w, ty[0], sh, false);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        S(V_AWG) += w[0][e];
+        S(V_P0G) += y[0][e] * p0v[e];
+        S(V_Q2G) += w[0][e] * pc[0][e];
+        S(V_P1G) += y[0][e] * p1v[e];
+      }
+    }
+  } else if (flex) {
     double y[2][E], w[3][E], tw[3];
     vjp_scans(G, msv, lvv, lvn, y, w, ty, tw, sh, false);
     // p2c: tile-local forward scan of p2, so that sum_j g1_j p2_j (g1 the
@@ -730,6 +851,7 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
   if (tid == 0) {
 #pragma unroll
     for (int q = 0; q < V_NROWS; ++q) {
+      if (TB && vtab_row(q) >= 0) continue;
       double v;
       if (q == V_AG) v = ty[0];
       else if (q == V_AM) v = ty[1];
@@ -740,7 +862,14 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
   }
   if (!last_arrival(g_arrive[1][r], i, nb, &lflag)) return;
   // this RHS's globals (fixed-order sums over the tiles) ...
-  auto row = [&](int q, int t) { return cld(W + (long long)q * nb + t); };
+  const double* TR = TB ? a.tab + tab_of(M, nb).rows : nullptr;
+  auto row = [&](int q, int t) {
+    if constexpr (TB) {
+      const int tq = vtab_row(q);
+      if (tq >= 0) return TR[(long long)tq * nb + t];
+    }
+    return cld(W + (long long)q * nb + t);
+  };
   double gsum[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   for (int t = tid; t < nb; t += NT) {
     gsum[0] += row(V_R1, t);
@@ -807,8 +936,9 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
 
 // second launch: the tile-local scans again and the spectrum cotangents
 // (plain: outputs; cg: the update), tile 0 the scalar cotangents; cg: the
-// r.r / x.r partials and the finalize by the last workgroup of the grid
-template <typename VT, int MODE>
+// r.r / x.r partials and the finalize by the last workgroup of the grid.
+// TB: the constant scans from the table
+template <typename VT, int MODE, bool TB>
 __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
   __shared__ double sh[3 * E * NW + 8];
   __shared__ int lflag;
@@ -853,9 +983,22 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
     const bool ok = j < M, okf = ok && flex;
     gb[e] = okf ? gr[j + 2] : 0.0;
     anv[e] = okf ? G_(c.An)[j + 2] : 0.0;
-    msv[e] = okf ? G_(c.mspec)[j + 2] : 0.0;
+    msv[e] = (okf && !TB) ? G_(c.mspec)[j + 2] : 0.0;
     lvv[e] = okf ? G_(c.lv)[j] : 0.0;
     lvn[e] = (okf && j + 1 < M) ? G_(c.lv)[j + 1] : 0.0;
+  }
+  // TB: ym, g1m, g1l (the mspec scan and the two constant weight scans)
+  double tym[E], tgm[E], tgl[E];
+  if constexpr (TB) {
+    const Tab T = tab_of(M, nb);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int j = j0 + e * NT;
+      const bool okf = j < M && flex;
+      tym[e] = okf ? a.tab[T.ym + j] : 0.0;
+      tgm[e] = okf ? a.tab[T.g1m + j] : 0.0;
+      tgl[e] = okf ? a.tab[T.g1l + j] : 0.0;
+    }
   }
   out_loads();
   const double kv = W[L.glb + 0];
@@ -873,14 +1016,17 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
     double G[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) G[e] = anv[e] * (c.fl * (TV * gb[e])) / 2.;
-    double y[2][E], w[3][E], ty[2], tw[3];
-    vjp_scans(G, msv, lvv, lvn, y, w, ty, tw, sh, true);
+    double y[TB ? 1 : 2][E], w[TB ? 1 : 3][E], ty[2], tw[3];
+    if constexpr (TB) vjp_scans_g(G, lvv, lvn, y, w, ty[0], sh, true);
+    else vjp_scans(G, msv, lvv, lvn, y, w, ty, tw, sh, true);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int j = j0 + e * NT;
       if (j >= M) continue;
-      const double yv = (y[0][e] - kv * y[1][e]) + bet;
-      const double g1 = ((w[0][e] - kv * w[1][e]) + bet * w[2][e]) + S1;
+      const double ym = TB ? tym[e] : y[TB ? 0 : 1][e];
+      const double wm = TB ? tgm[e] : w[TB ? 0 : 1][e], wl = TB ? tgl[e] : w[TB ? 0 : 2][e];
+      const double yv = (y[0][e] - kv * ym) + bet;
+      const double g1 = ((w[0][e] - kv * wm) + bet * wl) + S1;
       const double q0 = yv * c0v[e], q1 = g1 * sfv[e];
       if (!a.cg) {
         double v0 = q0, v1 = q1;
@@ -981,6 +1127,131 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
   }
 }
 
+// ======================================================== constant-scan table
+// one workgroup per tile: the constant scans and tile sums of the four
+// kernels, each by the code (scan_arr / btot, the same operands and order of
+// the per-thread sums) the non-table kernels run on them
+template <int MODE>
+__global__ __launch_bounds__(NT) void prep_kernel(AmpConst c0_, const AmpConst* dc1, int nb, double* __restrict__ tab) {
+  __shared__ double sh[3 * E * NW + 24 * NW];
+  const int i = blockIdx.x;
+  if (i >= nb) return;
+  const int tid = threadIdx.x;
+  const AmpConst c = const_of<MODE>(c0_, nullptr, dc1, 0);
+  const int M = (int)(c0_.B - 2);
+  const bool flex = c0_.has_flex, asp = c0_.has_asp;
+  const int j0 = i * TL + tid;
+  const Tab T = tab_of(M, nb);
+  double* TR = tab + T.rows;
+  double lvv[E], lvn[E], msv[E], scv[E], vsl[E], p0v[E], p1v[E], pc[1][E], lvc[1][E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    const bool ok = j < M, okf = ok && flex;
+    const int b = j + 2;
+    lvv[e] = okf ? G_(c.lv)[j] : 0.0;
+    lvn[e] = (okf && j + 1 < M) ? G_(c.lv)[j + 1] : 0.0;
+    msv[e] = ok ? G_(c.mspec)[b] : 0.0;
+    scv[e] = ok ? G_(c.sc)[b] : 0.0;
+    vsl[e] = ok ? G_(c.vslope)[b] : 0.0;
+    p0v[e] = okf ? G_(c.p0)[j] : 0.0;
+    p1v[e] = (okf && asp) ? G_(c.p1)[j] : 0.0;
+    pc[0][e] = okf ? G_(c.p2)[j] : 0.0;
+    lvc[0][e] = lvv[e];
+  }
+  // JVP (jvp2a): LVc and LVt; MS2 = sum mspec, MS3 = sum mspec LVc, MS4 =
+  // sum mspec sc (+ bins 0 and 1 on tile 0)
+  double LVt = 0.0;
+  if (flex) {
+    double t[1];
+    scan_arr<1, E, false>(lvc, t, sh);
+    LVt = t[0];
+  }
+  double sj[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int j = j0 + e * NT;
+    if (j >= M) continue;
+    sj[0] += msv[e];
+    sj[1] += msv[e] * (flex ? lvc[0][e] : 0.0);
+    sj[2] += msv[e] * scv[e];
+  }
+  if (i == 0 && tid < 2) sj[2] += G_(c.mspec)[tid] * G_(c.sc)[tid];
+  btot<3>(sj, sh);
+  // VJP (vjp2a / vjp2b): ym, the weight scans g1m / g1l, p2c and the rows
+  double y[2][E], w[3][E], ty[2] = {0.0, 0.0}, tw[3], tpc[1] = {0.0};
+  double G0[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) G0[e] = 0.0;
+  constexpr int NR = 12;
+  double sv[NR];  // R2M R3M AWM AWL P0M P0S Q2M Q2L P1M P1S (+2 unused)
+#pragma unroll
+  for (int q = 0; q < NR; ++q) sv[q] = 0.0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    sv[0] += vsl[e] * msv[e];
+    sv[1] += msv[e] * scv[e];
+  }
+  if (i == 0 && tid < 2) {
+    const int b = tid;
+    const double ms = G_(c.mspec)[b], vs = G_(c.vslope)[b], scb = G_(c.sc)[b];
+    sv[0] += vs * ms;
+    sv[1] += ms * scb;
+  }
+  if (flex) {
+    vjp_scans(G0, msv, lvv, lvn, y, w, ty, tw, sh, false);
+    scan_arr<1, E, false>(pc, tpc, sh);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      sv[2] += w[1][e];
+      sv[3] += w[2][e];
+      sv[4] += y[1][e] * p0v[e];
+      sv[5] += p0v[e];
+      sv[6] += w[1][e] * pc[0][e];
+      sv[7] += w[2][e] * pc[0][e];
+      sv[8] += y[1][e] * p1v[e];
+      sv[9] += p1v[e];
+    }
+    // the second launch's reverse scans of the two constant weights
+    double w2[2][E], t2[2];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      w2[0][e] = w[1][e];
+      w2[1][e] = w[2][e];
+    }
+    scan_arr<2, E, true>(w2, t2, sh);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int j = j0 + e * NT;
+      if (j >= M) continue;
+      tab[T.lvc + j] = lvc[0][e];
+      tab[T.ym + j] = y[1][e];
+      tab[T.g1m + j] = w2[0][e];
+      tab[T.g1l + j] = w2[1][e];
+      tab[T.p2c + j] = pc[0][e];
+    }
+  }
+  btot<NR>(sv, sh);
+  if (tid == 0) {
+    TR[TJ_LVT * nb + i] = LVt;
+    TR[TJ_MS2 * nb + i] = sj[0];
+    TR[TJ_MS3 * nb + i] = sj[1];
+    TR[TJ_MS4 * nb + i] = sj[2];
+    TR[TV_R2M * nb + i] = sv[0];
+    TR[TV_R3M * nb + i] = sv[1];
+    TR[TV_AM * nb + i] = ty[1];
+    TR[TV_AWM * nb + i] = sv[2];
+    TR[TV_AWL * nb + i] = sv[3];
+    TR[TV_P0M * nb + i] = sv[4];
+    TR[TV_P0S * nb + i] = sv[5];
+    TR[TV_Q2M * nb + i] = sv[6];
+    TR[TV_Q2L * nb + i] = sv[7];
+    TR[TV_P2S * nb + i] = tpc[0];
+    TR[TV_P1M * nb + i] = sv[8];
+    TR[TV_P1S * nb + i] = sv[9];
+  }
+}
+
 // ------------------------------------------------------------------ launch
 static int nblk(long long n, long long per) { return (int)std::max<long long>(1, (n + per - 1) / per); }
 
@@ -1019,21 +1290,43 @@ int nft_amp2_tiles(int64_t B, int nrhs, int item_mode) {
   return tiles_of(B, nrhs);
 }
 
+int64_t nft_amp2_tab_size(int64_t B) {
+  if (B < 3) return 0;
+  return (int64_t)tab_size(B, nblk(B - 2, TL));
+}
+
+int nft_amp2_prepare(const nft_amp_const* c, const nft_amp_const* item_consts, int item_mode, double* tab,
+                     hipStream_t stream) {
+  if (!c || !tab || c->B < 3 || (item_mode != 0 && item_mode != 2) || (item_mode == 2 && !item_consts)) {
+    set_last_error("nft_amp2_prepare: invalid arguments (item_mode 0 or 2)");
+    return NFT_ERR_ARG;
+  }
+  const int nb = nblk(c->B - 2, TL);
+  prof_mark(stream, "amp_prep");
+  if (item_mode == 2) hipLaunchKernelGGL((prep_kernel<2>), dim3(nb), dim3(NT), 0, stream, *c, item_consts, nb, tab);
+  else hipLaunchKernelGGL((prep_kernel<0>), dim3(nb), dim3(NT), 0, stream, *c, nullptr, nb, tab);
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
 }  // extern "C"
 
 namespace {
-#define NFT_AMP2_LAUNCH(KERN, VT, MODE, GRID, S, ARGS)                                  \
-  do {                                                                                  \
-    if ((MODE) == 1) hipLaunchKernelGGL((KERN<VT, 1>), GRID, dim3(NT), 0, S, ARGS);     \
-    else if ((MODE) == 2) hipLaunchKernelGGL((KERN<VT, 2>), GRID, dim3(NT), 0, S, ARGS); \
-    else hipLaunchKernelGGL((KERN<VT, 0>), GRID, dim3(NT), 0, S, ARGS);                 \
+// TB (a constant-scan table) with modes 0 and 2 only
+#define NFT_AMP2_LAUNCH(KERN, VT, MODE, TB, GRID, S, ARGS)                                     \
+  do {                                                                                         \
+    if ((MODE) == 1) hipLaunchKernelGGL((KERN<VT, 1, false>), GRID, dim3(NT), 0, S, ARGS);     \
+    else if ((MODE) == 2 && (TB)) hipLaunchKernelGGL((KERN<VT, 2, true>), GRID, dim3(NT), 0, S, ARGS); \
+    else if ((MODE) == 2) hipLaunchKernelGGL((KERN<VT, 2, false>), GRID, dim3(NT), 0, S, ARGS); \
+    else if (TB) hipLaunchKernelGGL((KERN<VT, 0, true>), GRID, dim3(NT), 0, S, ARGS);          \
+    else hipLaunchKernelGGL((KERN<VT, 0, false>), GRID, dim3(NT), 0, S, ARGS);                 \
   } while (0)
 
 template <typename VT>
 int amp2_jvp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, void* const* t,
                   const void* const* r, int64_t lat_stride, void* da, int64_t da_stride, int64_t da_elem_stride,
                   double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift, int nb,
-                  hipStream_t stream) {
+                  const double* tab, hipStream_t stream) {
   Jvp2Args<VT> a{};
   a.c = *cst_;
   a.dcs = item_mode == 1 ? item_consts : nullptr;
@@ -1055,11 +1348,13 @@ int amp2_jvp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, i
   a.part = part;
   a.pstride = pstride;
   a.shift = shift;
+  a.tab = tab;
+  const bool tb = tab != nullptr;
   const dim3 grid(grid_of(nb, nrhs));
   prof_mark(stream, a.dir ? "amp_jvp2a+dir" : "amp_jvp2a");
-  NFT_AMP2_LAUNCH(jvp2a_kernel, VT, item_mode, grid, stream, a);
+  NFT_AMP2_LAUNCH(jvp2a_kernel, VT, item_mode, tb, grid, stream, a);
   prof_mark(stream, "amp_jvp2b");
-  NFT_AMP2_LAUNCH(jvp2b_kernel, VT, item_mode, grid, stream, a);
+  NFT_AMP2_LAUNCH(jvp2b_kernel, VT, item_mode, tb, grid, stream, a);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
@@ -1068,7 +1363,7 @@ template <typename VT>
 int amp2_vjp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, const void* g,
                   int64_t g_stride, void* const* out, void* const* out2, const void* const* d, int64_t lat_stride,
                   double shift, double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
-                  int64_t gp_stride, int64_t gp_row, int ngp, int nb, hipStream_t stream) {
+                  int64_t gp_stride, int64_t gp_row, int ngp, int nb, const double* tab, hipStream_t stream) {
   Vjp2Args<VT> a{};
   a.c = *cst_;
   a.dcs = item_mode == 1 ? item_consts : nullptr;
@@ -1094,11 +1389,13 @@ int amp2_vjp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, i
   a.gps = gp_stride;
   a.gpr = gp_row;
   a.ngp = a.cg ? ngp : 0;
+  a.tab = tab;
+  const bool tb = tab != nullptr;
   const dim3 grid(grid_of(nb, nrhs));
   prof_mark(stream, a.cg ? "amp_vjp2a+cg" : "amp_vjp2a");
-  NFT_AMP2_LAUNCH(vjp2a_kernel, VT, item_mode, grid, stream, a);
+  NFT_AMP2_LAUNCH(vjp2a_kernel, VT, item_mode, tb, grid, stream, a);
   prof_mark(stream, a.cg ? "amp_vjp2b+cg" : "amp_vjp2b");
-  NFT_AMP2_LAUNCH(vjp2b_kernel, VT, item_mode, grid, stream, a);
+  NFT_AMP2_LAUNCH(vjp2b_kernel, VT, item_mode, tb, grid, stream, a);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
@@ -1109,9 +1406,9 @@ extern "C" {
 int nft_amp2_jvp(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, void* const* t,
                  const void* const* r, int64_t lat_stride, void* da, int64_t da_stride, int64_t da_elem_stride,
                  double* ws, int nrhs, const double* sc, double* part, int64_t pstride, double shift, int dtype,
-                 hipStream_t stream) {
+                 const double* tab, hipStream_t stream) {
   if (!cst_ || !t || !da || !ws || nrhs < 1 || cst_->B < 3 || (cst_->has_flex && !t[KSPEC]) ||
-      (r && (!sc || !part)) || (dtype != 0 && dtype != 1)) {
+      (r && (!sc || !part)) || (dtype != 0 && dtype != 1) || (tab && item_mode == 1)) {
     set_last_error("nft_amp2_jvp: invalid arguments");
     return NFT_ERR_ARG;
   }
@@ -1128,17 +1425,18 @@ int nft_amp2_jvp(const nft_amp_const* cst_, const nft_amp_const* item_consts, in
   if (!nb) return NFT_AMP2_FALLBACK;
   if (dtype == 1)
     return amp2_jvp_impl<float>(cst_, item_consts, item_mode, t, r, lat_stride, da, da_stride, da_elem_stride, ws,
-                                nrhs, sc, part, pstride, shift, nb, stream);
+                                nrhs, sc, part, pstride, shift, nb, tab, stream);
   return amp2_jvp_impl<double>(cst_, item_consts, item_mode, t, r, lat_stride, da, da_stride, da_elem_stride, ws,
-                               nrhs, sc, part, pstride, shift, nb, stream);
+                               nrhs, sc, part, pstride, shift, nb, tab, stream);
 }
 
 int nft_amp2_vjp(const nft_amp_const* cst_, const nft_amp_const* item_consts, int item_mode, const void* g,
                  int64_t g_stride, void* const* out, void* const* out2, const void* const* d, int64_t lat_stride,
                  double shift, double* ws, int nrhs, double* sc, double* part, int64_t pstride, const double* gpart,
-                 int64_t gp_stride, int64_t gp_row, int ngp, int dtype, hipStream_t stream) {
+                 int64_t gp_stride, int64_t gp_row, int ngp, int dtype, const double* tab, hipStream_t stream) {
   if (!cst_ || !g || !out || !ws || nrhs < 1 || cst_->B < 3 || (cst_->has_flex && !out[KSPEC]) ||
-      (out2 && (!d || !sc || !part || (ngp > 0 && !gpart))) || (dtype != 0 && dtype != 1)) {
+      (out2 && (!d || !sc || !part || (ngp > 0 && !gpart))) || (dtype != 0 && dtype != 1) ||
+      (tab && item_mode == 1)) {
     set_last_error("nft_amp2_vjp: invalid arguments");
     return NFT_ERR_ARG;
   }
@@ -1155,9 +1453,9 @@ int nft_amp2_vjp(const nft_amp_const* cst_, const nft_amp_const* item_consts, in
   if (!nb) return NFT_AMP2_FALLBACK;
   if (dtype == 1)
     return amp2_vjp_impl<float>(cst_, item_consts, item_mode, g, g_stride, out, out2, d, lat_stride, shift, ws, nrhs,
-                                sc, part, pstride, gpart, gp_stride, gp_row, ngp, nb, stream);
+                                sc, part, pstride, gpart, gp_stride, gp_row, ngp, nb, tab, stream);
   return amp2_vjp_impl<double>(cst_, item_consts, item_mode, g, g_stride, out, out2, d, lat_stride, shift, ws, nrhs,
-                               sc, part, pstride, gpart, gp_stride, gp_row, ngp, nb, stream);
+                               sc, part, pstride, gpart, gp_stride, gp_row, ngp, nb, tab, stream);
 }
 
 }  // extern "C"

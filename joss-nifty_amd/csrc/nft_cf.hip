@@ -406,8 +406,9 @@ __global__ __launch_bounds__(256) void bin_fold_half_sorted(const T* __restrict_
 // summed in ascending position from 0 (bitwise bin_scatter_chunk).
 template <typename T, int PRE, int CH>
 __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, const int* __restrict__ perm,
-                                                      const int* __restrict__ offs, T* __restrict__ out,
-                                                      long long npix, long long nbins, int nchunks) {
+                                                      const int* __restrict__ offs, const int* __restrict__ cb,
+                                                      T* __restrict__ out, long long npix, long long nbins,
+                                                      int nchunks) {
   static_assert(CH % 256 == 0, "bin_scatter_il loads CH / 256 positions per thread");
   constexpr int PER = CH / 256;
   // bins of more than LONGB positions (3-D grids: 512^3 has 87 k of its
@@ -438,8 +439,11 @@ __global__ __launch_bounds__(256) void bin_scatter_il(const T* __restrict__ in, 
 #pragma unroll
     for (int p = 0; p < PRE; ++p) v[i][p] = t + i * 256 < n ? in[(long long)pv[i] * PRE + p] : (T)0;
   if (t == 0) nlong = 0;
-  if (t < 2) {
-    // first bin whose start offset is >= j0 (+ CH)
+  if (t < 2 && cb) {
+    bnd[t] = cb[c + t];  // the plan's chunk -> first bin table
+  } else if (t < 2) {
+    // first bin whose start offset is >= j0 (+ CH): a chain of ~20 dependent
+    // loads per workgroup, the table's reason
     const long long target = j0 + (t ? CH : 0);
     long long lo = 0, hi = nbins;
     while (lo < hi) {
@@ -744,8 +748,10 @@ int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t
 
 // bin-sorted positions x items per nft_bin_scatter_il workgroup (4096 measured 31 -> 36 us)
 constexpr int SIL_CH = 2048;
-int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void* out, int64_t pre, int64_t npix,
-                       int64_t nbins, int dtype, hipStream_t stream) {
+static int sil_chunk(int64_t pre) { return SIL_CH / pre >= 256 ? (int)(SIL_CH / pre) / 256 * 256 : 256; }
+int nft_bin_scatter_il_chunk(int64_t pre) { return (pre == 2 || pre == 4 || pre == 8) ? sil_chunk(pre) : 0; }
+int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, const int* chunk_bins, void* out,
+                       int64_t pre, int64_t npix, int64_t nbins, int dtype, hipStream_t stream) {
   if (!(pre == 2 || pre == 4 || pre == 8) || npix < 0 || nbins < 0 || !perm || !offsets) {
     set_last_error("nft_bin_scatter_il: need pre in {2, 4, 8}, perm and offsets");
     return NFT_ERR_ARG;
@@ -762,7 +768,7 @@ int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, void
     const int nch = (int)((npix + CH - 1) / CH);                                                              \
     const unsigned nb = (unsigned)(((nch + NXCD - 1) / NXCD) * NXCD);                                         \
     hipLaunchKernelGGL((bin_scatter_il<TT, PP, CH>), dim3(nb), dim3(256), 0, stream, (const TT*)in, perm, offsets, \
-                       (TT*)out, (long long)npix, (long long)nbins, nch);                                     \
+                       chunk_bins, (TT*)out, (long long)npix, (long long)nbins, nch);                         \
   }
   if (dtype == 0) {
     if (pre == 2) NFT_SIL(double, 2) else if (pre == 4) NFT_SIL(double, 4) else NFT_SIL(double, 8)

@@ -62,6 +62,10 @@ _AMP_NATIVE_FWD = os.environ.get("NFT_AMP_NATIVE_FWD", "1") != "0"
 # folded prologue gather (NFT_PRO_FOLD=0 restores the per-pixel pindex gather)
 _PRO_FOLD = os.environ.get("NFT_PRO_FOLD", "1") != "0"
 
+# constant-scan tables for the two-phase amplitude kernels (nft_amp2_prepare:
+# bitwise the same results with fewer scans); tests switch it off for A/B
+AMP2_TABLE = True
+
 class AmpLin:
     """Linearisation points of the amplitude made on the device
     (_AmplitudeModel.forward_rows): values a (k, B), the per-row constant
@@ -343,6 +347,35 @@ class _AmplitudeModel:
             return const.host, item_consts, 1
         return const, item_consts, (1 if item_consts else 0)
 
+    def amp2_table(self, const):
+        """constant-scan table of the constant set `const` (nft_amp2_prepare),
+        made once per set and kept on it; None for per-RHS constant sets, when
+        switched off, or when first asked for during a graph capture"""
+        import ctypes
+        if not AMP2_TABLE:
+            return None
+        host, ic, mode = self._item_mode(const, None)
+        if mode == 1:
+            return None
+        tab = getattr(const, "_amp2_tab", None)
+        if tab is None:
+            if torch.cuda.is_current_stream_capturing():
+                return None
+            lib = _native.load()
+            n = int(lib.nft_amp2_tab_size(self.B))
+            if n <= 0:
+                return None
+            tab = torch.empty(n, dtype=torch.float64, device=self.vslope.device)
+            _native._check(lib.nft_amp2_prepare(ctypes.byref(host), ctypes.c_void_p(ic), mode,
+                                                ctypes.c_void_p(tab.data_ptr()), _native.stream_ptr()))
+            const._amp2_tab = tab
+        return tab
+
+    @staticmethod
+    def _tab_ptr(tab):
+        import ctypes
+        return ctypes.c_void_p(tab.data_ptr() if tab is not None else None)
+
     def native_jvp_batched(self, const, D, off, da, interleave=False, item_consts=None):
         """da[b] = J_amp D[b] for the k rows of a packed batch D (k, size);
         interleave: da is (B, k), bin-major (one contiguous run per bin)."""
@@ -354,9 +387,10 @@ class _AmplitudeModel:
         host, ic, mode = self._item_mode(const, item_consts)
         if da.dtype != D.dtype:
             raise _native.NativeError("native_jvp_batched: da and D dtypes differ")
+        tab = self.amp2_table(const) if item_consts is None else None
         st = lib.nft_amp2_jvp(ctypes.byref(host), P(ic), mode, self._key_ptrs(D, off), None, size, P(da.data_ptr()),
                               1 if interleave else self.B, k if interleave else 1, P(ws.data_ptr()), k, None, None,
-                              0, 0.0, _native.dtype_code(D.dtype), _native.stream_ptr())
+                              0, 0.0, _native.dtype_code(D.dtype), self._tab_ptr(tab), _native.stream_ptr())
         if st != _native.AMP2_FALLBACK:
             _native._check(st)
             return da
@@ -382,9 +416,10 @@ class _AmplitudeModel:
         dk = self._key_ptrs(D, off) if (D is not None and shift != 0.0) else None
         if g.dtype != Q.dtype or (D is not None and D.dtype != Q.dtype):
             raise _native.NativeError("native_vjp_batched: g, Q and D dtypes differ")
+        tab = self.amp2_table(const) if item_consts is None else None
         st = lib.nft_amp2_vjp(ctypes.byref(host), P(ic), mode, P(g.data_ptr()), self.B, self._key_ptrs(Q, off), None,
                               dk, size, float(shift), P(ws.data_ptr()), k, None, None, 0, None, 0, 0, 0,
-                              _native.dtype_code(Q.dtype), _native.stream_ptr())
+                              _native.dtype_code(Q.dtype), self._tab_ptr(tab), _native.stream_ptr())
         if st != _native.AMP2_FALLBACK:
             _native._check(st)
             return Q
@@ -425,7 +460,8 @@ class _AmplitudeModel:
         _native._check(lib.nft_amp2_jvp(ctypes.byref(host), P(ic), mode, self._key_ptrs(D, off),
                                         self._key_ptrs(R, off), size, P(da.data_ptr()), 1, k, P(ws.data_ptr()), k,
                                         P(SC.data_ptr()), P(part.data_ptr()), int(pstride), float(shift),
-                                        _native.dtype_code(D.dtype), _native.stream_ptr()))
+                                        _native.dtype_code(D.dtype), self._tab_ptr(self.amp2_table(const)),
+                                        _native.stream_ptr()))
         return da
 
     def native_vjp_cg(self, const, g, X, R, D, off, SC, part, pstride, gpart, gp_stride, gp_row, ngp, shift):
@@ -442,7 +478,8 @@ class _AmplitudeModel:
                                         self._key_ptrs(X, off), self._key_ptrs(R, off), self._key_ptrs(D, off), size,
                                         float(shift), P(ws.data_ptr()), k, P(SC.data_ptr()), P(part.data_ptr()),
                                         int(pstride), P(gpart.data_ptr()), int(gp_stride), int(gp_row), int(ngp),
-                                        _native.dtype_code(X.dtype), _native.stream_ptr()))
+                                        _native.dtype_code(X.dtype), self._tab_ptr(self.amp2_table(const)),
+                                        _native.stream_ptr()))
 
     def native_jvp(self, const, t, da):
         if isinstance(const, AmpLin):
@@ -553,6 +590,7 @@ class CFJacobian(LinearOperator):
     def _const(self):
         if self._k is None:
             self._k = self._m.amp.native_const(self._c)
+            self._m.amp.amp2_table(self._k[0])  # before any graph capture uses it
         return self._k[0]
 
     def _times_t(self, t):

@@ -15,10 +15,12 @@ from ..utilities import infer_space
 from .linear_operator import LinearOperator
 
 
-def _chunk_bins(offs, nbin, npix):
-    """First bin owned by each chunk of nft_bin_chunk() sorted positions (the
-    first bin whose offset is >= c * chunk), last entry nbin (int32)."""
-    ch = int(_native.load().nft_bin_chunk())
+def _chunk_bins(offs, nbin, npix, ch=None):
+    """First bin owned by each chunk of ch (default nft_bin_chunk()) sorted
+    positions (the first bin whose offset is >= c * chunk), last entry nbin
+    (int32)."""
+    if ch is None:
+        ch = int(_native.load().nft_bin_chunk())
     nch = (npix + ch - 1) // ch
     cb = np.searchsorted(offs[:-1], np.arange(nch + 1, dtype=np.int64) * ch, side="left")
     cb[-1] = nbin
@@ -138,9 +140,21 @@ class BinIndex:
             return _native.bin_scatter(src, self.perm, self.offsets, out, pre, self.npix, self.nbin, 1,
                                        order=self.gather_order)
         if isinstance(src, _ILFold):
-            return _native.bin_scatter_il(src.t, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin)
+            return _native.bin_scatter_il(src.t, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin,
+                                          chunk_bins=self._il_chunk_bins(pre))
         return _native.bin_scatter(src, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
                                    order=f["order"])
+
+    def _il_chunk_bins(self, pre):
+        """the interleaved scatter's chunk -> first bin table (per item count;
+        made once, on the host, from the folded offsets)"""
+        f = self.fold
+        cache = f.setdefault("il_cb", {})
+        if pre not in cache:
+            ch = int(_native.load().nft_bin_scatter_il_chunk(pre))
+            offs = f["offsets"].cpu().numpy().astype(np.int64)
+            cache[pre] = torch.from_numpy(_chunk_bins(offs, self.nbin, f["nf"], ch)).to(f["offsets"].device)
+        return cache[pre]
 
     @property
     def gather_order(self):

@@ -75,13 +75,16 @@ int main() {
   CHECK(nft_amp2_tiles(1197363, 8, 1) == 1170);  // C5
   CHECK(nft_amp2_tiles(313847, 300, 0) == 0);    // more RHS than arrival counters
   CHECK(nft_amp2_tiles(2, 1, 0) == 0);
+  CHECK(nft_amp2_tab_size(2) == 0);
+  CHECK(nft_amp2_tab_size(313847) == 5 * 313856 + 16 * 307);  // 5 padded scans + 16 rows of 307 tiles
+  CHECK(nft_amp2_prepare(nullptr, nullptr, 0, nullptr, nullptr) == NFT_ERR_ARG && err_mentions("nft_amp2_prepare"));
   {
     void* t[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     CHECK(nft_amp2_jvp(nullptr, nullptr, 0, t, nullptr, 0, nullptr, 0, 0, nullptr, 1, nullptr, nullptr, 0, 0.0, 0,
-                       nullptr) == NFT_ERR_ARG && err_mentions("nft_amp2_jvp"));
+                       nullptr, nullptr) == NFT_ERR_ARG && err_mentions("nft_amp2_jvp"));
     void* o[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     CHECK(nft_amp2_vjp(nullptr, nullptr, 0, nullptr, 0, o, nullptr, nullptr, 0, 0.0, nullptr, 1, nullptr, nullptr, 0,
-                       nullptr, 0, 0, 0, 0, nullptr) == NFT_ERR_ARG && err_mentions("nft_amp2_vjp"));
+                       nullptr, 0, 0, 0, 0, nullptr, nullptr) == NFT_ERR_ARG && err_mentions("nft_amp2_vjp"));
   }
   // CG segment update: partial blocks outside the partial array
   CHECK(nft_cg_update_seg_batched(nullptr, nullptr, nullptr, nullptr, nullptr, 1 << 20, 1 << 20, 4, 0, 1.0,

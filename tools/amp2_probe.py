@@ -33,6 +33,8 @@ def main():
     for _ in range(reps):
         bench.cg_iteration(lib, core, W, shift, bufs, k)
     torch.cuda.synchronize()
+    if os.environ.get("PROBE_NOWALL"):  # the kernel trace only (ablation builds)
+        return
     us = bench.cg_iteration_wall(lib, core, W, shift, bufs, k)
     print("NFT_CG_AMP2=%s N=%d iteration %.1f us" % (os.environ.get("NFT_CG_AMP2", "1"), n, us), flush=True)
 
