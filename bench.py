@@ -297,6 +297,9 @@ def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False, s=8):
         "fft_r2c": s * k * N + 2 * s * k * Hh,
         "fft_c2c": 2 * 2 * s * k * Hh,
         "fft_unpack": 2 * s * k * Hh + s * k * N,
+        # + the pointwise weight (shared by the k items) and the per-tile
+        # quadratic-form partials (negligible): W*h out (k)
+        "fft_unpack+quad": 2 * s * k * Hh + s * N + s * k * N,
         # epilogue: out = A*v (k), out2 = xi0*v (k), reads A, xi0
         "fft_unpack+epi": 2 * s * k * Hh + 2 * s * N + s * k * N + s * k * (Hh if pairs else N),
         # 5 B per nonzero, 12 B segment descriptors, x (k) and the column scale, partials (k)
