@@ -96,8 +96,10 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     // measured slower at 2048^2 with 4 items for the r2c prologue and the
     // plain epilogue (r2c+pro 200 -> 211 us, unpack+epi 148 -> 177 us), faster
     // for the CG-carrying epilogue, which is bound by its HBM traffic (the
-    // contiguous flavour, 231 -> 221 us): that pass only
-    const int mode = f.cg ? 2 : 0;
+    // contiguous flavour, 231 -> 221 us), and for the quadratic-form one (its
+    // shared weight read once per tile group: 1938 -> 1666 us at 512^3, 2
+    // items; unchanged at 4096^2): those passes only
+    const int mode = (f.cg || f.quad) ? 2 : 0;
     if (mode > 0 && shared && f.P > 0 && f.nb > 1 && ntiles % (8LL * f.nb) == 0) {
       b.bgroup = f.nb;
       b.bmode = mode;
