@@ -68,8 +68,9 @@ def parse():
                    help="C2/C4/C5: linear-CG iterations of the bounded CPU oracle sample (default 3; C4 1)")
     p.add_argument("--no-demo", action="store_true", help="skip the demo-controller line")
     p.add_argument("--deterministic-allreduce", action="store_true")
-    p.add_argument("--backend", choices=["nccl", "gloo"], default=None,
-                   help="process-group backend (default: nccl = RCCL on a GPU, gloo on CPU)")
+    p.add_argument("--backend", choices=["nccl", "gloo", "none"], default=None,
+                   help="process-group backend (default: nccl = RCCL on a GPU, also at N = 1; gloo on CPU "
+                        "at N > 1; none: no communicator, N = 1 only)")
     a = p.parse_args()
     cfg = CONFIGS[a.config]
     if a.size is None:
@@ -102,21 +103,33 @@ def launch_workers(n):
 
 
 def setup_dist(backend=None):
+    """One process per GPU.  On a GPU the process group is RCCL ("nccl")
+    whatever the world size: at N = 1 a world-size-1 group on an in-process
+    store, so the KL-mean all-reduce of the timed step runs through the same
+    RCCL call as at N = 8 (`--backend none` at N = 1: no communicator)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     lrank = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
         torch.cuda.set_device(lrank % torch.cuda.device_count())
+    backend = backend or ("nccl" if torch.cuda.is_available() else ("gloo" if ws > 1 else "none"))
+    if backend == "none":
+        if ws > 1:
+            raise SystemExit("bench.py: --backend none needs WORLD_SIZE 1")
+        return ws, rank, lrank, False
+    import torch.distributed as dist
     if ws > 1:
-        import torch.distributed as dist
-        dist.init_process_group(backend or ("nccl" if torch.cuda.is_available() else "gloo"))
-    return ws, rank, lrank
+        dist.init_process_group(backend)
+    else:
+        dist.init_process_group(backend, store=dist.HashStore(), rank=0, world_size=1)
+    return ws, rank, lrank, True
 
 
 def barrier_sync(ws):
     if torch.cuda.is_available():
         torch.cuda.synchronize()
-    if ws > 1:
+    import torch.distributed as dist
+    if dist.is_initialized():
         import torch.distributed as dist
         dist.barrier()
     if torch.cuda.is_available():
@@ -604,20 +617,32 @@ class _TimedComm:
         return t
 
 
+def _json_stdout():
+    """stdout carries ONE JSON line: RCCL prints a banner ("RCCL version :
+    ...") to fd 1 when its first communicator comes up, and libraries may
+    print too -- everything written to fd 1 from here on goes to stderr, the
+    result line to a duplicate of the original stdout"""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_workers(args.gpus))
+    result_out = _json_stdout()
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE is {os.environ.get('WORLD_SIZE')}",
               file=sys.stderr, flush=True)
         sys.exit(2)
-    ws, rank, lrank = setup_dist(args.backend)
+    ws, rank, lrank, has_pg = setup_dist(args.backend)
     import nifty_amd as ift
     ift.config.set_device(f"cuda:{lrank % torch.cuda.device_count()}" if torch.cuda.is_available() else "cpu")
     if args.deterministic_allreduce:
         ift.utilities.DETERMINISTIC_ALLREDUCE = True
-    comm = ift.TorchComm() if ws > 1 else None
+    comm = ift.TorchComm() if has_pg else None
     n = args.size
     cfg = CONFIGS[args.config]
     if cfg["cg"] == "fp32":
@@ -649,7 +674,7 @@ def main():
     el = time.perf_counter() - t0
     iters = ift.ConjugateGradient.iterations_total - it0
     dist_info = None
-    if ws > 1:
+    if has_pg:
         import torch.distributed as dist
         dev = "cuda" if torch.cuda.is_available() and dist.get_backend() != "gloo" else "cpu"
         t = torch.tensor([el, float(iters)], dtype=torch.float64, device=dev)
@@ -725,8 +750,8 @@ def main():
                 "cg_iter_per_s": round(cgps, 3), "cg_iters": int(iters),
                 "roofline": roof, "cpu_baseline": cpu, "demo_controllers": demo,
                 "cg_iteration": cgit, "kernels": kp, "distributed": dist_info}
-        print(json.dumps(line), flush=True)
-    if ws > 1:
+        print(json.dumps(line), file=result_out, flush=True)
+    if has_pg:
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -176,6 +176,16 @@ int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t
  * chunk_bins (nchunks + 1 entries, or NULL: a binary search of offsets per
  * workgroup): the first bin whose offset is >= c * chunk, last entry nbins
  * -- a plan-time table as for nft_bin_scatter_ordered. */
+/* The bin sums of a PLANAR mirror fold (pre, npix) -- nft_bin_fold /
+ * nft_bin_fold_half output -- in the arithmetic of nft_bin_scatter_il: bins
+ * of up to 64 positions summed in ascending position, longer bins (3-D
+ * grids) one wave each (lane-strided partials, fixed shuffle tree).  Bitwise
+ * nft_bin_scatter_il on the interleaved fold for every item, so a batch of k
+ * right-hand sides gives the k = 1 sums (DOFDistributor._adjoint_times inside
+ * the fused CF Jacobian adjoint, src/operators/distributors.py:105-112).
+ * chunk_bins: the nft_bin_chunk() table of nft_bin_scatter_ordered, or NULL. */
+int nft_bin_scatter_folded(const void* in, const int* perm, const int* offsets, const int* chunk_bins, void* out,
+                           int64_t pre, int64_t npix, int64_t nbins, int dtype, hipStream_t stream);
 int nft_bin_scatter_il_chunk(int64_t pre);
 int nft_bin_scatter_il(const void* in, const int* perm, const int* offsets, const int* chunk_bins, void* out,
                        int64_t pre, int64_t npix, int64_t nbins, int dtype, hipStream_t stream);

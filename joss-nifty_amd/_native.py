@@ -44,6 +44,7 @@ SIGNATURES = {
     "nft_bin_fold_half_sorted": (_i, [_p, _p, _p, _i64, _i, _p, _i, _p]),
     "nft_bin_scatter_il_chunk": (_i, [_i64]),
     "nft_bin_scatter_il": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
+    "nft_bin_scatter_folded": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "nft_bin_scatter_ordered": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p]),
     "nft_spmv_csr": (_i, [_p, _p, _p, _p, _p, _i64, _i, _d, _i64, _p]),
     "nft_csr_rowblocks": (_i, [_p, _i64, _p, _i64, ctypes.POINTER(_i64)]),
@@ -338,6 +339,18 @@ def bin_scatter_il(src, perm, offsets, out, pre, npix, nbins, chunk_bins=None):
     require_device(src, perm, offsets, out)
     _check(lib.nft_bin_scatter_il(ptr(src), ptr(perm), ptr(offsets), ptr(chunk_bins), ptr(out), pre, npix, nbins,
                                   dtype_code(src.dtype), stream_ptr()))
+    return out
+
+
+def bin_scatter_folded(src, perm, offsets, out, pre, npix, nbins, chunk_bins=None):
+    """out[p, b] = sum over bin b's cells of src[p, cell] (a planar mirror
+    fold) in nft_bin_scatter_il's arithmetic: bitwise the interleaved sums
+    for any item count (nft_bin_scatter_folded; chunk_bins: the
+    nft_bin_chunk() table or None)"""
+    lib = load()
+    require_device(src, perm, offsets, out)
+    _check(lib.nft_bin_scatter_folded(ptr(src), ptr(perm), ptr(offsets), ptr(chunk_bins), ptr(out), pre, npix,
+                                      nbins, dtype_code(src.dtype), stream_ptr()))
     return out
 
 

@@ -72,7 +72,14 @@ constexpr int NXCD = 8;
 // k-plane, crossed by each grid row in a few short runs, so consecutive lanes
 // read nearby addresses instead of one cache line each -- and stored to their
 // bin-sorted LDS slot; the per-bin sums are unchanged (bitwise).
-template <typename T, int K>
+//
+// LW (the mirror-folded bins of the CF Jacobian adjoint, nft_bin_scatter_folded):
+// bins of more than 64 positions are summed one wave each exactly as
+// bin_scatter_il sums them (lane-strided partials, then the shuffle tree), so
+// the planar and the interleaved folded sums agree bitwise for every item
+// count; without LW every bin is one thread's ascending chain (np.bincount's
+// order, the PowerDistributor's bit-exact adjoint).
+template <typename T, int K, bool LW = false>
 __global__ __launch_bounds__(256) void bin_scatter_chunk(const T* __restrict__ in, const int* __restrict__ perm,
                                                          const int* __restrict__ offs,
                                                          const int* __restrict__ gpix,
@@ -86,8 +93,11 @@ __global__ __launch_bounds__(256) void bin_scatter_chunk(const T* __restrict__ i
   // offsets are loaded before the barrier too (off the critical path).
   constexpr int PER = BS_CH / 256;
   constexpr int BPT = 2;  // bins per thread handled with prefetched offsets
+  constexpr int LONGB = 64;
   __shared__ T vals[K][BS_CH];
   __shared__ int bnd[2];
+  __shared__ int nlong;
+  __shared__ int longb[LW ? BS_CH / LONGB + 1 : 1];
   const int per = (nchunks + NXCD - 1) / NXCD;
   const int c = (int)(blockIdx.x % NXCD) * per + (int)(blockIdx.x / NXCD);
   if (c >= nchunks) return;
@@ -125,6 +135,7 @@ __global__ __launch_bounds__(256) void bin_scatter_chunk(const T* __restrict__ i
 #pragma unroll
     for (int i = 0; i < PER; ++i)
       if (t + i * 256 < n) vals[k][sl[i]] = v[k][i];
+  if (LW && t == 0) nlong = 0;
   if (!cbins && t < 2) {
     // first bin whose start offset is >= j0 (+ BS_CH)
     const long long target = j0 + (t ? BS_CH : 0);
@@ -151,6 +162,10 @@ __global__ __launch_bounds__(256) void bin_scatter_chunk(const T* __restrict__ i
       a = offs[b];
       e = offs[b + 1];
     }
+    if (LW && e - a > LONGB) {
+      longb[atomicAdd(&nlong, 1)] = b;  // list order is irrelevant: one bin per entry
+      continue;
+    }
     T acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = (T)0;
@@ -166,6 +181,34 @@ __global__ __launch_bounds__(256) void bin_scatter_chunk(const T* __restrict__ i
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) out[k * nbins + b] = acc[k];
+  }
+  if constexpr (LW) {
+    __syncthreads();
+    const int w = t >> 6, lane = t & 63;
+    for (int i = w; i < nlong; i += 4) {
+      const int b = longb[i];
+      const long long a = offs[b], e = offs[b + 1];
+      T acc[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[k] = (T)0;
+      for (long long j = a + lane; j < e; j += 64) {
+        if (j - j0 < BS_CH) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) acc[k] += vals[k][j - j0];
+        } else {
+          const int p = perm[j];
+#pragma unroll
+          for (int k = 0; k < K; ++k) acc[k] += in[k * npix + p];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        T v = acc[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+        if (lane == 0) out[k * nbins + b] = v;
+      }
+    }
   }
 }
 
@@ -644,6 +687,33 @@ int nft_bin_scatter_ordered(const void* in, const int* perm, const int* offsets,
     set_last_error("nft_bin_scatter: bad dtype");
     return NFT_ERR_ARG;
   }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_bin_scatter_folded(const void* in, const int* perm, const int* offsets, const int* chunk_bins, void* out,
+                           int64_t pre, int64_t npix, int64_t nbins, int dtype, hipStream_t stream) {
+  if (pre < 1 || pre > 65535 || npix < 0 || nbins < 0 || !perm || !offsets || !(dtype == 0 || dtype == 1)) {
+    set_last_error("nft_bin_scatter_folded: need 1 <= pre <= 65535, perm, offsets and dtype 0 / 1");
+    return NFT_ERR_ARG;
+  }
+  if (nbins == 0) return NFT_OK;
+  if (npix == 0) {
+    NFT_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)pre * nbins * (dtype == 0 ? 8 : 4), stream));
+    return NFT_OK;
+  }
+  const int nchunks = (int)((npix + BS_CH - 1) / BS_CH);
+  const unsigned nb = (unsigned)(((nchunks + NXCD - 1) / NXCD) * NXCD);
+  prof_mark(stream, "bin_scatter");
+  const dim3 grid(nb, (unsigned)pre);
+  if (dtype == 0)
+    hipLaunchKernelGGL((bin_scatter_chunk<double, 1, true>), grid, dim3(256), 0, stream, (const double*)in, perm,
+                       offsets, nullptr, nullptr, chunk_bins, (double*)out, (long long)npix, (long long)nbins,
+                       nchunks);
+  else
+    hipLaunchKernelGGL((bin_scatter_chunk<float, 1, true>), grid, dim3(256), 0, stream, (const float*)in, perm,
+                       offsets, nullptr, nullptr, chunk_bins, (float*)out, (long long)npix, (long long)nbins,
+                       nchunks);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

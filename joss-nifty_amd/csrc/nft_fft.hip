@@ -911,7 +911,15 @@ __global__ __launch_bounds__(256) void pro_fold_kernel(fast::FuseArgs f, T* __re
 // cross a line boundary in every wave, PMC 1.2x of the algorithmic bytes).
 // Same arithmetic per element (bitwise u and d); the d.d partials are per
 // row group (nft_hartley_dir_blocks).
-__host__ __device__ inline bool pro_rows_ok(int D, long long nlast) { return D >= 2 && nlast / 2 + 1 <= 2560; }
+// The row's dA runs take (nlast/2 + 1) * NBM * sizeof(T) bytes of dynamic LDS
+// beside the kernel's static d.d array (4 * NBM doubles); the bound is the
+// worst case (fp64, NBM = 8) of the 160 KB LDS, so that it holds for every
+// dtype and batch and nft_hartley_dir_blocks (which knows neither) agrees
+// with the launch: 2556 * 64 + 256 <= 163840.
+constexpr long long PRO_ROWS_MAXH = (160 * 1024 - 4 * 8 * 8) / (8 * 8);
+__host__ __device__ inline bool pro_rows_ok(int D, long long nlast) {
+  return D >= 2 && nlast / 2 + 1 <= PRO_ROWS_MAXH;
+}
 
 template <typename T, int D, int NBM, bool PI>
 __global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __restrict__ u, long long P, int nb) {
@@ -1075,29 +1083,29 @@ __global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __re
 }
 
 template <typename T, int D, int NBM, bool PI>
-static void launch_pro_rows_n(const fast::FuseArgs& f, T* u, hipStream_t s) {
+static int launch_pro_rows_n(const fast::FuseArgs& f, T* u, hipStream_t s) {
   long long nrg = 1;
   for (int a = 0; a < D - 1; ++a) nrg *= f.fn[a] / 2 + 1;
   const size_t lds = (size_t)(f.fn[D - 1] / 2 + 1) * NBM * sizeof(T);
   if (lds > 65536) {
-    static bool set = false;
-    if (!set) {
-      (void)hipFuncSetAttribute((const void*)pro_rows_kernel<T, D, NBM, PI>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      set = true;
+    // the attribute of this instance raised to the largest size asked so far
+    // (a later call on a longer last axis needs more than an earlier one)
+    static size_t set = 0;
+    if (lds > set) {
+      NFT_HIP_CHECK(hipFuncSetAttribute((const void*)pro_rows_kernel<T, D, NBM, PI>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      set = lds;
     }
   }
   hipLaunchKernelGGL((pro_rows_kernel<T, D, NBM, PI>), dim3((unsigned)nrg), dim3(256), lds, s, f, u, f.P, f.nb);
+  return NFT_OK;
 }
 
 template <typename T, int D, bool PI>
-static void launch_pro_rows(const fast::FuseArgs& f, T* u, hipStream_t s) {
-  if (f.nb <= 2)
-    launch_pro_rows_n<T, D, 2, PI>(f, u, s);
-  else if (f.nb <= 4)
-    launch_pro_rows_n<T, D, 4, PI>(f, u, s);
-  else
-    launch_pro_rows_n<T, D, 8, PI>(f, u, s);
+static int launch_pro_rows(const fast::FuseArgs& f, T* u, hipStream_t s) {
+  if (f.nb <= 2) return launch_pro_rows_n<T, D, 2, PI>(f, u, s);
+  if (f.nb <= 4) return launch_pro_rows_n<T, D, 4, PI>(f, u, s);
+  return launch_pro_rows_n<T, D, 8, PI>(f, u, s);
 }
 
 template <typename T, int D, bool PI>
@@ -1161,16 +1169,18 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
       prof_mark(s, f.dr ? "pro_fold+dir" : "pro_fold");
       const bool rows = pro_rows_ok(f.fnd, f.fn[f.fnd - 1]) && f.nb <= 8;
       const bool pi = f.sa != 0 || f.sb != 0;
+      int pst = NFT_OK;
       if (rows && f.fnd == 2)
-        pi ? launch_pro_rows<T, 2, true>(f, u, s) : launch_pro_rows<T, 2, false>(f, u, s);
+        pst = pi ? launch_pro_rows<T, 2, true>(f, u, s) : launch_pro_rows<T, 2, false>(f, u, s);
       else if (rows && f.fnd == 3)
-        pi ? launch_pro_rows<T, 3, true>(f, u, s) : launch_pro_rows<T, 3, false>(f, u, s);
+        pst = pi ? launch_pro_rows<T, 3, true>(f, u, s) : launch_pro_rows<T, 3, false>(f, u, s);
       else if (f.fnd == 1)
         launch_pro_fold<T, 1>(f, u, ncell, s);
       else if (f.fnd == 2)
         launch_pro_fold<T, 2>(f, u, ncell, s);
       else
         launch_pro_fold<T, 3>(f, u, ncell, s);
+      if (pst != NFT_OK) return pst;
     } else {
       prof_mark(s, "pro_batch");
       hipLaunchKernelGGL(pro_batch_kernel<T>, dim3(nblk), dim3(256), 0, s, f, u, f.P, f.nb);

@@ -17,14 +17,23 @@ bool g_prof_on = false;
 static std::vector<hipEvent_t> g_ev;
 static std::vector<std::string> g_lab;
 static size_t g_cap = 0;
+// the first failed event call of a profiling window (reported by nft_prof_end)
+static hipError_t g_err = hipSuccess;
 
 void prof_mark_impl(hipStream_t s, const char* label) {
   if (g_lab.size() >= g_cap) return;
   hipEvent_t e;
   // no system-scope release: the default fence writes back L2 and would perturb
   // the next kernel's cache state
-  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return;
-  hipEventRecord(e, s);
+  hipError_t st = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  if (st == hipSuccess) {
+    st = hipEventRecord(e, s);
+    if (st != hipSuccess) (void)hipEventDestroy(e);
+  }
+  if (st != hipSuccess) {
+    if (g_err == hipSuccess) g_err = st;
+    return;
+  }
   g_ev.push_back(e);
   g_lab.push_back(label);
 }
@@ -36,11 +45,17 @@ using namespace nft;
 extern "C" {
 
 int nft_prof_begin(int capacity) {
-  for (auto e : g_ev) hipEventDestroy(e);
+  hipError_t st = hipSuccess;
+  for (auto e : g_ev) {
+    const hipError_t d = hipEventDestroy(e);
+    if (st == hipSuccess) st = d;
+  }
   g_ev.clear();
+  g_err = hipSuccess;
   g_lab.clear();
   g_cap = capacity > 0 ? (size_t)capacity : 0;
   g_prof_on = g_cap > 0;
+  NFT_HIP_CHECK(st);
   return NFT_OK;
 }
 
@@ -48,7 +63,10 @@ int nft_prof_end(hipStream_t stream, float* ms, int cap, int* n) {
   g_prof_on = false;
   const int m = (int)g_ev.size();
   *n = 0;
-  if (m == 0) return NFT_OK;
+  if (m == 0) {
+    NFT_HIP_CHECK(g_err);
+    return NFT_OK;
+  }
   hipEvent_t last;
   NFT_HIP_CHECK(hipEventCreate(&last));
   NFT_HIP_CHECK(hipEventRecord(last, stream));
@@ -60,7 +78,8 @@ int nft_prof_end(hipStream_t stream, float* ms, int cap, int* n) {
     ms[k] = t;
   }
   *n = k;
-  hipEventDestroy(last);
+  NFT_HIP_CHECK(hipEventDestroy(last));
+  NFT_HIP_CHECK(g_err);  // a mark that could not be recorded: the times above skip it
   return NFT_OK;
 }
 

@@ -21,6 +21,7 @@ scan kernels on constants precomputed at the expansion point.  CFJacobian also i
 ``metric_flat`` so that SandwichOperator and the fused CG can evaluate
 J^T W J without materialising the operator tree."""
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -729,14 +730,20 @@ class CFJacobian(LinearOperator):
         return c[dtype]
 
     def _weight(self, W, dtype):
-        """a pointwise weight tensor in the storage dtype (cached per tensor)"""
+        """a pointwise weight tensor in the storage dtype: ONE cached copy,
+        keyed on the tensor object itself (a weak reference: a new W at a
+        recycled address is not mistaken for the old one) and its version
+        counter (an in-place update of W is seen)"""
         if not torch.is_tensor(W) or W.dtype == dtype:
             return W
-        c = self.__dict__.setdefault("_w32", {})
-        key = (W.data_ptr(), dtype)
-        if key not in c:
-            c[key] = W.to(dtype).contiguous()
-        return c[key]
+        c = self.__dict__.get("_w32")
+        if c is not None:
+            ref, ver, dt, val = c
+            if ref() is W and ver == W._version and dt == dtype:
+                return val
+        val = W.to(dtype).contiguous()
+        self._w32 = (weakref.ref(W), W._version, dtype, val)
+        return val
 
     def phases_fp32(self, k):
         """True if the phase methods (mv_*) run on fp32 storage: the

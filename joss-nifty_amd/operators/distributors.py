@@ -79,7 +79,13 @@ class BinIndex:
         offs = np.zeros(self.nbin + 1, dtype=np.int64)
         np.cumsum(np.bincount(f, minlength=self.nbin), out=offs[1:])
         cb = _chunk_bins(offs, self.nbin, f.size)
-        return dict(shape=tuple(int(n) for n in shp), nf=int(f.size),
+        # the interleaved scatter's chunk -> first bin tables, made here on the
+        # host (a first use inside a HIP-graph capture must not sync)
+        lib = _native.load()
+        il_cb = {pre: torch.from_numpy(_chunk_bins(offs, self.nbin, f.size,
+                                                   int(lib.nft_bin_scatter_il_chunk(pre)))).to(device)
+                 for pre in (2, 4, 8)}
+        return dict(shape=tuple(int(n) for n in shp), nf=int(f.size), il_cb=il_cb,
                     pindex=torch.from_numpy(f.astype(np.int32)).to(device),   # cell -> bin
                     perm=torch.from_numpy(perm.astype(np.int32)).to(device),
                     offsets=torch.from_numpy(offs.astype(np.int32)).to(device),
@@ -106,8 +112,8 @@ class BinIndex:
                                        order=self.gather_order)
         wf = torch.empty((pre, f["nf"]), dtype=w.dtype, device=w.device)
         _native.bin_fold(w, wf, pre, f["shape"])
-        return _native.bin_scatter(wf, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
-                                   order=f["order"])
+        return _native.bin_scatter_folded(wf, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin,
+                                          chunk_bins=f["order"][2])
 
     # the half-grid fold with the items interleaved (bin_fold_half_sorted,
     # cpos None) + bin sums gathering all items of a cell at once
@@ -142,19 +148,13 @@ class BinIndex:
         if isinstance(src, _ILFold):
             return _native.bin_scatter_il(src.t, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin,
                                           chunk_bins=self._il_chunk_bins(pre))
-        return _native.bin_scatter(src, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin, 1,
-                                   order=f["order"])
+        return _native.bin_scatter_folded(src, f["perm"], f["offsets"], out, pre, f["nf"], self.nbin,
+                                          chunk_bins=f["order"][2])
 
     def _il_chunk_bins(self, pre):
-        """the interleaved scatter's chunk -> first bin table (per item count;
-        made once, on the host, from the folded offsets)"""
-        f = self.fold
-        cache = f.setdefault("il_cb", {})
-        if pre not in cache:
-            ch = int(_native.load().nft_bin_scatter_il_chunk(pre))
-            offs = f["offsets"].cpu().numpy().astype(np.int64)
-            cache[pre] = torch.from_numpy(_chunk_bins(offs, self.nbin, f["nf"], ch)).to(f["offsets"].device)
-        return cache[pre]
+        """the interleaved scatter's chunk -> first bin table of an item count
+        (pre in 2, 4, 8; made with the plan, _make_fold)"""
+        return self.fold["il_cb"][pre]
 
     @property
     def gather_order(self):
