@@ -15,6 +15,7 @@ Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline
 and CPU-baseline definitions.
 """
 import argparse
+import collections
 import json
 import os
 import sys
@@ -395,10 +396,13 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
         tot_us += tot * 1e3 / reps
         tot_b += (by or 0) * (cnt // reps)
     wall_us = cg_iteration_wall(lib, core, W, shift, bufs, k)
+    # the per-launch byte model of the kernel table (every operand array once
+    # per launch), over the same iteration time -- a bandwidth, not a second
+    # roofline fraction: the line's fraction is roofline.frac (SURVEY §8(d)
+    # bytes) beside roofline.traffic_frac (PMC bytes)
     it = {"rhs": k, "us_per_iteration": round(wall_us, 1), "timing": "HIP graph replay of the iteration body",
-          "us_sum_of_launches": round(tot_us, 1), "algorithmic_bytes": tot_b,
-          "gbs": round(tot_b / (wall_us * 1e-6) / 1e9, 1),
-          "frac": round(tot_b / (wall_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+          "us_sum_of_launches": round(tot_us, 1), "launch_model_bytes": tot_b,
+          "launch_model_gbs": round(tot_b / (wall_us * 1e-6) / 1e9, 1)}
     return out, it
 
 
@@ -460,8 +464,13 @@ def roofline_of(kp, cgit, cf, R, config="C3"):
             break
         traffic += t * e["launches"]
     dom = max(kp, key=lambda lab: kp[lab]["avg_us"] * kp[lab]["launches"])
+    # the rocprof-achieved bandwidth north_star asks for: PMC HBM bytes of the
+    # iteration's launches over the same iteration time
+    tfrac = None if traffic is None else round(traffic / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "cg_iteration",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_frac": tfrac,
+            "traffic_source": "profiles/" + ("pmc_traffic.json" if config == "C3" else f"pmc_traffic_{config}.json"),
+            "kernel": "cg_iteration",
             "rhs": k, "avg_launch_us": us, "algorithmic_bytes_per_launch": by,
             "bytes_model": bytes_model_text(config),
             "largest_kernel": {"label": dom, "avg_us": kp[dom]["avg_us"], "launches": kp[dom]["launches"],
@@ -562,6 +571,7 @@ def newton_roofline(ift, one, R):
     if not torch.cuda.is_available():
         return None
     rec = [0, 0, 0.0]
+    paths = collections.Counter()
     orig = fused_cg.FusedCGBatch.run_packed
 
     def run_packed(self, X, Rr, Bv, starts):
@@ -575,8 +585,10 @@ def newton_roofline(ift, one, R):
         rec[0] += 1
         rec[1] += ift.ConjugateGradient.iterations_total - it0
         rec[2] += time.perf_counter() - t
+        paths[getattr(self, "path", "?")] += 1
         return r
     fused_cg.FusedCGBatch.run_packed = run_packed
+    spec0 = fused_cg.STATS["pipelined_spec"]
     try:
         one()
     finally:
@@ -593,8 +605,9 @@ def newton_roofline(ift, one, R):
     return {"solves": rec[0], "rhs_iters": rec[1], "ms": round(rec[2] * 1e3, 1),
             "us_per_rhs_iter": round(rec[2] * 1e6 / rec[1], 1), "bytes_per_rhs_iter": per,
             "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s", "frac": round(gbs / 8000.0, 4),
-            "path": "per-iteration host read, separate direction / curvature d.q / update passes "
-                    "(value-driven AbsDelta controller)"}
+            "path": "separate direction / curvature d.q / update passes (value-driven controllers keep the "
+                    "reference's d.q); solves by fused_cg path: " + ", ".join(f"{p} {n}" for p, n in sorted(paths.items())),
+            "speculative_steps": int(fused_cg.STATS["pipelined_spec"] - spec0)}
 
 
 class _TimedComm:

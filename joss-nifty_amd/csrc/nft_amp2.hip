@@ -188,8 +188,10 @@ __device__ __forceinline__ void scan_arr(double (&v)[NA][EE], double (&tot)[NA],
 // each other): one write-back per workgroup measured 2-3x slower here
 // (round 4: a VJP first launch 36 -> 131 us, second 116 -> 210 us at C3).
 // Values handed to a LATER launch need neither (kernel boundaries write back
-// and invalidate the L2s).  The counters are one device-global set: these
-// kernels must not run concurrently on two streams (nifty_amd.h).
+// and invalidate the L2s).  The counters are one device-global set (and the
+// callers share one workspace): two calls must never run concurrently.  The
+// launcher enforces it (guard_enter below): a call on another stream than
+// the previous call's waits for that stream's work first.
 constexpr int NGRP = 16;
 struct Line {
   unsigned v[16];  // one 64-byte line per counter
@@ -255,6 +257,9 @@ __device__ __forceinline__ void chunk_scan(const double (&x)[Q], double (&ex)[Q]
   run += t[0];
 }
 constexpr int CQ = 2;  // tiles per thread in the carry scans (chunks of 512 tiles)
+#ifndef NFT_AMP2_FINK
+#define NFT_AMP2_FINK 0
+#endif
 
 // ======================================================================= JVP
 // VT: storage of the latent vectors, da and g (double, or float for the
@@ -938,6 +943,9 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
 // (plain: outputs; cg: the update), tile 0 the scalar cotangents; cg: the
 // r.r / x.r partials and the finalize by the last workgroup of the grid.
 // TB: the constant scans from the table
+template <typename VT>
+__device__ __forceinline__ void fin_rhs(const Vjp2Args<VT>& a, int r, double* sh);
+
 template <typename VT, int MODE, bool TB>
 __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
   __shared__ double sh[3 * E * NW + 8];
@@ -1097,9 +1105,17 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
   }
   // finalize (the last workgroup of the grid): the tile partials of every
   // RHS folded in index order, then cg_finalize_kernel's bookkeeping
+  if (NFT_AMP2_FINK) return;  // a kernel of its own (fin_kernel)
   if (!last_arrival(g_arrive[2][0], i * a.nrhs + r, nb * a.nrhs, &lflag)) return;
-  for (int rr_ = 0; rr_ < a.nrhs; ++rr_) {
-    const double* pp = a.part + (long long)rr_ * a.pstride;
+  for (int rr_ = 0; rr_ < a.nrhs; ++rr_) fin_rhs(a, rr_, sh);
+}
+
+// the finalize of RHS r (vjp2b_kernel's last workgroup, or fin_kernel)
+template <typename VT>
+__device__ __forceinline__ void fin_rhs(const Vjp2Args<VT>& a, int r, double* sh) {
+  const int tid = threadIdx.x, nb = a.nb;
+  {
+    const double* pp = a.part + (long long)r * a.pstride;
     double f[2] = {0.0, 0.0};
     for (int t = tid; t < nb; t += NT) {
       f[0] += cld(pp + t);
@@ -1107,7 +1123,7 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
     }
     btot<2>(f, sh);
     if (tid == 0) {
-      double* scb = a.sc + (long long)rr_ * NS_;
+      double* scb = a.sc + (long long)r * NS_;
       if (scb[NFT_CG_DONE] == 0.0) {
         const double curv = scb[NFT_CG_CURV], gprev = scb[NFT_CG_GAMMA];
         const double alpha = gprev / curv;
@@ -1125,6 +1141,13 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
       }
     }
   }
+}
+
+// the finalize as its own launch (NFT_AMP2_FINK): one workgroup per RHS
+template <typename VT>
+__global__ __launch_bounds__(NT) void fin_kernel(Vjp2Args<VT> a) {
+  __shared__ double sh[8 * NW];
+  fin_rhs(a, (int)blockIdx.x, sh);
 }
 
 // ======================================================== constant-scan table
@@ -1255,6 +1278,30 @@ __global__ __launch_bounds__(NT) void prep_kernel(AmpConst c0_, const AmpConst* 
 // ------------------------------------------------------------------ launch
 static int nblk(long long n, long long per) { return (int)std::max<long long>(1, (n + per - 1) / per); }
 
+// Cross-stream ordering of the calls (the device-global arrival counters and
+// the shared workspace make two concurrently running calls corrupt each
+// other): a call on a different stream than the previous eager call first
+// waits on the host for that stream's work (hipStreamSynchronize), so calls
+// from any number of streams execute one after the other, and single-stream
+// use -- every call on the hot path -- pays nothing on the device (an event
+// recorded after every call measured +5 us per launch pair).  A call on a
+// stream under HIP-graph capture is not tracked: a captured graph is ordered
+// by its replay stream, so graphs holding these kernels must not be replayed
+// concurrently with each other or with eager calls on another stream.
+static hipStream_t g_last_stream = nullptr;
+static bool g_any_call = false;
+static bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+static int guard_enter(hipStream_t s) {
+  if (capturing(s)) return NFT_OK;
+  if (g_any_call && s != g_last_stream) NFT_HIP_CHECK(hipStreamSynchronize(g_last_stream));
+  g_last_stream = s;
+  g_any_call = true;
+  return NFT_OK;
+}
+
 // NFT_AMP2=0: off (the multi-kernel path); nft_amp2_set_enabled overrides
 // the environment (tests, A/B)
 static int g_override = -1;
@@ -1351,6 +1398,7 @@ int amp2_jvp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, i
   a.tab = tab;
   const bool tb = tab != nullptr;
   const dim3 grid(grid_of(nb, nrhs));
+  if (int st = guard_enter(stream)) return st;
   prof_mark(stream, a.dir ? "amp_jvp2a+dir" : "amp_jvp2a");
   NFT_AMP2_LAUNCH(jvp2a_kernel, VT, item_mode, tb, grid, stream, a);
   prof_mark(stream, "amp_jvp2b");
@@ -1392,10 +1440,15 @@ int amp2_vjp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, i
   a.tab = tab;
   const bool tb = tab != nullptr;
   const dim3 grid(grid_of(nb, nrhs));
+  if (int st = guard_enter(stream)) return st;
   prof_mark(stream, a.cg ? "amp_vjp2a+cg" : "amp_vjp2a");
   NFT_AMP2_LAUNCH(vjp2a_kernel, VT, item_mode, tb, grid, stream, a);
   prof_mark(stream, a.cg ? "amp_vjp2b+cg" : "amp_vjp2b");
   NFT_AMP2_LAUNCH(vjp2b_kernel, VT, item_mode, tb, grid, stream, a);
+  if (NFT_AMP2_FINK && a.cg) {
+    prof_mark(stream, "amp_fin");
+    hipLaunchKernelGGL((fin_kernel<VT>), dim3((unsigned)nrhs), dim3(NT), 0, stream, a);
+  }
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

@@ -920,6 +920,12 @@ constexpr long long PRO_ROWS_MAXH = (160 * 1024 - 4 * 8 * 8) / (8 * 8);
 __host__ __device__ inline bool pro_rows_ok(int D, long long nlast) {
   return D >= 2 && nlast / 2 + 1 <= PRO_ROWS_MAXH;
 }
+// workgroups (= d.d partial slots) of the row-staged prologue
+__host__ __device__ inline long long pro_rows_groups(int D, const long long* n) {
+  long long nrg = 1;
+  for (int a = 0; a < D - 1; ++a) nrg *= n[a] / 2 + 1;
+  return nrg;
+}
 
 template <typename T, int D, int NBM, bool PI>
 __global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __restrict__ u, long long P, int nb) {
@@ -1084,8 +1090,7 @@ __global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __re
 
 template <typename T, int D, int NBM, bool PI>
 static int launch_pro_rows_n(const fast::FuseArgs& f, T* u, hipStream_t s) {
-  long long nrg = 1;
-  for (int a = 0; a < D - 1; ++a) nrg *= f.fn[a] / 2 + 1;
+  const long long nrg = pro_rows_groups(D, f.fn);
   const size_t lds = (size_t)(f.fn[D - 1] / 2 + 1) * NBM * sizeof(T);
   if (lds > 65536) {
     // the attribute of this instance raised to the largest size asked so far
@@ -1463,9 +1468,9 @@ int nft_hartley_dir_blocks(int ndim, const int64_t* shape) {
     if (shape[a] < 1) return 0;
   if (pro_rows_ok(ndim, shape[ndim - 1])) {
     // the row-staged prologue: one block per group of mirror rows
-    long long nrg = 1;
-    for (int a = 0; a < ndim - 1; ++a) nrg *= shape[a] / 2 + 1;
-    return (int)nrg;
+    long long n[3];
+    for (int a = 0; a < ndim; ++a) n[a] = shape[a];
+    return (int)pro_rows_groups(ndim, n);
   }
   long long ncell = 1;
   for (int a = 0; a < ndim; ++a) {

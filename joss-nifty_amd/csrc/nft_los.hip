@@ -34,7 +34,37 @@ constexpr int LOS_CAP_F = 2048;  // entries per forward work item (host-guarante
 constexpr int LOS_CH_A = 2048;   // adjoint: entries staged in LDS per chunk
 constexpr int LOS_YL = 2048;     // adjoint: LDS slots for the line values of a box (all batch vectors)
 constexpr int LOS_KMAX = 8;      // vectors per batched launch
-constexpr int LOS_SEG_ROUNDS = 4;  // forward: <= 256 segments per item = 4 rounds of 64 quads (host-guaranteed)
+// forward: one lane per segment (<= 256 segments per work item,
+// host-guaranteed: one round of the 256 lanes), summing the segment's
+// entries in the order the earlier four-lane groups did -- four strided
+// partial sums (entries a + q, a + q + 4, ... into acc[q]), then
+// (acc0 + acc1) + (acc2 + acc3), the quad's xor-shuffle tree -- so the
+// results are bitwise those of four lanes per segment (the sampling CG with
+// value-driven controllers follows the reference's decisions only with this
+// rounding: a plain serial sum moved demo64's AbsDelta solve from 28 to 24
+// checks).  Four lanes with shuffles: 131 us; one lane: 120 us (4 x 2048^2,
+// per-box kernel): the segments are short (16 entries on average at 2048^2 /
+// 16384 lines) and the shuffles and idle lanes of a partly filled second
+// round cost more than the longer chain per lane.
+// sum of the products w_k * u[l_k][b] over entries [a, e) of a segment for
+// the K vectors, in the four-lane order (see above)
+template <int K, typename F>
+__device__ __forceinline__ void seg_sum4(int a, int e, F&& prod, double (&out)[K]) {
+#pragma clang fp contract(off)
+  double acc[4][K];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int b = 0; b < K; ++b) acc[q][b] = 0.0;
+  for (int k = a; k < e; k += 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (k + q < e) prod(k + q, acc[q]);
+  }
+#pragma unroll
+  for (int b = 0; b < K; ++b) out[b] = (acc[0][b] + acc[1][b]) + (acc[2][b] + acc[3][b]);
+}
+
 struct BoxGeom {
   long long H, W;
   int bh, bw, nby, nbx;
@@ -52,15 +82,15 @@ struct BoxGeom {
 
 // Batched over K vectors (template, 1 <= K <= LOS_KMAX): the entries of a
 // work item (fp32 weight + 8-bit local pixel) are staged in LDS ONCE and
-// applied to every vector's tile; each segment's 4-lane group accumulates all
-// K vectors in registers.  Per vector the products and their summation order
+// applied to every vector's tile; each segment's lane accumulates all K
+// vectors in registers.  Per vector the products and their summation order
 // are those of K = 1 (bitwise).
 //
 // Segment s's partial of vector b goes to part[seg_slot[s] * pk + b] (pk =
 // vectors of the call): one contiguous store per segment for all vectors, and
-// the reduce reads each line's slots contiguously.  The bounds and slots of
-// all of a thread's segments (LOS_SEG_ROUNDS rounds of 64) are loaded before
-// the barrier, off the critical path of the segment loop.
+// the reduce reads each line's slots contiguously.  The bounds and slot of a
+// thread's segment are loaded before the barrier, off the critical path of
+// the segment loop.
 
 template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __restrict__ x,
@@ -106,18 +136,12 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
     }
     u[t][b] = v;
   }
-  // four lanes per segment: thread t serves segments sq + 64 r
-  constexpr int RND = LOS_SEG_ROUNDS;
-  const int sub = t & 3;
-  const int sq = s0 + (t >> 2);
-  int sa[RND], sb[RND], so[RND];
-#pragma unroll
-  for (int r = 0; r < RND; ++r) {
-    const int s = sq + 64 * r;
-    sa[r] = s < s1 ? p.seg_ent[s] - e0 : 0;
-    sb[r] = s < s1 ? p.seg_ent[s + 1] - e0 : 0;
-    so[r] = s < s1 ? p.seg_slot[s] : 0;
-  }
+  // one lane per segment: thread t serves segment s0 + t (+ 256 r beyond
+  // the host guarantee)
+  const int sq = s0 + t;
+  const int sa = sq < s1 ? p.seg_ent[sq] - e0 : 0;
+  const int sb = sq < s1 ? p.seg_ent[sq + 1] - e0 : 0;
+  const int so = sq < s1 ? p.seg_slot[sq] : 0;
   if (K > 1 && staged) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -141,45 +165,33 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
     }
     __syncthreads();
     auto seg1 = [&](int slot, int a, int e) {
-      double a0 = 0.0;
+      double a0[1];
       if (staged) {
-        for (int k = a + sub; k < e; k += 4) a0 += prod[k];
+        seg_sum4<1>(a, e, [&](int k, double(&acc)[1]) { acc[0] += prod[k]; }, a0);
       } else {
-        for (int k = a + sub; k < e; k += 4) a0 = a0 + (double)p.ent_wf[e0 + k] * u[p.ent_loc[e0 + k]][0];
+        seg_sum4<1>(a, e, [&](int k, double(&acc)[1]) {
+          acc[0] = acc[0] + (double)p.ent_wf[e0 + k] * u[p.ent_loc[e0 + k]][0];
+        }, a0);
       }
-      a0 += __shfl_xor(a0, 1, 64);
-      a0 += __shfl_xor(a0, 2, 64);
-      if (sub == 0) part[(long long)slot * pk] = a0;
+      part[(long long)slot * pk] = a0[0];
     };
-#pragma unroll
-    for (int r = 0; r < RND; ++r)
-      if (sq + 64 * r < s1) seg1(so[r], sa[r], sb[r]);
-    for (int s = sq + 64 * RND; s < s1; s += 64) seg1(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
+    if (sq < s1) seg1(so, sa, sb);
+    for (int s = sq + 256; s < s1; s += 256) seg1(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
     return;
   }
   auto segk = [&](int slot, int a, int e) {
     double acc[K];
-#pragma unroll
-    for (int b = 0; b < K; ++b) acc[b] = 0.0;
-    for (int k = a + sub; k < e; k += 4) {
+    seg_sum4<K>(a, e, [&](int k, double(&c)[K]) {
       const double w = staged ? (double)ew[k] : (double)p.ent_wf[e0 + k];
       const int l = staged ? el[k] : p.ent_loc[e0 + k];
 #pragma unroll
-      for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
-    }
+      for (int b = 0; b < K; ++b) c[b] = c[b] + w * u[l][b];
+    }, acc);
 #pragma unroll
-    for (int b = 0; b < K; ++b) {
-      double v = acc[b];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      // every lane of the quad holds the sum: lane sub stores vectors sub, sub + 4
-      if ((b & 3) == sub) part[(long long)slot * pk + b] = v;
-    }
+    for (int b = 0; b < K; ++b) part[(long long)slot * pk + b] = acc[b];
   };
-#pragma unroll
-  for (int r = 0; r < RND; ++r)
-    if (sq + 64 * r < s1) segk(so[r], sa[r], sb[r]);
-  for (int s = sq + 64 * RND; s < s1; s += 64) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
+  if (sq < s1) segk(so, sa, sb);
+  for (int s = sq + 256; s < s1; s += 256) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
 }
 
 // One workgroup per box (nft_los_plan.box_item, K > 1): the pixel tile's
@@ -196,7 +208,6 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
                                                      long long xs, int pk, long long css) {
 #pragma clang fp contract(off)
   static_assert(K > 1, "one vector takes los_fwd_items");
-  constexpr int RND = LOS_SEG_ROUNDS;
   __shared__ __align__(16) double u[256][K];
   __shared__ __align__(16) float ew[LOS_CAP_F + 16];
   __shared__ __align__(16) unsigned char el[LOS_CAP_F + 16];
@@ -227,7 +238,6 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
     s1 = p.item_seg[ci + 1];
     e1 = p.item_ent[ci + 1];
   }
-  const int sub = t & 3;
   for (bool first = true;; first = false) {
     const int n = e1 - e0;
     const int eo = e0 & 15;
@@ -241,15 +251,10 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
 #pragma unroll
       for (int j = 0; j < 4; ++j) vw[j] = *(const float4*)(p.ent_wf + c + 4 * j);
     }
-    const int sq = s0 + (t >> 2);
-    int sa[RND], sb[RND], so[RND];
-#pragma unroll
-    for (int r = 0; r < RND; ++r) {
-      const int s = sq + 64 * r;
-      sa[r] = s < s1 ? p.seg_ent[s] - e0 : 0;
-      sb[r] = s < s1 ? p.seg_ent[s + 1] - e0 : 0;
-      so[r] = s < s1 ? p.seg_slot[s] : 0;
-    }
+    const int sq = s0 + t;  // one lane per segment (<= 256 per work item)
+    const int sa = sq < s1 ? p.seg_ent[sq] - e0 : 0;
+    const int sb = sq < s1 ? p.seg_ent[sq + 1] - e0 : 0;
+    const int so = sq < s1 ? p.seg_slot[sq] : 0;
     if (first) {
 #pragma unroll
       for (int b = 0; b < K; ++b) u[t][b] = xv[b];
@@ -262,26 +267,16 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
       for (int j = 0; j < 4; ++j) *(float4*)(ew + 16 * t + 4 * j) = vw[j];
     }
     __syncthreads();
+    if (sq < s1) {
+      double acc[K];
+      seg_sum4<K>(sa + eo, sb + eo, [&](int k, double(&c)[K]) {
+        const double w = (double)ew[k];
+        const int l = el[k];
 #pragma unroll
-    for (int r = 0; r < RND; ++r) {
-      if (sq + 64 * r < s1) {
-        double acc[K];
+        for (int b = 0; b < K; ++b) c[b] = c[b] + w * u[l][b];
+      }, acc);
 #pragma unroll
-        for (int b = 0; b < K; ++b) acc[b] = 0.0;
-        for (int k = sa[r] + eo + sub; k < sb[r] + eo; k += 4) {
-          const double w = (double)ew[k];
-          const int l = el[k];
-#pragma unroll
-          for (int b = 0; b < K; ++b) acc[b] = acc[b] + w * u[l][b];
-        }
-#pragma unroll
-        for (int b = 0; b < K; ++b) {
-          double v = acc[b];
-          v += __shfl_xor(v, 1, 64);
-          v += __shfl_xor(v, 2, 64);
-          if ((b & 3) == sub) part[(long long)so[r] * pk + b] = v;
-        }
-      }
+      for (int b = 0; b < K; ++b) part[(long long)so * pk + b] = acc[b];
     }
     if (!multi || ++ci >= ci1) break;
     s0 = s1;

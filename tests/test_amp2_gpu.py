@@ -289,3 +289,78 @@ def test_logging_controller_sees_every_energy(ift):
     assert len(h.energy_values) == logged._itcount + 2 == 10
     assert h.energy_values[0] == h.energy_values[1]
     assert h.energy_values[-1] == pytest.approx(r1[0].value, rel=1e-9)
+
+
+def test_amp2_calls_on_two_streams(ift, restore):
+    """Calls of the two-phase kernels (device-global arrival counters, one
+    shared workspace) issued alternately on two streams with no host sync
+    between them run one after the other (nft_amp2's stream guard): bitwise
+    the results of the same calls on one stream."""
+    _toggle(1)
+    with ift.random.Context(31):
+        cf, amp, keys, c, (const, keep), lin, lay, D, off = _setup(ift, (2048, 2048), CF_ARGS, 4)
+    B, dev = amp.B, D.device
+    gen = torch.Generator(device=dev).manual_seed(31)
+    gs = [torch.randn((4, B), dtype=torch.float64, device=dev, generator=gen) for _ in range(6)]
+    Ds = [D * (1.0 + 0.125 * i) for i in range(6)]
+
+    def run(i):
+        da = torch.empty((B, 4), dtype=torch.float64, device=dev)
+        amp.native_jvp_batched(lin, Ds[i], off, da, interleave=True)
+        Q = torch.zeros_like(D)
+        amp.native_vjp_batched(lin, gs[i], Q, off, Ds[i], 0.75)
+        return da, Q
+    ref = [run(i) for i in range(6)]
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    cur = torch.cuda.current_stream()
+    s1.wait_stream(cur)
+    s2.wait_stream(cur)
+    out = []
+    for i in range(6):
+        with torch.cuda.stream(s1 if i % 2 == 0 else s2):
+            out.append(run(i))
+    torch.cuda.synchronize()
+    for i in range(6):
+        assert torch.equal(out[i][0], ref[i][0]), i
+        assert torch.equal(out[i][1], ref[i][1]), i
+
+
+def test_two_captured_iteration_graphs_bitwise(ift):
+    """Two HIP graphs of the bench's batched CG iteration (bench.cg_iteration:
+    the carried iteration with the two-phase amplitude kernels, whose arrival
+    counters and workspace every launch shares) on two buffer sets, replayed
+    back to back A B A B: bitwise the same four iterations run eagerly."""
+    import bench
+    from nifty_amd import _native
+    from nifty_amd.minimization import fused_cg
+    cf, R, lh, pos, _ = bench.build_problem(ift, 256, 2048, "C3")
+    lib = _native.load()
+    k = 4
+    core, W, shift, XS = bench.probe_setup(ift, lh, pos, k)
+    n = XS.shape[1]
+
+    def fresh(scale):
+        X, Rr, D = (XS[i * k:(i + 1) * k] * scale for i in range(3))
+        SC = torch.zeros((k, _native.CG_NSCALARS), dtype=torch.float64, device=XS.device)
+        SC[:, _native.CG_GAMMA] = 1.0
+        SC[:, _native.CG_GPREV] = 1.0
+        ws = torch.empty(k * lib.nft_reduce_workspace(n), dtype=torch.uint8, device=XS.device)
+        return (X.clone(), Rr.clone(), D.clone(), torch.zeros_like(X), SC, ws)
+
+    warm = fresh(1.0)
+    bench.cg_iteration(lib, core, W, shift, warm, k)   # plans, tables, first-use allocations
+    torch.cuda.synchronize()
+    eager = {"A": fresh(1.0), "B": fresh(0.5)}
+    for name in "ABAB":
+        bench.cg_iteration(lib, core, W, shift, eager[name], k)
+    graph = {"A": fresh(1.0), "B": fresh(0.5)}
+    gr = {name: fused_cg._capture(lambda b=graph[name]: bench.cg_iteration(lib, core, W, shift, b, k))
+          for name in "AB"}
+    for name in "ABAB":
+        gr[name].replay()
+    torch.cuda.synchronize()
+    for name in "AB":
+        for i, (a, b) in enumerate(zip(eager[name][:5], graph[name][:5])):
+            assert torch.equal(a, b), (name, i)
+
