@@ -170,8 +170,7 @@ __device__ __forceinline__ void scan_arr(double (&v)[NA][EE], double (&tot)[NA],
 
 // ------------------------------------------------------------ arrival
 // Per-RHS arrival counters of the first launches (the last workgroup of a
-// RHS forms that RHS's tile carries) and the grid counter of the VJP's second
-// launch (its last workgroup runs the CG finalize).  Hierarchical: arrival i
+// RHS forms that RHS's tile carries).  Hierarchical: arrival i
 // of n counts at group counter i % 16, the last arrival of a group at the top
 // counter -- a few hundred atomics on ONE address serialise at the memory-side
 // atomic unit (tens of microseconds), sixteen lines do not.  Each counter is
@@ -196,7 +195,7 @@ constexpr int NGRP = 16;
 struct Line {
   unsigned v[16];  // one 64-byte line per counter
 };
-__device__ Line g_arrive[3][MAXR][NGRP + 1];
+__device__ Line g_arrive[2][MAXR][NGRP + 1];
 
 // true in exactly one of the n workgroups (arrival index idx) that call it
 // with the same counter set, after every caller's device-coherent stores
@@ -257,9 +256,7 @@ __device__ __forceinline__ void chunk_scan(const double (&x)[Q], double (&ex)[Q]
   run += t[0];
 }
 constexpr int CQ = 2;  // tiles per thread in the carry scans (chunks of 512 tiles)
-#ifndef NFT_AMP2_FINK
-#define NFT_AMP2_FINK 0
-#endif
+
 
 // ======================================================================= JVP
 // VT: storage of the latent vectors, da and g (double, or float for the
@@ -943,13 +940,9 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
 // (plain: outputs; cg: the update), tile 0 the scalar cotangents; cg: the
 // r.r / x.r partials and the finalize by the last workgroup of the grid.
 // TB: the constant scans from the table
-template <typename VT>
-__device__ __forceinline__ void fin_rhs(const Vjp2Args<VT>& a, int r, double* sh);
-
 template <typename VT, int MODE, bool TB>
 __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
   __shared__ double sh[3 * E * NW + 8];
-  __shared__ int lflag;
   int i, r;
   const bool valid = place(a.nb, a.nrhs, i, r);
   if (!valid) return;
@@ -1099,18 +1092,19 @@ __global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
   btot<2>(v, sh);
   if (tid == 0) {
     double* pp = a.part + (long long)r * a.pstride;
-    // this tile's amplitude sums, then its slice of the grid partials
-    cst(pp + i, v[0] + W[(long long)V_CRR * nb + i]);
-    cst(pp + nb + i, v[1] + W[(long long)V_CXR * nb + i]);
+    // this tile's amplitude sums, then its slice of the grid partials (read
+    // by fin_kernel)
+    pp[i] = v[0] + W[(long long)V_CRR * nb + i];
+    pp[nb + i] = v[1] + W[(long long)V_CXR * nb + i];
   }
-  // finalize (the last workgroup of the grid): the tile partials of every
-  // RHS folded in index order, then cg_finalize_kernel's bookkeeping
-  if (NFT_AMP2_FINK) return;  // a kernel of its own (fin_kernel)
-  if (!last_arrival(g_arrive[2][0], i * a.nrhs + r, nb * a.nrhs, &lflag)) return;
-  for (int rr_ = 0; rr_ < a.nrhs; ++rr_) fin_rhs(a, rr_, sh);
+  // the finalize runs as a launch of its own (fin_kernel): a last-arrival
+  // finalize in this kernel made every workgroup wait for its stores and an
+  // atomic before it could retire (4-RHS VJP at 2048^2 45 -> 37 + 6 us, 4096^2
+  // fp32 153 -> 140 + 6 us; iteration -9 us at both)
 }
 
-// the finalize of RHS r (vjp2b_kernel's last workgroup, or fin_kernel)
+// the finalize of RHS r: the tile partials folded in index order, then
+// cg_finalize_kernel's bookkeeping
 template <typename VT>
 __device__ __forceinline__ void fin_rhs(const Vjp2Args<VT>& a, int r, double* sh) {
   const int tid = threadIdx.x, nb = a.nb;
@@ -1118,8 +1112,8 @@ __device__ __forceinline__ void fin_rhs(const Vjp2Args<VT>& a, int r, double* sh
     const double* pp = a.part + (long long)r * a.pstride;
     double f[2] = {0.0, 0.0};
     for (int t = tid; t < nb; t += NT) {
-      f[0] += cld(pp + t);
-      f[1] += cld(pp + nb + t);
+      f[0] += pp[t];
+      f[1] += pp[nb + t];
     }
     btot<2>(f, sh);
     if (tid == 0) {
@@ -1143,7 +1137,7 @@ __device__ __forceinline__ void fin_rhs(const Vjp2Args<VT>& a, int r, double* sh
   }
 }
 
-// the finalize as its own launch (NFT_AMP2_FINK): one workgroup per RHS
+// the finalize: one workgroup per RHS, after every tile of vjp2b_kernel
 template <typename VT>
 __global__ __launch_bounds__(NT) void fin_kernel(Vjp2Args<VT> a) {
   __shared__ double sh[8 * NW];
@@ -1445,7 +1439,7 @@ int amp2_vjp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, i
   NFT_AMP2_LAUNCH(vjp2a_kernel, VT, item_mode, tb, grid, stream, a);
   prof_mark(stream, a.cg ? "amp_vjp2b+cg" : "amp_vjp2b");
   NFT_AMP2_LAUNCH(vjp2b_kernel, VT, item_mode, tb, grid, stream, a);
-  if (NFT_AMP2_FINK && a.cg) {
+  if (a.cg) {
     prof_mark(stream, "amp_fin");
     hipLaunchKernelGGL((fin_kernel<VT>), dim3((unsigned)nrhs), dim3(NT), 0, stream, a);
   }

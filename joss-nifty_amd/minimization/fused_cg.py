@@ -171,9 +171,12 @@ _COUNT_ONLY_STATE = _CountOnlyState()
 CHUNK = os.environ.get("NFT_CG_CHUNK", "1") != "0"
 
 # value-driven controllers checked on the device (nft_cg_check_batched) so
-# that the host queues step i + 1 before it reads step i (NFT_CG_PIPELINE=0:
-# one synchronous read per step)
-PIPELINE = os.environ.get("NFT_CG_PIPELINE", "1") != "0"
+# that the host queues step i + 1 before it reads step i (NFT_CG_PIPELINE=1;
+# off by default: bitwise the synchronous loop, but measured slower -- demo
+# step 815 -> 870 ms, Newton-direction CG 794 -> 866 us per RHS iteration:
+# the step queued behind a solve's last one runs the whole batched matvec for
+# frozen right-hand sides, and the eager launch gaps it hides were smaller)
+PIPELINE = os.environ.get("NFT_CG_PIPELINE", "0") == "1"
 
 
 def _device_ctl(ctl):
