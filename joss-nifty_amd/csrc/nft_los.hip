@@ -95,7 +95,7 @@ struct BoxGeom {
 template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __restrict__ x,
                                                      const T* __restrict__ cs, double* __restrict__ part,
-                                                     long long xs, int pk, long long css) {
+                                                     long long xs, int pk, long long css, int kv) {
   // every product is rounded before it is summed, in all K variants alike
   // (no FMA contraction): batched results are bitwise the K = 1 results
 #pragma clang fp contract(off)
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 #pragma unroll
   for (int b = 0; b < K; ++b) {
     double v = 0.0;
-    if (ok) {
+    if (ok && b < kv) {
       v = (double)x[b * xs + px];
       if (cs) v *= (double)cs[b * css + px];
     }
@@ -188,7 +188,8 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
       for (int b = 0; b < K; ++b) c[b] = c[b] + w * u[l][b];
     }, acc);
 #pragma unroll
-    for (int b = 0; b < K; ++b) part[(long long)slot * pk + b] = acc[b];
+    for (int b = 0; b < K; ++b)
+      if (b < kv) part[(long long)slot * pk + b] = acc[b];
   };
   if (sq < s1) segk(so, sa, sb);
   for (int s = sq + 256; s < s1; s += 256) segk(p.seg_slot[s], p.seg_ent[s] - e0, p.seg_ent[s + 1] - e0);
@@ -200,17 +201,26 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 // or > 256 segments) loops over them with the tile staged once.  The entries
 // of an item are staged from the aligned 16-entry chunks covering it (one
 // uint4 of pixel indices and four float4 of weights per thread; entry k of
-// the item at LDS slot (e0 & 15) + k).  Per segment and vector the products
-// and their order are los_fwd_items' (bitwise).
+// the item at LDS slot (e0 & 15) + k).  The sums take K lanes per segment
+// (lane b: vector b; ~90 segments per box leave one lane per segment mostly
+// idle), each in seg_sum4's four-lane order: per segment and vector the
+// products and their order are los_fwd_items' (bitwise).  (Measured against
+// one lane per segment: 125-130 vs 130-132 us at 4 x 2048^2, Newton-metric
+// CG 4080-4092 vs 4113-4119 us per 7-RHS iteration; an XCD-contiguous box
+// order measured slower, 156 us -- the dense middle boxes then load a few
+// XCDs --, and a persistent grid that loads item i + G while summing item i
+// slower still, 162-186 us, at 4-5 instead of 7 waves per SIMD.)
 template <typename T, int K>
 __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __restrict__ x,
                                                      const T* __restrict__ cs, double* __restrict__ part,
-                                                     long long xs, int pk, long long css) {
+                                                     long long xs, int pk, long long css, int kv) {
 #pragma clang fp contract(off)
   static_assert(K > 1, "one vector takes los_fwd_items");
   __shared__ __align__(16) double u[256][K];
   __shared__ __align__(16) float ew[LOS_CAP_F + 16];
   __shared__ __align__(16) unsigned char el[LOS_CAP_F + 16];
+  // the item's segment ends and partial slots
+  __shared__ int send[256], sslot[256];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int box = (int)blockIdx.x;
   if (box >= p.nbox) return;
@@ -221,7 +231,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
 #pragma unroll
   for (int b = 0; b < K; ++b) {
     double v = 0.0;
-    if (ok) {
+    if (ok && b < kv) {
       v = (double)x[b * xs + px];
       if (cs) v *= (double)cs[b * css + px];
     }
@@ -251,8 +261,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
 #pragma unroll
       for (int j = 0; j < 4; ++j) vw[j] = *(const float4*)(p.ent_wf + c + 4 * j);
     }
-    const int sq = s0 + t;  // one lane per segment (<= 256 per work item)
-    const int sa = sq < s1 ? p.seg_ent[sq] - e0 : 0;
+    const int sq = s0 + t;  // segment t's end and slot (<= 256 per work item)
     const int sb = sq < s1 ? p.seg_ent[sq + 1] - e0 : 0;
     const int so = sq < s1 ? p.seg_slot[sq] : 0;
     if (first) {
@@ -266,17 +275,24 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
 #pragma unroll
       for (int j = 0; j < 4; ++j) *(float4*)(ew + 16 * t + 4 * j) = vw[j];
     }
-    __syncthreads();
     if (sq < s1) {
-      double acc[K];
-      seg_sum4<K>(sa + eo, sb + eo, [&](int k, double(&c)[K]) {
-        const double w = (double)ew[k];
-        const int l = el[k];
+      send[t] = sb;
+      sslot[t] = so;
+    }
+    __syncthreads();
+    // K lanes per segment, lane b summing vector b in the four-lane order of
+    // seg_sum4 (bitwise its value)
+    constexpr int SPR = 256 / K;
+    const int b = t % K, ns = s1 - s0;
+    for (int j = t / K; j < ns; j += SPR) {
+      const int a = (j ? send[j - 1] : 0) + eo, e = send[j] + eo;
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int k = a; k < e; k += 4) {
 #pragma unroll
-        for (int b = 0; b < K; ++b) c[b] = c[b] + w * u[l][b];
-      }, acc);
-#pragma unroll
-      for (int b = 0; b < K; ++b) part[(long long)so * pk + b] = acc[b];
+        for (int q = 0; q < 4; ++q)
+          if (k + q < e) acc[q] = acc[q] + (double)ew[k + q] * u[el[k + q]][b];
+      }
+      if (b < kv) part[(long long)sslot[j] * pk + b] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     }
     if (!multi || ++ci >= ci1) break;
     s0 = s1;
@@ -347,14 +363,14 @@ template <typename T, typename IDX, int K, bool VEC = false>
 __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* __restrict__ lidx,
                                                      const T* __restrict__ yv, const T* __restrict__ cs,
                                                      const T* __restrict__ rs, T* __restrict__ out, double scale,
-                                                     long long ys, long long os, long long rss) {
+                                                     long long ys, long long os, long long rss, int kv) {
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CH_A / 256;
   // line table: 256 lines per vector cover every box of an 8-bit-index plan
   // (boxes with more lines read y from global memory); sized per K so that
   // K = 4 fits 8 workgroups per CU (18 KB of LDS instead of 28 KB)
   constexpr int YL = 256 * K < LOS_YL ? 256 * K : LOS_YL;
-  __shared__ double yl[YL];
+  __shared__ __align__(16) double yl[YL];
   // K == 1 uses ew as a double product buffer (LOS_CH_A doubles)
   __shared__ __align__(16) float ew[K == 1 ? 2 * LOS_CH_A : LOS_CH_A];
   __shared__ __align__(16) IDX el[K == 1 ? 1 : LOS_CH_A];
@@ -373,8 +389,8 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   const long long px = g.pixel(box, t, ok);
   double rsv[K];
 #pragma unroll
-  for (int v = 0; v < K; ++v) rsv[v] = (rs && ok) ? (double)rs[v * rss + px] : 1.0;
-  const int ystr = nl;  // line-table stride per vector
+  for (int v = 0; v < K; ++v) rsv[v] = (rs && ok && v < kv) ? (double)rs[v * rss + px] : 1.0;
+  // line table, line-major: yl[li * K + v]
   // the first chunk's entry loads go out before the line-table staging so the
   // two dependent load chains overlap
   int lv[PER];
@@ -409,9 +425,9 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
       const double c = cs ? (double)cs[li] : 1.0;
 #pragma unroll
       for (int v = 0; v < K; ++v) {
-        double yy = (double)yv[v * ys + li];
+        double yy = v < kv ? (double)yv[v * ys + li] : 0.0;
         if (cs) yy *= c;
-        yl[v * nl + i] = yy;
+        yl[i * K + v] = yy;
       }
     }
   }
@@ -478,13 +494,13 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
       const int li = el[k - c0];
       if (tab) {
 #pragma unroll
-        for (int v = 0; v < K; ++v) acc[v] = acc[v] + w * yl[v * ystr + li];
+        for (int v = 0; v < K; ++v) acc[v] = acc[v] + w * yl[li * K + v];
       } else {
         const int gl = p.box_lines[l0 + li];
         const double cc = cs ? (double)cs[gl] : 1.0;
 #pragma unroll
         for (int v = 0; v < K; ++v) {
-          double yy = (double)yv[v * ys + gl];
+          double yy = v < kv ? (double)yv[v * ys + gl] : 0.0;
           if (cs) yy *= cc;
           acc[v] = acc[v] + w * yy;
         }
@@ -497,40 +513,47 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
     for (int v = 0; v < K; ++v) {
       double o = acc[v] * scale;
       if (rs) o *= rsv[v];
-      out[v * os + px] = (T)o;
+      if (v < kv) out[v * os + px] = (T)o;
     }
   }
 }
 
 template <typename T, int K>
 static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* part, long long xs, int pk,
-                        long long css, hipStream_t s) {
+                        long long css, int kv, hipStream_t s) {
   if constexpr (K > 1) {
     if (p->box_item) {
       hipLaunchKernelGGL((los_fwd_boxes<T, K>), dim3((unsigned)p->nbox), dim3(256), 0, s, *p, x, cs, part, xs, pk,
-                         css);
+                         css, kv);
       return;
     }
   }
-  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, pk, css);
+  hipLaunchKernelGGL((los_fwd_items<T, K>), dim3((unsigned)p->nitems), dim3(256), 0, s, *p, x, cs, part, xs, pk, css,
+                     kv);
 }
 
 template <typename T, typename IDX, int K>
 static void adj_boxes_k(const nft_los_plan* p, const IDX* li, const T* y, const T* cs, const T* rs, T* out,
-                        double scale, long long ys, long long os, long long rss, hipStream_t s) {
+                        double scale, long long ys, long long os, long long rss, int kv, hipStream_t s) {
   const dim3 grid((unsigned)p->nbox);
   if constexpr (K > 1 && sizeof(IDX) == 1) {
     if (p->box_ent_adj) {
       hipLaunchKernelGGL((los_adj_boxes<T, IDX, K, true>), grid, dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys, os,
-                         rss);
+                         rss, kv);
       return;
     }
   }
-  hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), grid, dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys, os, rss);
+  hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), grid, dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys, os, rss,
+                     kv);
 }
 
-// vectors are processed in groups of 8 / 4 / 2 / 1 (template sizes)
-static int kgroup(int k) { return k >= 8 ? 8 : (k >= 4 ? 4 : (k >= 2 ? 2 : 1)); }
+// vectors are processed in groups of 8 / 4 / 2 / 1 (template sizes); a
+// remainder of 5-7 (3) vectors takes ONE launch of the 8 (4) instance with
+// the missing vectors masked (kv valid), not 4 + 2 + 1 launches that each
+// stream the whole matrix (the geoVI Newton metrics' batches shrink through
+// every count as samples finish).  Per vector the arithmetic does not depend
+// on the instance (bitwise).
+static int kgroup(int k) { return k >= 5 ? 8 : (k >= 3 ? 4 : (k == 2 ? 2 : 1)); }
 
 template <typename T>
 static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, const void* rs, void* y, double* part,
@@ -539,17 +562,17 @@ static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, c
   prof_mark(s, "los_fwd_items");
   if (p->nitems > 0) {
     for (int v = 0; v < K;) {
-      const int g = kgroup(K - v);
+      const int g = kgroup(K - v), kv = std::min(g, K - v);
       const T* xv = (const T*)x + v * xs;
       const T* cv = cs ? (const T*)cs + v * css : nullptr;
       double* pv = part + v;  // slot-major partials, K per slot
       switch (g) {
-        case 8: fwd_items_k<T, 8>(p, xv, cv, pv, xs, K, css, s); break;
-        case 4: fwd_items_k<T, 4>(p, xv, cv, pv, xs, K, css, s); break;
-        case 2: fwd_items_k<T, 2>(p, xv, cv, pv, xs, K, css, s); break;
-        default: fwd_items_k<T, 1>(p, xv, cv, pv, xs, K, css, s); break;
+        case 8: fwd_items_k<T, 8>(p, xv, cv, pv, xs, K, css, kv, s); break;
+        case 4: fwd_items_k<T, 4>(p, xv, cv, pv, xs, K, css, kv, s); break;
+        case 2: fwd_items_k<T, 2>(p, xv, cv, pv, xs, K, css, kv, s); break;
+        default: fwd_items_k<T, 1>(p, xv, cv, pv, xs, K, css, 1, s); break;
       }
-      v += g;
+      v += kv;
     }
   }
   prof_mark(s, "los_fwd_reduce");
@@ -575,17 +598,17 @@ static void los_adjoint_idx(const nft_los_plan* p, const IDX* li, const void* y,
                             void* out, double scale, int K, long long ys, long long os, hipStream_t s,
                             long long rss = 0) {
   for (int v = 0; v < K;) {
-    const int g = kgroup(K - v);
+    const int g = kgroup(K - v), kv = std::min(g, K - v);
     const T* yv = (const T*)y + v * ys;
     const T* rv = rs ? (const T*)rs + v * rss : nullptr;
     T* ov = (T*)out + v * os;
     switch (g) {
-      case 8: adj_boxes_k<T, IDX, 8>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, s); break;
-      case 4: adj_boxes_k<T, IDX, 4>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, s); break;
-      case 2: adj_boxes_k<T, IDX, 2>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, s); break;
-      default: adj_boxes_k<T, IDX, 1>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, s); break;
+      case 8: adj_boxes_k<T, IDX, 8>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s); break;
+      case 4: adj_boxes_k<T, IDX, 4>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s); break;
+      case 2: adj_boxes_k<T, IDX, 2>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s); break;
+      default: adj_boxes_k<T, IDX, 1>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, 1, s); break;
     }
-    v += g;
+    v += kv;
   }
 }
 

@@ -9,6 +9,7 @@ for i in 1 2; do
     if [ "$lib" = "-" ]; then
       timeout -k 10 240 python -u tools/iter_probe.py || exit $?
     else
+      [ -d "$lib" ] && lib=$lib/libnifty_amd.so
       NFT_LIB=$PWD/$lib timeout -k 10 240 python -u tools/iter_probe.py || exit $?
     fi
   done

@@ -3,7 +3,7 @@ k right-hand sides on the geoVI Newton metric (geovi_batch._MetricCore, the
 bench's C3 problem) with AbsDeltaEnergyController(iteration_limit=10) as
 NewtonCG's direction requests use it -- wall time per iteration from the
 host -- against the graph-replayed GPU time of the same iteration body
-(direction, matvec, curvature, update).  Usage: python tools/newton_cg_probe.py [k]"""
+(direction, matvec, curvature, update).  Usage: python tools/newton_cg_probe.py [k] [--solves-only]"""
 import os
 import sys
 import time
@@ -16,6 +16,7 @@ import bench  # noqa: E402
 
 def main():
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    solves_only = "--solves-only" in sys.argv   # (for a kernel trace of the eager solves)
     import nifty_amd as ift
     from nifty_amd import _native
     from nifty_amd.minimization import fused_cg, geovi_batch
@@ -44,6 +45,21 @@ def main():
         wall = time.perf_counter() - t
         print(f"solve {rep}: {cg.niter} iterations, {wall * 1e3:.1f} ms, {wall / cg.niter * 1e6:.0f} us per "
               f"iteration (k={k}, path {cg.path})", flush=True)
+    if solves_only:
+        return
+    # where the solve loop's host time goes beyond the body and the read
+    import cProfile
+    import pstats
+    ctls = [ift.AbsDeltaEnergyController(1e-300, iteration_limit=10) for _ in range(k)]
+    cg = fused_cg.FusedCGBatch(core, None, 0.0, ctls, 20)
+    starts = [fused_cg._State(0.0, 1.0, lambda: None) for _ in range(k)]
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    pr.enable()
+    cg.run_packed(torch.zeros_like(G), -G, G, starts)
+    torch.cuda.synchronize()
+    pr.disable()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
     n = lay.size
     X, Rr, D = torch.zeros_like(G), -G.clone(), G.clone()
     Q = torch.zeros_like(X)
@@ -65,6 +81,36 @@ def main():
     ev[1].record()
     torch.cuda.synchronize()
     print(f"graph-replayed iteration body: {ev[0].elapsed_time(ev[1]) * 1e3 / 10:.0f} us (k={k})", flush=True)
+    # the same body queued eagerly back to back (no host read between):
+    # the device time of eager launches without the host's decision loop
+    torch.cuda._sleep(200_000_000)
+    ev[0].record()
+    for _ in range(10):
+        bench.cg_iteration(lib, core, None, 0.0, bufs, k)
+    ev[1].record()
+    torch.cuda.synchronize()
+    print(f"eager iteration body queued back to back: {ev[0].elapsed_time(ev[1]) * 1e3 / 10:.0f} us (k={k})",
+          flush=True)
+    # the eager loop's host round trip without the controllers: body, async
+    # copy of the scalars, wait (stream synchronize / spinning event query)
+    host = torch.zeros((k, _native.CG_NSCALARS), dtype=torch.float64).pin_memory()
+    for mode in ("stream-sync", "event-spin", "stream-sync"):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(10):
+            bench.cg_iteration(lib, core, None, 0.0, bufs, k)
+            host.copy_(SC, non_blocking=True)
+            if mode == "stream-sync":
+                torch.cuda.current_stream().synchronize()
+            else:
+                e = torch.cuda.Event()
+                e.record()
+                while not e.query():
+                    pass
+            h = host.numpy()
+            float(h[0, 0])
+        wall = (time.perf_counter() - t) / 10
+        print(f"eager body + scalar read ({mode}): {wall * 1e6:.0f} us per iteration", flush=True)
     # host enqueue time of one eager iteration body while the GPU is busy
     torch.cuda._sleep(2_000_000_000)
     ts = []
