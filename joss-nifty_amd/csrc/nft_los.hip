@@ -201,7 +201,12 @@ __global__ __launch_bounds__(256) void los_fwd_items(nft_los_plan p, const T* __
 // or > 256 segments) loops over them with the tile staged once.  The entries
 // of an item are staged from the aligned 16-entry chunks covering it (one
 // uint4 of pixel indices and four float4 of weights per thread; entry k of
-// the item at LDS slot (e0 & 15) + k).  The sums take K lanes per segment
+// the item at LDS slot (e0 & 15) + k).  LDS holds the tile, the entries and
+// the segment ends (19.5 KB at K = 4: 8 workgroups per CU; with the partial
+// slots staged too, 20.5 KB and 7 workgroups, 126-129 instead of 111-113 us at
+// 4 x 2048^2 -- the slot is loaded from global memory ahead of each segment's
+// sum instead; staging 3072 / 4096 entries instead of 2048, fewer boxes of
+// several items but 6 / 5 workgroups: 134 / 150 us).  The sums take K lanes per segment
 // (lane b: vector b; ~90 segments per box leave one lane per segment mostly
 // idle), each in seg_sum4's four-lane order: per segment and vector the
 // products and their order are los_fwd_items' (bitwise).  (Measured against
@@ -220,7 +225,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
   __shared__ __align__(16) float ew[LOS_CAP_F + 16];
   __shared__ __align__(16) unsigned char el[LOS_CAP_F + 16];
   // the item's segment ends and partial slots
-  __shared__ int send[256], sslot[256];
+  __shared__ int send[256];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
   const int box = (int)blockIdx.x;
   if (box >= p.nbox) return;
@@ -263,7 +268,6 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
     }
     const int sq = s0 + t;  // segment t's end and slot (<= 256 per work item)
     const int sb = sq < s1 ? p.seg_ent[sq + 1] - e0 : 0;
-    const int so = sq < s1 ? p.seg_slot[sq] : 0;
     if (first) {
 #pragma unroll
       for (int b = 0; b < K; ++b) u[t][b] = xv[b];
@@ -277,7 +281,6 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
     }
     if (sq < s1) {
       send[t] = sb;
-      sslot[t] = so;
     }
     __syncthreads();
     // K lanes per segment, lane b summing vector b in the four-lane order of
@@ -285,6 +288,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
     constexpr int SPR = 256 / K;
     const int b = t % K, ns = s1 - s0;
     for (int j = t / K; j < ns; j += SPR) {
+      const int so_j = p.seg_slot[s0 + j];  // issued ahead of the sum, used by its store
       const int a = (j ? send[j - 1] : 0) + eo, e = send[j] + eo;
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
       for (int k = a; k < e; k += 4) {
@@ -292,7 +296,7 @@ __global__ __launch_bounds__(256) void los_fwd_boxes(nft_los_plan p, const T* __
         for (int q = 0; q < 4; ++q)
           if (k + q < e) acc[q] = acc[q] + (double)ew[k + q] * u[el[k + q]][b];
       }
-      if (b < kv) part[(long long)sslot[j] * pk + b] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      if (b < kv) part[(long long)so_j * pk + b] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     }
     if (!multi || ++ci >= ci1) break;
     s0 = s1;
@@ -553,6 +557,9 @@ static void adj_boxes_k(const nft_los_plan* p, const IDX* li, const T* y, const 
 // stream the whole matrix (the geoVI Newton metrics' batches shrink through
 // every count as samples finish).  Per vector the arithmetic does not depend
 // on the instance (bitwise).
+// (Two launches of the 4 instance for 5-8 vectors, whose 19.5 KB of LDS
+// allow 8 workgroups per CU against 5 for the 8 instance: Newton-metric CG
+// 4175 vs 4101 us per 7-RHS iteration, 4692 vs 4572 at 8 -- one launch kept.)
 static int kgroup(int k) { return k >= 5 ? 8 : (k >= 3 ? 4 : (k == 2 ? 2 : 1)); }
 
 template <typename T>
