@@ -41,16 +41,20 @@ def main(path, reps):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
     # period of the replayed tail: the smallest L with the last reps * L names
-    # repeating every L
-    n = len(names)
+    # repeating every L, after at most a few trailing dispatches (the probe's
+    # check of the scalars after the replays)
     L = None
-    for cand in range(4, n // reps + 1):
-        tail = names[n - reps * cand:]
-        if all(tail[i] == tail[i % cand] for i in range(len(tail))):
-            L = cand
+    for skip in range(0, 9):
+        n = len(names) - skip
+        for cand in range(4, n // reps + 1):
+            tail = names[n - reps * cand:n]
+            if all(tail[i] == tail[i % cand] for i in range(len(tail))):
+                L = cand
+                break
+        if L:
             break
     assert L, "no periodic tail found"
-    tail = rows[n - reps * L:]
+    tail = rows[n - reps * L:n]
     per = defaultdict(list)
     spans = []
     order = OrderedDict()
