@@ -1,8 +1,8 @@
 """Wall time of the phases of one bench step (draw_samples + SampledKLEnergy
-at the C3 size) and how busy the GPU is inside each: the phases are timed
+at a bench config's size, C3 by default) and how busy the GPU is inside each: the phases are timed
 with a device synchronisation at their ends, the GPU busy time is the union
 of the kernel intervals torch.profiler records.  Usage:
-python tools/step_phases.py"""
+python tools/step_phases.py [--demo] [--config C2|C3|C4|C5] [--phase LABEL]"""
 import sys
 import time
 from collections import defaultdict
@@ -75,7 +75,13 @@ def main():
     import nifty_amd as ift
     from nifty_amd.minimization import geovi_batch
     ift.config.set_device("cuda:0")
-    cf, Rr, lh, pos, _ = bench.build_problem(ift, 2048, 16384)
+    c = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "C3"
+    cfg = bench.CONFIGS[c]
+    if cfg["cg"] == "fp32":
+        ift.config.set_cg_precision("fp32")
+    cf, Rr, lh, pos, _ = bench.build_problem(ift, cfg["shape"][0], 16384, c)
+    pairs = cfg["pairs"]
+    print(f"config {c}: {cfg['desc']}, {pairs} mirrored pairs", flush=True)
     if "--demo" in sys.argv:     # SURVEY 8(d)'s demo controllers (bench.py demo_step)
         H = ift.StandardHamiltonian(lh, ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=100))
         mini = ift.NewtonCG(ift.AbsDeltaEnergyController(deltaE=0.5, convergence_level=2, iteration_limit=15))
@@ -85,7 +91,7 @@ def main():
     ift.random.push_sseq_from_seed(1000)
 
     def step():
-        sl = ift.draw_samples(pos, H, mini, 4, True)
+        sl = ift.draw_samples(pos, H, mini, pairs, True)
         ift.SampledKLEnergyClass(sl, H, [], None, True)
         torch.cuda.synchronize()
     step()
@@ -129,7 +135,7 @@ def main():
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
         torch.cuda.synchronize()
         t = time.perf_counter()
-        sl = ift.draw_samples(pos, H, mini, 4, True)
+        sl = ift.draw_samples(pos, H, mini, pairs, True)
         torch.cuda.synchronize()
         WALL["draw_samples total"] += time.perf_counter() - t
         t1 = time.perf_counter()
