@@ -18,15 +18,15 @@ def label(name, seen):
     n = name
     rules = [(r"cg_dir_dd_kernel", "cg_dir_dd2"), (r"jvp2a_kernel", "amp_jvp2a+dir"), (r"jvp2b_kernel", "amp_jvp2b"),
              (r"vjp2a_kernel", "amp_vjp2a+cg"), (r"vjp2b_kernel", "amp_vjp2b+cg"), (r"pro_fold_kernel|pro_rows_kernel", "pro_fold+dir"),
-             (r"fast_kernel<double, 2048, 256, 1", "fft_r2c"), (r"fast_kernel<double, 64, 256, 0", "fft_c2c"),
+             (r"fast_kernel<double, \d+, \d+, 1, true", "fft_r2c"), (r"fast_kernel<double, \d+, \d+, 0, false", "fft_c2c"),
              (r"fin_kernel", "amp_fin"),
              (r"los_fwd_items|los_fwd_boxes|los_fwd_tiles", "los_fwd_items"), (r"los_fwd_reduce", "los_fwd_reduce"),
              (r"los_adj_boxes", "los_adj_boxes"), (r"fold_wide", "fold_partials"), (r"bin_fold", "bin_fold"),
              (r"bin_scatter", "bin_scatter"), (r"cg_update_kernel", "cg_update_seg2"),
              (r"cg_finalize_kernel", "cg_finalize_kernel")]
-    # the four-step split of 2048 is 64 x 32 (round 5): pass A length 64,
-    # the unpack pass B length 32
-    if re.search(r"fast_kernel<double, 32, 256, 3", n):
+    # the strided unpack passes (kind 3), whatever their length and thread
+    # count: the forward transform's, then the CG-carrying adjoint's
+    if re.search(r"fast_kernel<double, \d+, \d+, 3, false", n):
         k = seen["unpack"]
         seen["unpack"] += 1
         return "fft_unpack" if k == 0 else "fft_unpack+cg"
