@@ -18,6 +18,22 @@ constexpr int nt_rows(int N) { return N <= 2048 ? 256 : (N == 4096 ? 512 : 1024)
 // (N = 512 with 512 threads -- 8-line tiles, two workgroups per CU -- measured
 // slower at 512^3: C4 iteration 14.2 -> 15.1 ms)
 constexpr int nt_strided(int N) { return N <= 128 ? 256 : (N == 256 ? 512 : 1024); }
+// fp64 strided passes up to length 128 run their L = nt_strided(N) * VPT / N
+// line tile with twice the threads at VP = 4 values each: the same tile, LDS
+// and tile count (every tile partial in the same slot), twice the resident
+// waves (their ~38 KB tile held them at 4 per SIMD): at 4 x 2048^2 fft_c2c
+// 54 -> 50 us, fft_unpack 65 -> 57 us, iteration -7..-9 us.  fp32 tiles take
+// half the LDS and already run 8 waves per SIMD: VP = 4 only costs there
+// (4096^2: c2c 120 -> 130 us, unpack+quad 196 -> 211 us)
+#ifndef NFT_STRIDED_VP4
+#define NFT_STRIDED_VP4 1
+#endif
+template <typename T>
+constexpr int vp_strided(int N) { return (NFT_STRIDED_VP4 && sizeof(T) == 8 && N <= 128) ? 4 : VPT; }
+template <typename T>
+constexpr int nt_strided_launch(int N) { return nt_strided(N) * VPT / vp_strided<T>(N); }
+// (the fp64 row passes of length 512..2048 the same way, the persistent R2C at
+// 512 threads: fft_r2c 63 -> 68 us at 4 x 2048^2, not kept)
 
 inline bool is_pow2(long long n) { return n > 0 && (n & (n - 1)) == 0; }
 
@@ -36,10 +52,10 @@ inline void fourstep_split(int N, int& N1, int& N2) {
   N1 = N / N2;
 }
 
-template <typename T, int N, int NT, int KIND, bool ROWS>
+template <typename T, int N, int NT, int KIND, bool ROWS, int VP = VPT>
 static int launch_one(const FastArgs<T>& a, hipStream_t s) {
-  constexpr int L = NT * VPT / N;
-  const size_t lds = pass_lds_bytes<T, N, NT, KIND, ROWS>();
+  constexpr int L = NT * VP / N;
+  const size_t lds = pass_lds_bytes<T, N, NT, KIND, ROWS, VP>();
   long long ntiles;
   if (ROWS) {
     long long nl = (KIND == K_R2C || KIND == K_H1D) ? (a.Ireal + 1) / 2 : a.g.O;
@@ -60,15 +76,15 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   if (lds > 65536) {
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false>,
+      (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, 0, VP>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if constexpr (persist_ok<N, NT, KIND>())
-        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, true>,
+      if constexpr (persist_ok<N, NT, KIND, VP>())
+        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, true, 0, VP>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if constexpr (KIND == K_UNPACK && !ROWS) {
-        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, 1>,
+        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, 1, VP>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, 2>,
+        (void)hipFuncSetAttribute((const void*)fast_kernel<T, N, NT, KIND, ROWS, false, 2, VP>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       }
       attr_set = true;
@@ -119,39 +135,42 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     else
       ncu = 256;
   }
-  constexpr int per_cu = 8;
+  constexpr int per_cu = 8 * 256 / NT;  // 2048 threads per CU
   static const char* const kind_name[4] = {"fft_c2c", "fft_r2c", "fft_h1d", "fft_unpack"};
   static const char* const kind_fused[4] = {"fft_c2c", "fft_r2c+pro", "fft_h1d+fused", "fft_unpack+epi"};
   prof_mark(s, a.f.cg ? "fft_unpack+cg" : a.f.quad ? "fft_unpack+quad" : (a.f.pro || a.f.epi) ? kind_fused[KIND] : kind_name[KIND]);
   bool launched = false;
-  if constexpr (persist_ok<N, NT, KIND>()) {
+  if constexpr (persist_ok<N, NT, KIND, VP>()) {
     if (!launched && !a.f.pro) {
       const long long grid = std::min<long long>(ntiles, (long long)ncu * std::max(1, per_cu));
-      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, true>), dim3((unsigned)grid), dim3(NT), lds, s, b);
+      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, true, 0, VP>), dim3((unsigned)grid), dim3(NT), lds, s, b);
       launched = true;
     }
   }
   if constexpr (KIND == K_UNPACK && !ROWS) {
     if (!launched && a.f.cg) {
-      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 1>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
+      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 1, VP>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
       launched = true;
     }
     if (!launched && a.f.quad) {
-      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 2>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
+      hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 2, VP>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
       launched = true;
     }
   }
   if (!launched)
-    hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
+    hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 0, VP>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
 
 template <typename T, int KIND, bool ROWS>
 static int launch_n(int N, const FastArgs<T>& a, hipStream_t s) {
-#define NFT_CASE(n)                                                                   \
-  case n:                                                                             \
-    return launch_one<T, n, (ROWS ? nt_rows(n) : nt_strided(n)), KIND, ROWS>(a, s);
+#define NFT_CASE(n)                                                                \
+  case n:                                                                          \
+    if constexpr (ROWS)                                                            \
+      return launch_one<T, n, nt_rows(n), KIND, ROWS>(a, s);                       \
+    else                                                                           \
+      return launch_one<T, n, nt_strided_launch<T>(n), KIND, ROWS, vp_strided<T>(n)>(a, s);
   if (ROWS) {
     switch (N) {
       NFT_CASE(8) NFT_CASE(16) NFT_CASE(32) NFT_CASE(64) NFT_CASE(128) NFT_CASE(256) NFT_CASE(512)

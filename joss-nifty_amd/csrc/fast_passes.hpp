@@ -214,9 +214,9 @@ __device__ __forceinline__ long long batch_tile_contig(long long w, long long nt
 // (more resident waves) wins.
 // (the persistent variant for N = 4096 with 512 threads measured slower:
 // fp32 4096^2 R2C 141 -> 190 us per 4-RHS launch)
-template <int N, int NT, int KIND>
+template <int N, int NT, int KIND, int VP = VPT>
 constexpr bool persist_ok() {
-  return N <= 2048 && NT <= 256 && KIND == K_R2C;
+  return N <= 2048 && NT * VP <= 256 * VPT && KIND == K_R2C;
 }
 
 // in-line LDS padding of a pass (fft_fast.hpp padx): every 8 elements for
@@ -239,23 +239,26 @@ constexpr int pass_pitch() {
 
 // dynamic LDS of a pass: L lines (+ the unpack line table), then the
 // quarter twiddle table (N/4 entries) at a 16-byte aligned offset
-template <typename T, int N, int NT, int KIND, bool ROWS>
+template <typename T, int N, int NT, int KIND, bool ROWS, int VP = VPT>
 constexpr size_t tw_lds_offset() {
-  constexpr int L = NT * VPT / N;
+  constexpr int L = NT * VP / N;
   constexpr int PITCH = pass_pitch<N, ROWS>();
   return ((size_t)L * PITCH * sizeof(cplx_t<T>) + (KIND == K_UNPACK ? (size_t)L * sizeof(UnpackLine) : 0) + 15) &
          ~(size_t)15;
 }
-template <typename T, int N, int NT, int KIND, bool ROWS>
+template <typename T, int N, int NT, int KIND, bool ROWS, int VP = VPT>
 constexpr size_t pass_lds_bytes() {
-  return tw_lds_offset<T, N, NT, KIND, ROWS>() + (size_t)(N / 4) * sizeof(cplx_t<T>);
+  return tw_lds_offset<T, N, NT, KIND, ROWS, VP>() + (size_t)(N / 4) * sizeof(cplx_t<T>);
 }
 
 // EM (unpack passes): epilogue mode -- 0 plain, 1 the CG-carrying epilogue
 // (a.f.cg), 2 the plain epilogue plus the per-tile quadratic-form partials
 // (a.f.quad).  Each compiled alone: the plain unpack instance carries none of
 // their registers (occupancy)
-template <typename T, int N, int NT, int KIND, bool ROWS, bool PF, int EM = 0>
+// VP: values per thread in the load / store phases (L = NT * VP / N lines per
+// tile): the strided passes run VP = 4 at twice the threads of VPT = 8 -- the
+// same tile and LDS, twice the resident waves
+template <typename T, int N, int NT, int KIND, bool ROWS, bool PF, int EM = 0, int VP = VPT>
 __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   // Persistent: workgroup b processes tiles b, b + G, b + 2G, ...  The input
   // of tile t + G is loaded into registers while tile t is transformed and
@@ -264,14 +267,14 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   // is one latency-bound wave of load, compute, store).  The prologue variant
   // (gathers feeding arithmetic) loads at the top of the loop instead.
   using C = cplx_t<T>;
-  constexpr int L = NT * VPT / N;
-  static_assert(L >= 1, "NT*VPT must cover one line");
+  constexpr int L = NT * VP / N;
+  static_assert(L >= 1, "NT*VP must cover one line");
   constexpr int PITCH = pass_pitch<N, ROWS>();
   constexpr int PS = pass_pad<N, ROWS>();
   constexpr int SHN = ilog2(N), SHL = ilog2(L);
   extern __shared__ __align__(16) unsigned char smem[];
   C* lds = (C*)smem;
-  C* twq = (C*)(smem + tw_lds_offset<T, N, NT, KIND, ROWS>());
+  C* twq = (C*)(smem + tw_lds_offset<T, N, NT, KIND, ROWS, VP>());
   for (int r = threadIdx.x; r < N / 4; r += NT) twq[r] = ((const C*)a.tw)[r];  // synced before the first stage
   const int tid = threadIdx.x;
   const Lines& g = a.g;
@@ -306,11 +309,11 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
     }
   };
   // global -> registers (input values of tile t in load order)
-  auto load = [&](long long t, C (&rv)[VPT]) {
+  auto load = [&](long long t, C (&rv)[VP]) {
     long long o, m, i0;
     tile_of(t, o, m, i0);
 #pragma unroll
-    for (int r = 0; r < VPT; ++r) {
+    for (int r = 0; r < VP; ++r) {
       int l, x;
       lx_of(r, l, x);
       C v = C{(T)0, (T)0};
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
 
   constexpr bool PERSIST = PF;
   constexpr bool prefetch = PF;  // launched persistent only without a prologue
-  C rv[VPT];
+  C rv[VP];
   long long t = blockIdx.x;
   if constexpr (!PERSIST) {
     if (a.bgroup > 1) t = a.bmode == 2 ? batch_tile_contig(t, ntiles, a.bgroup) : batch_tile(t, ntiles, a.bgroup);
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   while (t < ntiles) {
     if (!prefetch) load(t, rv);
 #pragma unroll
-    for (int r = 0; r < VPT; ++r) {
+    for (int r = 0; r < VP; ++r) {
       int l, x;
       lx_of(r, l, x);
       lds[l * PITCH + padx<PS>(x)] = rv[r];
@@ -376,7 +379,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       C* out = (C*)a.out;
       const C* tw2 = (const C*)a.tw2;
 #pragma unroll
-      for (int r = 0; r < VPT; ++r) {
+      for (int r = 0; r < VP; ++r) {
         int l, x;
         lx_of(r, l, x);
         C v = lds[l * PITCH + padx<PS>(x)];
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         T* out = (T*)a.out;
         const T hs = (T)0.5 * a.scale, sg = (T)a.sigma;
 #pragma unroll
-        for (int r = 0; r < VPT; ++r) {
+        for (int r = 0; r < VP; ++r) {
           const int e = tid + r * NT;
           const int l = e >> SHN;
           const int k = e & (N - 1);
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       const int Nf = a.Nfull;
       if constexpr (EM == 0) {
 #pragma unroll
-        for (int r = 0; r < VPT; ++r) {
+        for (int r = 0; r < VP; ++r) {
           int l, x;
           lx_of(r, l, x);
           const UnpackLine u = lines[l];
@@ -488,7 +491,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         const long long item = o;
         const T* __restrict__ ea = (const T*)a.f.ea;
         double qs = 0.0;
-        constexpr int QCH = QUAD_CH_VALUES;
+        constexpr int QCH = QUAD_CH_VALUES < VP ? QUAD_CH_VALUES : VP;
         auto elem = [&](int r, int h, bool& use, T& hv, long long& b, long long& j) {
           int l, x;
           lx_of(r, l, x);
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
           fuse_split(a.f, idx, b, j);
         };
 #pragma unroll
-        for (int r0 = 0; r0 < VPT; r0 += QCH) {
+        for (int r0 = 0; r0 < VP; r0 += QCH) {
           T wv[QCH][2];
 #pragma unroll
           for (int c = 0; c < QCH; ++c) {
@@ -561,7 +564,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         T* __restrict__ cx = (T*)a.f.cx;
         T* __restrict__ cr = (T*)a.f.cr;
 #pragma unroll
-        for (int r0 = 0; r0 < VPT; r0 += CG_CH) {
+        for (int r0 = 0; r0 < VP; r0 += CG_CH) {
           long long ev[CG_CH][2], jv[CG_CH][2], bv[CG_CH][2];
           bool use[CG_CH][2];
           T hv[CG_CH][2], xv[CG_CH][2], rv_[CG_CH][2], dv[CG_CH][2], qv[CG_CH][2], wv[CG_CH][2];
