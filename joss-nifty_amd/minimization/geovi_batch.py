@@ -289,9 +289,11 @@ def _pixel_rows(d, k, a, b):
     return d.reshape(1, -1) if d.shape[0] == 1 else d.reshape(k, -1)[a:b]
 
 
-def _los_fwd(R, V, d=None):
-    """R (d * V) row by row; d (the derivative of a pointwise stage in front
-    of R) is applied as the kernel loads the pixels (nft_los_forward_ex)."""
+def _los_fwd(R, V, d=None, scale=1.0):
+    """scale * R (d * V) row by row; d (the derivative of a pointwise stage in
+    front of R) is applied as the kernel loads the pixels, the scalar of a
+    scaling stage behind R as it stores each line (nft_los_forward_ex: the
+    same product as the separate multiply)."""
     from ..library.los_response import LOS_KMAX
     plan = R._box_plan()
     k = V.shape[0]
@@ -300,15 +302,16 @@ def _los_fwd(R, V, d=None):
     for a in range(0, k, LOS_KMAX):
         b = min(k, a + LOS_KMAX)
         if d is None:
-            _native.los_forward_batched(plan, V[a:b], y[a:b])
+            _native.los_forward_batched(plan, V[a:b], y[a:b], scale=scale)
         else:
-            _native.los_forward_ex(plan, V[a:b], y[a:b], colscale=_pixel_rows(d, k, a, b))
+            _native.los_forward_ex(plan, V[a:b], y[a:b], colscale=_pixel_rows(d, k, a, b), scale=scale)
     return y
 
 
-def _los_adj(R, Y, d=None):
-    """d * R^T Y row by row (d applied as the pixels are stored,
-    nft_los_adjoint_ex)."""
+def _los_adj(R, Y, d=None, ys=None):
+    """d * R^T (ys * Y) row by row (d applied as the pixels are stored,
+    nft_los_adjoint_ex; ys, a per-line vector, as the line values are read --
+    the same product as the separate multiply)."""
     from ..library.los_response import LOS_KMAX
     plan = R._box_plan()
     k = Y.shape[0]
@@ -317,10 +320,10 @@ def _los_adj(R, Y, d=None):
     out = torch.empty((k, npix), dtype=Y.dtype, device=Y.device)
     for a in range(0, k, LOS_KMAX):
         b = min(k, a + LOS_KMAX)
-        if d is None:
+        if d is None and ys is None:
             _native.los_adjoint_batched(plan, Y[a:b], out[a:b])
         else:
-            _native.los_adjoint_ex(plan, Y[a:b], out[a:b], rowscale=_pixel_rows(d, k, a, b))
+            _native.los_adjoint_ex(plan, Y[a:b], out[a:b], colscale=ys, rowscale=_pixel_rows(d, k, a, b))
     return out
 
 
@@ -385,14 +388,23 @@ class Pipeline:
             return False
         return d.dtype == U.dtype and d.is_contiguous() and d.shape[0] in (1, U.shape[0])
 
+    def _scalar_after(self, j):
+        """the factor of a scalar scaling stage at index j (it rides in the LOS
+        kernel next to it), else None"""
+        if j < len(self.stages) and isinstance(self.stages[j], _LinStage) and self.stages[j].kind == "scale" \
+                and _FUSE_PTW:
+            return float(self.stages[j].v)
+        return None
+
     def jvp(self, states, V):
         U = self.stages[0].jvp(states[0], V)
         i = 1
         while i < len(self.stages):
             s, st = self.stages[i], states[i]
             if self._fused_ptw_los(i, st, U):
-                U = _los_fwd(self.stages[i + 1].v, U.reshape(U.shape[0], -1), st)
-                i += 2
+                f = self._scalar_after(i + 2)
+                U = _los_fwd(self.stages[i + 1].v, U.reshape(U.shape[0], -1), st, 1.0 if f is None else f)
+                i += 2 if f is None else 3
                 continue
             U = s.jvp(st, U)
             i += 1
@@ -405,6 +417,20 @@ class Pipeline:
         i = len(self.stages) - 1
         while i >= 1:
             s, st = self.stages[i], states[i]
+            f = self._scalar_after(i)
+            if f is not None and i >= 3 and isinstance(self.stages[i - 1], _LinStage) and \
+                    self.stages[i - 1].kind == "los" and self._fused_ptw_los(i - 2, states[i - 2], U):
+                # scale stage, LOS, pointwise stage: one adjoint launch with the
+                # scale as a per-line factor of the line values
+                R = self.stages[i - 1].v
+                ys = self.__dict__.setdefault("_lsc", {}).get((i, str(U.device)))
+                if ys is None:
+                    ys = torch.full((R.target.shape[0],), f, dtype=torch.float64, device=U.device)
+                    self._lsc[(i, str(U.device))] = ys
+                U = _los_adj(R, U.reshape(U.shape[0], -1), states[i - 2], ys=ys.to(U.dtype)).reshape(
+                    (U.shape[0],) + self.stages[i - 1].dshape)
+                i -= 3
+                continue
             if i >= 2 and self._fused_ptw_los(i - 1, states[i - 1], U):
                 U = _los_adj(s.v, U.reshape(U.shape[0], -1), states[i - 1]).reshape((U.shape[0],) + s.dshape)
                 i -= 2
@@ -485,9 +511,24 @@ class GeoVIBatch:
                 Q[:, a:b] = 0.0
         return Q
 
-    def _J0T(self, F, plus=None):
+    def _scratch(self, k, device):
+        """a _latent buffer kept for intermediates that die inside one call
+        (the metric's u, evaluate's residual): its padding is zeroed once, not
+        by several fill launches per call.  Not created during a graph
+        capture (the capture takes a fresh buffer from its own pool)."""
+        cache = self.__dict__.setdefault("_scr", {})
+        key = (k, str(device))
+        Q = cache.get(key)
+        if Q is None:
+            Q = self._latent(k, device)
+            if not torch.cuda.is_current_stream_capturing():
+                cache[key] = Q
+        return Q
+
+    def _J0T(self, F, plus=None, out=None):
         """J0^T F (+ plus, added inside the adjoint: bitwise the separate add)"""
-        return self.pipe.vjp(self.st0, F, self._latent(F.shape[0], F.device), plus, 1.0)
+        Q = self._latent(F.shape[0], F.device) if out is None else out
+        return self.pipe.vjp(self.st0, F, Q, plus, 1.0)
 
     def _JT(self, states, G, plus=None):
         return self.pipe.vjp(states, G, self._latent(G.shape[0], G.device), plus, 1.0)
@@ -495,7 +536,7 @@ class GeoVIBatch:
     def evaluate(self, X, M):
         """values, |gradient|, gradients and per-sample states at the rows of X"""
         F, states = self.pipe.fwd(X)
-        Rr = self._J0T(F)
+        Rr = self._J0T(F, out=self._scratch(X.shape[0], X.device))
         Rr.add_(X).sub_(M)
         G = self._JT(states, self._J0(Rr), plus=Rr)
         k = X.shape[0]
@@ -507,7 +548,7 @@ class GeoVIBatch:
     def metric_batch(self, states):
         """callable (D, Q) -> Q = M_b D for the stacked per-sample states"""
         def mv(D, Q):
-            U = self._J0T(self.pipe.jvp(states, D), plus=D)
+            U = self._J0T(self.pipe.jvp(states, D), plus=D, out=self._scratch(D.shape[0], D.device))
             self.pipe.vjp(states, self._J0(U), Q, U, 1.0)   # overwrites every key segment
             return Q
         return mv
