@@ -120,9 +120,6 @@ class _CFStage:
         self.axes = tuple(range(1, 1 + len(self.grid)))
         self.xo = self.off[model.k_xi]
 
-    def _xi(self, X):
-        return X[:, self.xo:self.xo + self.N].reshape((X.shape[0],) + self.grid)
-
     def fwd(self, X):
         m = self.m
         k = X.shape[0]
@@ -135,10 +132,13 @@ class _CFStage:
         afull = torch.empty((k,) + self.grid, dtype=A.dtype, device=A.device)
         b = m.bins
         _native.bin_gather(A, b.pindex, afull, k, b.npix, b.nbin, 1)
-        u = afull * self._xi(X)
-        s = torch.empty_like(u)
+        # A * xi inside the transform's first pass (the prologue's product is
+        # the separate multiply's: bitwise), not a (k, N) pass of its own
+        s = torch.empty_like(afull)
         from ..ducc_dispatch import hartley_convention_code
-        _native.hartley_fused(s, self.axes, m.c_h, x=u, convention=hartley_convention_code(), shape=s.shape)
+        _native.hartley_fused(s, self.axes, m.c_h, pro=dict(a=afull, x=X[0, self.xo:]),
+                              convention=hartley_convention_code(), shape=s.shape,
+                              batch=dict(period=self.N, x=X.shape[1], a=self.N))
         if m.offset_mean is not None:
             s = s + m.offset_mean
         return s, dict(afull=afull, X=X, lin=lin, lins=[lin], dconst=lin.dconst, k=k)
