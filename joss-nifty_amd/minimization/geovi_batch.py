@@ -140,7 +140,7 @@ class _CFStage:
                               convention=hartley_convention_code(), shape=s.shape,
                               batch=dict(period=self.N, x=X.shape[1], a=self.N))
         if m.offset_mean is not None:
-            s = s + m.offset_mean
+            s.add_(m.offset_mean)
         return s, dict(afull=afull, X=X, lin=lin, lins=[lin], dconst=lin.dconst, k=k)
 
     @staticmethod
@@ -536,8 +536,9 @@ class GeoVIBatch:
     def evaluate(self, X, M):
         """values, |gradient|, gradients and per-sample states at the rows of X"""
         F, states = self.pipe.fwd(X)
-        Rr = self._J0T(F, out=self._scratch(X.shape[0], X.device))
-        Rr.add_(X).sub_(M)
+        # + X inside the adjoint (bitwise the separate add, _J0T)
+        Rr = self._J0T(F, plus=X, out=self._scratch(X.shape[0], X.device))
+        Rr.sub_(M)
         G = self._JT(states, self._J0(Rr), plus=Rr)
         k = X.shape[0]
         h = _rowdots([(Rr, Rr), (G, G)])
