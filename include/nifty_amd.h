@@ -112,6 +112,10 @@ size_t nft_reduce_workspace(int64_t n);
 int nft_dot(const void* a, const void* b, int64_t n, int dtype, double* out, void* ws,
             hipStream_t stream);
 int nft_scale(void* x, int64_t n, int dtype, double scale, hipStream_t stream);
+/* v = 0.5 + 0.5 tanh(x), d = 0.5 (1 - tanh(x)^2) for n values (dtype 0
+ * fp64, 1 fp32): the value and derivative of the `sigmoid` pointwise map
+ * (src/pointwise.py) in one pass, bitwise the separate elementwise passes. */
+int nft_sigmoid_pair(const void* x, void* v, void* d, int64_t n, int dtype, hipStream_t stream);
 /* For the metric shift*1 + M' with q = M' d formed without the shift:
  * sc[CURV] = sum d*(q + shift*d) */
 int nft_cg_curv(const void* d, const void* q, int64_t n, int dtype, double shift, double* sc,

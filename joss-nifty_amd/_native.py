@@ -27,6 +27,7 @@ SIGNATURES = {
     "nft_reduce_workspace": (_sz, [_i64]),
     "nft_dot": (_i, [_p, _p, _i64, _i, _p, _p, _p]),
     "nft_scale": (_i, [_p, _i64, _i, _d, _p]),
+    "nft_sigmoid_pair": (_i, [_p, _p, _p, _i64, _i, _p]),
     "nft_cg_curv": (_i, [_p, _p, _i64, _i, _d, _p, _p, _p]),
     "nft_dot_batched": (_i, [_p, _p, _i64, _i64, _i, _i, _p, _i64, _p, _p]),
     "nft_cg_curv_batched": (_i, [_p, _p, _i64, _i64, _i, _i, _d, _p, _p, _p]),
@@ -278,6 +279,18 @@ def dot(a, b, out=None):
     ws = workspace(lib.nft_reduce_workspace(n), a.device, "reduce")
     _check(lib.nft_dot(ptr(a), ptr(b), n, dtype_code(a.dtype), ptr(out), ptr(ws), stream_ptr()))
     return out
+
+
+def sigmoid_pair(x, v, d):
+    """v = 0.5 + 0.5 tanh(x), d = 0.5 (1 - tanh(x)^2) in one pass
+    (nft_sigmoid_pair: bitwise the torch elementwise passes of
+    pointwise._sigmoid); contiguous device tensors of one dtype."""
+    require_device(x, v, d)
+    if not (x.is_contiguous() and v.is_contiguous() and d.is_contiguous()
+            and x.dtype == v.dtype == d.dtype and x.numel() == v.numel() == d.numel()):
+        raise NativeError("sigmoid_pair: contiguous x, v, d of one dtype and size required")
+    _check(load().nft_sigmoid_pair(ptr(x), ptr(v), ptr(d), x.numel(), dtype_code(x.dtype), stream_ptr()))
+    return v, d
 
 
 def bin_gather(src, pindex, out, pre, npix, nbins, post):

@@ -121,6 +121,22 @@ __global__ __launch_bounds__(RED_NT) void fold_partials(const double* __restrict
 int scale_real_impl(void* x, long long n, int dtype, double scale, hipStream_t s);
 
 // ------------------------------------------------------------------ scale
+// Value and derivative of NIFTy's sigmoid (src/pointwise.py: 0.5 + 0.5
+// tanh(x) and 0.5 (1 - tanh(x)^2), pointwise.py:31-33 here) in one pass over
+// x, every operation rounded as the separate elementwise passes round it (no
+// contraction; the same tanh): bitwise those passes
+template <typename T>
+__global__ void sigmoid_pair_kernel(const T* __restrict__ x, T* __restrict__ v, T* __restrict__ d, long long n) {
+#pragma clang fp contract(off)
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const T t = tanh(x[i]);
+    const T h = (T)0.5 * t;
+    v[i] = (T)0.5 + h;
+    const T q = t * t;
+    d[i] = (T)0.5 * ((T)1 - q);
+  }
+}
+
 template <typename T>
 __global__ void scale_kernel(T* __restrict__ x, long long n, T s) {
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -488,6 +504,27 @@ int nft_dot(const void* a, const void* b, int64_t n, int dtype, double* out, voi
 
 int nft_scale(void* x, int64_t n, int dtype, double scale, hipStream_t stream) {
   return scale_real(x, n, dtype, scale, stream);
+}
+
+int nft_sigmoid_pair(const void* x, void* v, void* d, int64_t n, int dtype, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!x || !v || !d))) {
+    set_last_error("nft_sigmoid_pair: bad arguments");
+    return NFT_ERR_ARG;
+  }
+  if (n == 0) return NFT_OK;
+  const unsigned nb = (unsigned)std::min<long long>((n + 255) / 256, 65536);
+  if (dtype == 0)
+    hipLaunchKernelGGL(sigmoid_pair_kernel<double>, dim3(nb), dim3(256), 0, stream, (const double*)x, (double*)v,
+                       (double*)d, (long long)n);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(sigmoid_pair_kernel<float>, dim3(nb), dim3(256), 0, stream, (const float*)x, (float*)v,
+                       (float*)d, (long long)n);
+  else {
+    set_last_error("nft_sigmoid_pair: bad dtype %d", dtype);
+    return NFT_ERR_ARG;
+  }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
 }
 
 int nft_cg_curv_batched(const void* d, const void* q, int64_t n, int64_t vstride, int nrhs, int dtype, double shift,

@@ -227,10 +227,16 @@ _FUSE_PTW = os.environ.get("NFT_FUSE_PTW", "1") != "0"
 class _PtwStage:
     def __init__(self, name, args, kwargs):
         from ..pointwise import ptw_dict
+        self.name = name
         self.f = ptw_dict[name][1]
         self.args, self.kwargs = args, kwargs
 
     def fwd(self, U):
+        if self.name == "sigmoid" and not self.args and not self.kwargs and U.is_cuda and \
+                U.dtype in (torch.float64, torch.float32):
+            # value and derivative in one native pass (bitwise pointwise._sigmoid)
+            U = U.contiguous()
+            return _native.sigmoid_pair(U, torch.empty_like(U), torch.empty_like(U))
         v, d = self.f(U, *self.args, **self.kwargs)
         return v, d
 

@@ -145,3 +145,23 @@ def test_batched_kl_matches_per_sample(ift, kind):
     for k in cf.domain.keys():
         ga, gb = a.gradient[k].val.cpu().numpy(), b.gradient[k].val.cpu().numpy()
         assert np.linalg.norm(ga - gb) <= 1e-11 * max(np.linalg.norm(gb), 1e-300), k
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_sigmoid_pair_bitwise(ift, dtype):
+    """nft_sigmoid_pair (the batched geoVI pipeline's sigmoid stage) is
+    bitwise the torch elementwise passes of pointwise._sigmoid, special
+    values included."""
+    import torch
+    from nifty_amd import _native
+    from nifty_amd.pointwise import _sigmoid
+    dt = getattr(torch, dtype)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    x = torch.cat([torch.randn(100003, dtype=torch.float64, device="cuda", generator=g) * 4,
+                   torch.tensor([0.0, -0.0, 1e-300, -1e-300, 20.0, -20.0, 400.0, -400.0, float("inf"),
+                                 float("-inf")], dtype=torch.float64, device="cuda")]).to(dt)
+    v0, d0 = _sigmoid(x)
+    v1, d1 = _native.sigmoid_pair(x, torch.empty_like(x), torch.empty_like(x))
+    assert torch.equal(v0, v1) and torch.equal(d0, d1)
+    assert torch.equal(torch.signbit(v0), torch.signbit(v1)) and torch.equal(torch.signbit(d0), torch.signbit(d1))
