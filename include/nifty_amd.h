@@ -546,9 +546,12 @@ int nft_amp_vjp_batched(const nft_amp_const* c, const nft_amp_const* item_consts
  * and the outputs); the batched forms above take this path when it applies.
  * These kernels keep device-global arrival counters, so calls must not
  * overlap: a call on another stream than the previous (eager) call first
- * waits on the host for that stream's work (calls on a stream under HIP-graph
- * capture are not tracked -- graphs holding them must not be replayed
- * concurrently with each other or with eager calls on other streams).  Key arrays are indexed fl, sl, flex, asp, zm, spec (NULL:
+ * waits on the host for that stream's work, under a library mutex held from
+ * that check through the call's launches, so eager calls from any number of
+ * streams and host threads run one after the other.  Calls on a stream under
+ * HIP-graph capture are not tracked: graphs holding them must not be replayed
+ * concurrently with each other or with eager calls on other streams (the
+ * caller's rule; the library cannot see a replay).  Key arrays are indexed fl, sl, flex, asp, zm, spec (NULL:
  * absent key), pointing at right-hand side 0, rows lat_stride elements apart.
  * item_mode: 0 = every RHS uses *c; 1 = item_consts is a DEVICE array of nrhs
  * constant sets (one per RHS); 2 = item_consts is ONE device constant set

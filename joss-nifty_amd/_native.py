@@ -84,6 +84,10 @@ SIGNATURES = {
     "nft_amp2_tiles": (_i, [_i64, _i, _i]),
     "nft_amp2_tab_size": (_i64, [_i64]),
     "nft_amp2_prepare": (_i, [_p, _p, _i, _p, _p]),
+    # two-phase amplitude kernels: one device-global counter set, so eager
+    # calls from several streams / threads are serialised by the library, but
+    # HIP graphs holding these kernels must never be replayed concurrently
+    # with each other or with eager calls on another stream (nifty_amd.h)
     "nft_amp2_jvp": (_i, [_p, _p, _i, _p, _p, _i64, _p, _i64, _i64, _p, _i, _p, _p, _i64, _d, _i, _p, _p]),
     "nft_amp2_vjp": (_i, [_p, _p, _i, _p, _i64, _p, _p, _p, _i64, _d, _p, _i, _p, _p, _i64, _p, _i64, _i64, _i, _i,
                           _p, _p]),

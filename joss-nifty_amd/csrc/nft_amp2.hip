@@ -37,6 +37,7 @@
 // share the launch.
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 #include "nft_api_internal.hpp"
 #include "../../include/nifty_amd.h"
@@ -1275,22 +1276,34 @@ static int nblk(long long n, long long per) { return (int)std::max<long long>(1,
 // Cross-stream ordering of the calls (the device-global arrival counters and
 // the shared workspace make two concurrently running calls corrupt each
 // other): a call on a different stream than the previous eager call first
-// waits on the host for that stream's work (hipStreamSynchronize), so calls
-// from any number of streams execute one after the other, and single-stream
-// use -- every call on the hot path -- pays nothing on the device (an event
-// recorded after every call measured +5 us per launch pair).  A call on a
-// stream under HIP-graph capture is not tracked: a captured graph is ordered
-// by its replay stream, so graphs holding these kernels must not be replayed
-// concurrently with each other or with eager calls on another stream.
+// waits on the host for that stream's work (hipStreamSynchronize), so eager
+// calls from any number of streams and host threads execute one after the
+// other, and single-stream use -- every call on the hot path -- pays nothing
+// on the device (an event recorded after every call measured +5 us per launch
+// pair).  g_guard_mu is held from the check through the launches of a call
+// (AmpGuard), so two host threads cannot both skip the wait (ctypes releases
+// the GIL around these calls).  The previous stream may have been destroyed
+// since: a failing stream wait falls back to a device-wide synchronisation.
+// A call on a stream under HIP-graph capture is not tracked: a captured graph
+// is ordered by its replay stream, so graphs holding these kernels must not
+// be replayed concurrently with each other or with eager calls on another
+// stream (nifty_amd.h, nft_amp2_jvp).
+static std::mutex g_guard_mu;
 static hipStream_t g_last_stream = nullptr;
 static bool g_any_call = false;
 static bool capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
+// caller holds g_guard_mu
 static int guard_enter(hipStream_t s) {
   if (capturing(s)) return NFT_OK;
-  if (g_any_call && s != g_last_stream) NFT_HIP_CHECK(hipStreamSynchronize(g_last_stream));
+  if (g_any_call && s != g_last_stream) {
+    if (hipStreamSynchronize(g_last_stream) != hipSuccess) {
+      (void)hipGetLastError();
+      NFT_HIP_CHECK(hipDeviceSynchronize());
+    }
+  }
   g_last_stream = s;
   g_any_call = true;
   return NFT_OK;
@@ -1392,6 +1405,7 @@ int amp2_jvp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, i
   a.tab = tab;
   const bool tb = tab != nullptr;
   const dim3 grid(grid_of(nb, nrhs));
+  std::lock_guard<std::mutex> lk(g_guard_mu);
   if (int st = guard_enter(stream)) return st;
   prof_mark(stream, a.dir ? "amp_jvp2a+dir" : "amp_jvp2a");
   NFT_AMP2_LAUNCH(jvp2a_kernel, VT, item_mode, tb, grid, stream, a);
@@ -1434,6 +1448,7 @@ int amp2_vjp_impl(const nft_amp_const* cst_, const nft_amp_const* item_consts, i
   a.tab = tab;
   const bool tb = tab != nullptr;
   const dim3 grid(grid_of(nb, nrhs));
+  std::lock_guard<std::mutex> lk(g_guard_mu);
   if (int st = guard_enter(stream)) return st;
   prof_mark(stream, a.cg ? "amp_vjp2a+cg" : "amp_vjp2a");
   NFT_AMP2_LAUNCH(vjp2a_kernel, VT, item_mode, tb, grid, stream, a);

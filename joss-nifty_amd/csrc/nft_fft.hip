@@ -1132,6 +1132,11 @@ static void launch_pro_fold(const fast::FuseArgs& f, T* u, long long ncell, hipS
     launch_pro_fold_pi<T, D, false>(f, u, ncell, s);
 }
 
+// the fused prologue + R2C pass of nft_pro_r2c.hip (done: it ran and wrote
+// the half spectra to ws)
+int pro_r2c_try(const fast::FuseArgs& f, int dtype, int nd, const long long* shape, int naxes, const int* ax,
+                void* ws, size_t hws, hipStream_t s, bool* done);
+
 template <typename T>
 static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out, const Geo& g,
                               const std::vector<int>& ax, int sigma, double scale, void* ws, size_t ws_bytes,
@@ -1168,6 +1173,19 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
     T* u = (T*)((char*)ws + align256(hws));
     // one element per thread (no grid-stride chain of dependent gathers)
     const unsigned nblk = (unsigned)((f.P + 255) / 256);
+    {
+      bool done = false;
+      int pst = pro_r2c_try(f, sizeof(T) == 8 ? 0 : 1, g.nd, g.shape, (int)ax.size(), ax.data(), ws, hws, s, &done);
+      if (pst != NFT_OK) return pst;
+      if (done) {
+        fast::FuseArgs f2 = f;
+        f2.pro = 0;
+        f2.px = f2.pa = f2.pb = f2.pc = nullptr;
+        f2.pidx = nullptr;
+        f2.dr = nullptr;
+        return hartley_v2<T>(nullptr, out, g, ax, sigma, scale, ws, hws, s, &f2, true);
+      }
+    }
     if (f.fnd > 0 && f.pb) {
       long long ncell = 1;  // padded cell grid (pro_fold_kernel)
       for (int a = 0; a < f.fnd; ++a) ncell *= a == f.fnd - 1 ? ((f.fn[a] / 2 + 1 + 63) & ~63LL) : f.fn[a] / 2 + 1;

@@ -305,7 +305,19 @@ def fused_cg_batch_or_none(energies, controllers, nreset):
         return None
     if any(e.position.domain != core.domain for e in energies):
         return None
-    return FusedCGBatch(core, W, shift, controllers, nreset).run(energies)
+    # at most MAX_BATCH right-hand sides per loop: the direction carried by
+    # the folded prologue (and with it the rounding of the curvature) exists
+    # for <= 8 items, so a rank holding 32 samples solves them in batches of
+    # 8 with the per-RHS arithmetic of a rank holding 4 -- bit-identical KL
+    # values on any rank count (test_mpi/test_kl.py:46-114,
+    # tests/test_dist_ranks_gpu.py)
+    out = []
+    for i in range(0, len(energies), MAX_BATCH):
+        out += FusedCGBatch(core, W, shift, controllers[i:i + MAX_BATCH], nreset).run(energies[i:i + MAX_BATCH])
+    return out
+
+
+MAX_BATCH = 8
 
 
 # The grid segment's CG update carried by the adjoint transform's epilogue

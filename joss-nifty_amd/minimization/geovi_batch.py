@@ -394,11 +394,13 @@ class Pipeline:
             return False
         return d.dtype == U.dtype and d.is_contiguous() and d.shape[0] in (1, U.shape[0])
 
-    def _scalar_after(self, j):
+    def _scalar_after(self, j, dtype):
         """the factor of a scalar scaling stage at index j (it rides in the LOS
-        kernel next to it), else None"""
-        if j < len(self.stages) and isinstance(self.stages[j], _LinStage) and self.stages[j].kind == "scale" \
-                and _FUSE_PTW:
+        kernel next to it), else None.  fp64 only: the kernels apply the factor
+        in double, which is the separate multiply's rounding only when the
+        vectors are double (fp32 vectors round after every multiply)"""
+        if dtype == torch.float64 and j < len(self.stages) and isinstance(self.stages[j], _LinStage) \
+                and self.stages[j].kind == "scale" and _FUSE_PTW:
             return float(self.stages[j].v)
         return None
 
@@ -408,7 +410,7 @@ class Pipeline:
         while i < len(self.stages):
             s, st = self.stages[i], states[i]
             if self._fused_ptw_los(i, st, U):
-                f = self._scalar_after(i + 2)
+                f = self._scalar_after(i + 2, U.dtype)
                 U = _los_fwd(self.stages[i + 1].v, U.reshape(U.shape[0], -1), st, 1.0 if f is None else f)
                 i += 2 if f is None else 3
                 continue
@@ -423,7 +425,7 @@ class Pipeline:
         i = len(self.stages) - 1
         while i >= 1:
             s, st = self.stages[i], states[i]
-            f = self._scalar_after(i)
+            f = self._scalar_after(i, U.dtype)
             if f is not None and i >= 3 and isinstance(self.stages[i - 1], _LinStage) and \
                     self.stages[i - 1].kind == "los" and self._fused_ptw_los(i - 2, states[i - 2], U):
                 # scale stage, LOS, pointwise stage: one adjoint launch with the
@@ -521,15 +523,22 @@ class GeoVIBatch:
         """a _latent buffer kept for intermediates that die inside one call
         (the metric's u, evaluate's residual): its padding is zeroed once, not
         by several fill launches per call.  Not created during a graph
-        capture (the capture takes a fresh buffer from its own pool)."""
+        capture (the capture takes a fresh buffer from its own pool).
+        One buffer per device, as many rows as the largest batch asked for;
+        a batch of k rows gets its first k rows (the batches only shrink as
+        samples finish: one buffer instead of one per batch size).  A buffer
+        outgrown by a larger batch is retired, not freed: a captured graph may
+        still write into it."""
         cache = self.__dict__.setdefault("_scr", {})
-        key = (k, str(device))
+        key = str(device)
         Q = cache.get(key)
-        if Q is None:
-            Q = self._latent(k, device)
-            if not torch.cuda.is_current_stream_capturing():
-                cache[key] = Q
-        return Q
+        if Q is None or Q.shape[0] < k:
+            if torch.cuda.is_current_stream_capturing():
+                return self._latent(k, device)
+            if Q is not None:
+                self.__dict__.setdefault("_scr_retired", []).append(Q)
+            Q = cache[key] = self._latent(k, device)
+        return Q[:k]
 
     def _J0T(self, F, plus=None, out=None):
         """J0^T F (+ plus, added inside the adjoint: bitwise the separate add)"""

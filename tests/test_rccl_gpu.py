@@ -14,8 +14,6 @@ the same code takes its device-tensor branches (`TorchComm._staged` is false,
 * draw_samples + SampledKLEnergyClass (MGVI and geoVI, mirrored pairs) and the
   KL metric through TorchComm(nccl) -- bitwise the comm=None run.
 """
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -32,15 +30,24 @@ def nccl_comm(dev):
     import nifty_amd as ift
     if dist.is_initialized():
         pytest.skip("a process group is already initialised in this process")
-    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # HSA_ENABLE_IPC_MODE_LEGACY=0 must be in the environment before the GPU
+    # initialises (it is exported on the box and in the image); a world-size-1
+    # group exchanges no IPC handles either way
+    prev = ift.config.device() if callable(getattr(ift.config, "device", None)) else None
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
     ift.config.set_device("cuda:0")
     comm = ift.TorchComm()
     assert comm.backend == "nccl" and comm.Get_size() == 1
-    yield comm
-    dist.barrier()
-    dist.destroy_process_group()
+    try:
+        yield comm
+    finally:
+        try:
+            dist.barrier()
+        finally:
+            dist.destroy_process_group()
+            if prev is not None:
+                ift.config.set_device(prev)
 
 
 def _payloads(seed):

@@ -18,6 +18,7 @@ def label(name, seen):
     n = name
     rules = [(r"cg_dir_dd_kernel", "cg_dir_dd2"), (r"jvp2a_kernel", "amp_jvp2a+dir"), (r"jvp2b_kernel", "amp_jvp2b"),
              (r"vjp2a_kernel", "amp_vjp2a+cg"), (r"vjp2b_kernel", "amp_vjp2b+cg"), (r"pro_fold_kernel|pro_rows_kernel", "pro_fold+dir"),
+             (r"pro_r2c_kernel", "pro_r2c+dir"),
              (r"fast_kernel<double, \d+, \d+, 1, true", "fft_r2c"), (r"fast_kernel<double, \d+, \d+, 0, false", "fft_c2c"),
              (r"fin_kernel", "amp_fin"),
              (r"los_fwd_items|los_fwd_boxes|los_fwd_tiles", "los_fwd_items"), (r"los_fwd_reduce", "los_fwd_reduce"),
