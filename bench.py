@@ -603,7 +603,6 @@ def newton_roofline(ift, one, R):
         paths[getattr(self, "path", "?")] += 1
         return r
     fused_cg.FusedCGBatch.run_packed = run_packed
-    spec0 = fused_cg.STATS["pipelined_spec"]
     try:
         one()
     finally:
@@ -621,8 +620,7 @@ def newton_roofline(ift, one, R):
             "us_per_rhs_iter": round(rec[2] * 1e6 / rec[1], 1), "bytes_per_rhs_iter": per,
             "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s", "frac": round(gbs / 8000.0, 4),
             "path": "separate direction / curvature d.q / update passes (value-driven controllers keep the "
-                    "reference's d.q); solves by fused_cg path: " + ", ".join(f"{p} {n}" for p, n in sorted(paths.items())),
-            "speculative_steps": int(fused_cg.STATS["pipelined_spec"] - spec0)}
+                    "reference's d.q); solves by fused_cg path: " + ", ".join(f"{p} {n}" for p, n in sorted(paths.items()))}
 
 
 class _TimedComm:

@@ -75,21 +75,6 @@ extern "C" {
                         * NaN new gamma freezes the RHS too (DONE = 2; the guard always does) */
 #define NFT_CG_NSCALARS 16
 
-/* device-resident controller block of one RHS (double[NFT_CG_NCTL]) for
- * nft_cg_check_batched: the state of its iteration controller */
-#define NFT_CTL_KIND 0     /* NFT_CTL_GRADNORM / _ABSDELTA / _DELTA */
-#define NFT_CTL_P0 1       /* deltaE / tol_rel_deltaE (GradientNorm: unused) */
-#define NFT_CTL_P1 2       /* unused */
-#define NFT_CTL_LEVEL 3    /* convergence_level */
-#define NFT_CTL_LIMIT 4    /* iteration_limit (-1: none) */
-#define NFT_CTL_ITER 5     /* _itcount */
-#define NFT_CTL_CCOUNT 6   /* _ccount */
-#define NFT_CTL_EOLD 7     /* _Eold */
-#define NFT_CTL_NCTL 8
-#define NFT_CG_NCTL NFT_CTL_NCTL
-#define NFT_CTL_GRADNORM 1
-#define NFT_CTL_ABSDELTA 2
-#define NFT_CTL_DELTA 3
 
 const char* nft_last_error(void);
 void nft_release_caches(void);
@@ -482,17 +467,6 @@ int nft_cg_update_seg2_batched(void* x, void* r, const void* d, const void* q, i
                                int64_t n2, int blk2, int64_t vstride, int nrhs, int dtype, double shift,
                                const double* sc, double* part, int nbtot, hipStream_t stream);
 int nft_cg_finalize_batched(const double* part, int nbtot, int nrhs, double* sc, hipStream_t stream);
-/* The host's per-step checks on the device (ConjugateGradient, conjugate_
- * gradient.py:84-118, then the RHS's controller: GradientNormController
- * without tolerances (the count), DeltaEnergyController,
- * AbsDeltaEnergyController, iteration_controllers.py), on the step's scalars
- * sc (energy 0.5 (x.r - x.b)) and the controller blocks ctl (NFT_CG_NCTL doubles per RHS,
- * updated as the controller's check updates its state).  A RHS whose DONE is
- * 0 and whose step is terminal gets DONE = 2 (guard tripped, gamma NaN,
- * negative or zero), one whose controller stops DONE = 3: queued steps behind
- * it leave it unchanged.  Lets the host queue the next step before it reads
- * this one (FusedCGBatch with value-driven controllers). */
-int nft_cg_check_batched(double* sc, double* ctl, int nrhs, hipStream_t stream);
 
 /* ---- correlated-field amplitude Jacobian ------------------------------ */
 /* Constants of the amplitude linearisation at one expansion point (all device

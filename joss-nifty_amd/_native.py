@@ -78,7 +78,6 @@ SIGNATURES = {
     "nft_cg_update_seg2_batched": (_i, [_p, _p, _p, _p, _i64, _i, _i64, _i64, _i, _i64, _i, _i, _d, _p, _p, _i, _p]),
     "nft_cg_direction_dd2_batched": (_i, [_p, _p, _i64, _i64, _i64, _i64, _i, _i, _p, _d, _p, _i64, _i64, _p]),
     "nft_cg_finalize_batched": (_i, [_p, _i, _i, _p, _p]),
-    "nft_cg_check_batched": (_i, [_p, _p, _i, _p]),
     "nft_amp2_enabled": (_i, []),
     "nft_amp2_set_enabled": (None, [_i]),
     "nft_amp2_tiles": (_i, [_i64, _i, _i]),
@@ -143,9 +142,6 @@ class AmpOut(ctypes.Structure):
 
 CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD, CG_DONE, CG_ITER, CG_AUTO = range(11)
 CG_NSCALARS = 16
-# controller blocks of nft_cg_check_batched (nifty_amd.h NFT_CTL_*)
-CG_NCTL = 8
-CTL_GRADNORM, CTL_ABSDELTA, CTL_DELTA = 1, 2, 3
 AMP2_FALLBACK = 1  # NFT_AMP2_FALLBACK
 
 _lib = None

@@ -52,6 +52,16 @@ constexpr int E = 4;  // bins per thread: tile = E * NT bins, whatever the batch
 constexpr int TL = E * NT;
 constexpr int MAXR = 256;     // right-hand sides per launch (per-RHS arrival counters)
 constexpr int NS_ = NFT_CG_NSCALARS;
+// minimum waves per SIMD asked of the compiler for the four tile kernels
+// (__launch_bounds__ second argument; 0: none)
+#ifndef NFT_AMP2_WAVES
+#define NFT_AMP2_WAVES 0
+#endif
+#if NFT_AMP2_WAVES > 0
+#define NFT_AMP2_LB __launch_bounds__(NT, NFT_AMP2_WAVES)
+#else
+#define NFT_AMP2_LB __launch_bounds__(NT)
+#endif
 
 enum { KFL = 0, KSL = 1, KFLEX = 2, KASP = 3, KZM = 4, KSPEC = 5 };
 
@@ -351,7 +361,7 @@ __device__ __forceinline__ AmpConst const_of(const AmpConst& c, const AmpConst* 
 // last workgroup of each RHS then forms that RHS's tile carries.  TB: the
 // constant scan (LVc) and sums (LVt, MS2..MS4) from the table
 template <typename VT, int MODE, bool TB>
-__global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
+__global__ NFT_AMP2_LB void jvp2a_kernel(Jvp2Args<VT> a) {
   __shared__ double sh[2 * E * NW + 8 * NW];
   __shared__ int lflag;
   int i, r;
@@ -550,7 +560,7 @@ __global__ __launch_bounds__(NT) void jvp2a_kernel(Jvp2Args<VT> a) {
 // second launch: da from Eh and the carries; tile 0 writes the scalar keys'
 // new direction.  TB: LVc from the table
 template <typename VT, int MODE, bool TB>
-__global__ __launch_bounds__(NT) void jvp2b_kernel(Jvp2Args<VT> a) {
+__global__ NFT_AMP2_LB void jvp2b_kernel(Jvp2Args<VT> a) {
   __shared__ double sh[E * NW + 8];
   int i, r;
   if (!place(a.nb, a.nrhs, i, r)) return;
@@ -721,7 +731,7 @@ __device__ __forceinline__ void vjp_scans_g(const double (&G)[E], const double (
 // that RHS's k, R1, R2, R4, R5 and the carries beta, S1 of every tile.  TB:
 // the constant rows and scans from the table
 template <typename VT, int MODE, bool TB>
-__global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
+__global__ NFT_AMP2_LB void vjp2a_kernel(Vjp2Args<VT> a) {
   __shared__ double sh[3 * E * NW + 24 * NW];
   __shared__ int lflag;
   int i, r;
@@ -942,7 +952,7 @@ __global__ __launch_bounds__(NT) void vjp2a_kernel(Vjp2Args<VT> a) {
 // r.r / x.r partials and the finalize by the last workgroup of the grid.
 // TB: the constant scans from the table
 template <typename VT, int MODE, bool TB>
-__global__ __launch_bounds__(NT) void vjp2b_kernel(Vjp2Args<VT> a) {
+__global__ NFT_AMP2_LB void vjp2b_kernel(Vjp2Args<VT> a) {
   __shared__ double sh[3 * E * NW + 8];
   int i, r;
   const bool valid = place(a.nb, a.nrhs, i, r);

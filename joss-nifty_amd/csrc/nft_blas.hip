@@ -265,47 +265,6 @@ __global__ __launch_bounds__(RED_NT) void cg_finalize_kernel(const double* __res
   }
 }
 
-// The host-side checks of one CG step, on the device (nft_cg_check_batched):
-// one thread per RHS, the decisions of conjugate_gradient.py:84-118 (guard ->
-// ERROR, gamma NaN / negative -> ERROR, gamma zero -> CONVERGED) and then of
-// the RHS's controller (iteration_controllers.py:188-221 GradientNorm without
-// tolerances, :319-357 DeltaEnergy, :390-423 AbsDeltaEnergy) on the step's
-// scalars, the same IEEE operations the Python check does on the host copy.  A stop
-// freezes the RHS (DONE = 2 terminal, 3 controller) before the next queued
-// step runs; the host replays the checks later and compares.
-__global__ void cg_check_kernel(double* __restrict__ sc, double* __restrict__ ctl, int nrhs) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrhs) return;
-  double* s = sc + (long long)r * NFT_CG_NSCALARS;
-  double* c = ctl + (long long)r * NFT_CG_NCTL;
-  if (s[NFT_CG_DONE] != 0.0) return;
-  const double g = s[NFT_CG_GAMMA];
-  if (s[NFT_CG_FLAG] != 0.0 || g != g || g <= 0.0) {
-    s[NFT_CG_DONE] = 2.0;
-    return;
-  }
-  const int kind = (int)c[NFT_CTL_KIND];
-  const double it = c[NFT_CTL_ITER] + 1.0;
-  c[NFT_CTL_ITER] = it;
-  bool inclvl = false;
-  if (kind != NFT_CTL_GRADNORM) {  // GradientNorm without tolerances: counts only
-    const double e = 0.5 * (s[NFT_CG_XR] - s[NFT_CG_XB]);
-    const double eo = c[NFT_CTL_EOLD];
-    if (it > 0.0) {
-      if (kind == NFT_CTL_ABSDELTA) {
-        inclvl = fabs(eo - e) < c[NFT_CTL_P0];
-      } else {
-        inclvl = fabs(eo - e) / fmax(fabs(eo), fabs(e)) < c[NFT_CTL_P0];
-      }
-    }
-    c[NFT_CTL_EOLD] = e;
-  }
-  const double cc = inclvl ? c[NFT_CTL_CCOUNT] + 1.0 : fmax(0.0, c[NFT_CTL_CCOUNT] - 1.0);
-  c[NFT_CTL_CCOUNT] = cc;
-  const double lim = c[NFT_CTL_LIMIT];
-  if ((lim >= 0.0 && it >= lim) || cc >= c[NFT_CTL_LEVEL]) s[NFT_CG_DONE] = 3.0;
-}
-
 // d = max(0, gamma/gprev) d + r
 template <typename T>
 __global__ void cg_dir_kernel(T* __restrict__ d, const T* __restrict__ r, long long n, long long vs,
@@ -635,18 +594,6 @@ int nft_cg_update_seg2_batched(void* x, void* r, const void* d, const void* q, i
 int nft_cg_finalize_batched(const double* part, int nbtot, int nrhs, double* sc, hipStream_t stream) {
   prof_mark(stream, "cg_finalize_kernel");
   hipLaunchKernelGGL(cg_finalize_kernel, dim3(nrhs), dim3(RED_NT), 0, stream, part, nbtot, sc);
-  NFT_HIP_CHECK(hipGetLastError());
-  return NFT_OK;
-}
-
-int nft_cg_check_batched(double* sc, double* ctl, int nrhs, hipStream_t stream) {
-  if (!sc || !ctl || nrhs < 0) {
-    set_last_error("nft_cg_check_batched: invalid arguments");
-    return NFT_ERR_ARG;
-  }
-  if (nrhs == 0) return NFT_OK;
-  prof_mark(stream, "cg_check");
-  hipLaunchKernelGGL(cg_check_kernel, dim3((nrhs + 63) / 64), dim3(64), 0, stream, sc, ctl, nrhs);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

@@ -170,37 +170,6 @@ _COUNT_ONLY_STATE = _CountOnlyState()
 # queued CG iterations between host reads (NFT_CG_CHUNK=0: one read per step)
 CHUNK = os.environ.get("NFT_CG_CHUNK", "1") != "0"
 
-# value-driven controllers checked on the device (nft_cg_check_batched) so
-# that the host queues step i + 1 before it reads step i (NFT_CG_PIPELINE=1;
-# off by default: bitwise the synchronous loop, but measured slower -- demo
-# step 815 -> 870 ms, Newton-direction CG 794 -> 866 us per RHS iteration:
-# the step queued behind a solve's last one runs the whole batched matvec for
-# frozen right-hand sides, and the eager launch gaps it hides were smaller)
-PIPELINE = os.environ.get("NFT_CG_PIPELINE", "0") == "1"
-
-
-def _device_ctl(ctl):
-    """the controller block (nifty_amd.h NFT_CTL_*) of a controller whose
-    check nft_cg_check_batched evaluates with the host's arithmetic, taken
-    right after ctl.start(), or None.  Exact classes only (a subclass may
-    override check); GradientNormController without tolerances (it counts),
-    AbsDeltaEnergyController and DeltaEnergyController."""
-    from .iteration_controllers import (AbsDeltaEnergyController, DeltaEnergyController,
-                                        GradientNormController)
-    lim = getattr(ctl, "_iteration_limit", None)
-    lim = -1.0 if lim is None else float(lim)
-    if _count_only(ctl):
-        return [float(_native.CTL_GRADNORM), 0.0, 0.0, float(ctl._convergence_level), lim,
-                float(ctl._itcount), float(ctl._ccount), 0.0]
-    t = type(ctl)
-    if t is AbsDeltaEnergyController or t is DeltaEnergyController:
-        kind = _native.CTL_ABSDELTA if t is AbsDeltaEnergyController else _native.CTL_DELTA
-        p0 = ctl._deltaE if t is AbsDeltaEnergyController else ctl._tol_rel_deltaE
-        return [float(kind), float(p0), 0.0, float(ctl._convergence_level), lim,
-                float(ctl._itcount), float(ctl._ccount), float(ctl._Eold)]
-    return None
-
-
 def _quad_blocks(core, W, dtype, controllers=()):
     """partials per RHS of the metric's data-space quadratic form, or 0"""
     if not CURV_DATA or dtype not in (torch.float64, torch.float32):
@@ -701,153 +670,6 @@ class FusedCGBatch(FusedCG):
         # stays eager (the one-off capture measured slower: demo step 858 ->
         # 834 ms eager, Newton-direction CG 788 -> 747 us per RHS iteration)
         eager_only = any(_reads_value(c) for c in self.controllers)
-        ctl_rows = [_device_ctl(self.controllers[j]) if j in active else [0.0] * _native.CG_NCTL
-                    for j in range(k0)]
-        # (a decision trace reads the values the checks see: path-neutral)
-        if PIPELINE and eager_only and not chunkable and all(ctl_rows[j] is not None for j in active):
-            self.path += "+pipeline"
-            CTL = torch.tensor(ctl_rows, dtype=torch.float64).to(dev)
-            nonlocal_state = {"ii": ii, "first": first}
-            ring = []
-
-            def new_ring(k):
-                ring[:] = [(torch.zeros((k, NS), dtype=torch.float64).pin_memory(), torch.cuda.Event())
-                           for _ in range(3)]
-            new_ring(len(rows))
-            nslot = [0]
-
-            def enqueue():
-                """one step on the device, its checks on the device, and an
-                async copy of its scalars (read by process() later)"""
-                ii_, first_ = nonlocal_state["ii"] + 1, nonlocal_state["first"]
-                k = X.shape[0]
-                sp = _native.stream_ptr()
-                if ii_ < self.nreset:
-                    body(not first_)
-                else:
-                    Q, Bu = st["Q"], st["Bu"]
-                    if not first_:
-                        chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), sp))
-                    core.metric_flat_batch(D, Q, self.W, 0.0)
-                    chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), sp))
-                    gp = SC[:, _native.CG_GAMMA].clone()
-                    chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws),
-                                                  sp))
-                    if st["AX"] is None:
-                        st["AX"] = torch.zeros_like(X)
-                    AX = st["AX"]
-                    core.metric_flat_batch(X, AX, self.W, 0.0)
-                    flag = SC[:, _native.CG_FLAG].clone()
-                    chk(lib.nft_cg_residual_batched(P(Rr), P(AX), P(X), P(Bv), n, n, k, dt, sh, P(SC), P(ws), sp))
-                    live = SC[:, _native.CG_DONE] == 0.0
-                    SC[:, _native.CG_GPREV] = torch.where(live, gp, SC[:, _native.CG_GPREV])
-                    SC[:, _native.CG_FLAG] = torch.where(live, flag, SC[:, _native.CG_FLAG])
-                    ii_ = 0
-                chk(lib.nft_cg_check_batched(P(SC), P(CTL), k, _native.stream_ptr()))
-                buf, ev = ring[nslot[0] % len(ring)]
-                nslot[0] += 1
-                buf.copy_(SC, non_blocking=True)
-                ev.record()
-                nonlocal_state["ii"], nonlocal_state["first"] = ii_, False
-                xb_dev = st["Bu"] is not None or st["xbdot"] or ii_ == 0
-                return buf, ev, xb_dev
-
-            def process(rec):
-                """the host's checks of one queued step, in the synchronous
-                loop's order, against the device's decisions"""
-                buf, ev, xb_dev = rec
-                ev.synchronize()
-                h = buf.numpy()
-                self.niter += 1
-                ConjugateGradient.iterations_total += len(active)
-                for j in list(active):
-                    ctl = self.controllers[j]
-                    hj = h[pos[j]]
-                    status = None
-                    if hj[_native.CG_FLAG] != 0.0:
-                        curv = hj[_native.CG_CURV]
-                        if np.isnan(curv):
-                            logger.error("Error: ConjugateGradient: curv==NaN")
-                        elif curv == 0.:
-                            logger.error("Error: ConjugateGradient: curv==0.")
-                        else:
-                            logger.error("Error: ConjugateGradient: alpha<0.")
-                        status = ctl.ERROR
-                    else:
-                        gamma = float(hj[_native.CG_GAMMA])
-                        if np.isnan(gamma):
-                            logger.error("Error: ConjugateGradient: gamma==NaN")
-                            status = ctl.ERROR
-                        elif gamma < 0:
-                            logger.error("Positive definiteness of preconditioner violated!")
-                            status = ctl.ERROR
-                        elif gamma == 0:
-                            status = ctl.CONVERGED
-                        else:
-                            xr = float(hj[_native.CG_XR])
-                            xb = float(hj[_native.CG_XB]) if (xb_dev or Bv is None) else math.nan
-                            if not (xb_dev or Bv is None):
-                                raise RuntimeError("pipelined CG step without x.b on the device")
-                            state = _State(0.5 * (xr - xb), math.sqrt(gamma), _stale)
-                            ehist[j] = (ehist[j] + [0.5 * (xr - xb)])[-3:]
-                            sts = ctl.check(state)
-                            if sts != ctl.CONTINUE:
-                                status = sts
-                    dev_stop = hj[_native.CG_DONE] in (2.0, 3.0)
-                    if dev_stop != (status is not None):
-                        raise RuntimeError(f"device controller check of RHS {j} disagrees with the host "
-                                           f"(device stop {dev_stop}, host status {status})")
-                    if status is not None:
-                        finish(j, status)
-                        active.remove(j)
-
-            # energies of the last processed steps per RHS (speculation guess)
-            ehist = {j: ([self.controllers[j]._Eold] if ctl_rows[j][0] != _native.CTL_GRADNORM else [])
-                     for j in active}
-
-            def likely_last(j):
-                """True if RHS j probably stops at its next (queued, not yet
-                read) step: its iteration limit, or an energy-difference
-                controller whose differences, extrapolated geometrically from
-                the last two, fall below its threshold.  A guess: it only
-                decides whether the host queues one more step before reading
-                (a wrong guess costs a wasted step or a host round trip)."""
-                ctl = self.controllers[j]
-                lim = getattr(ctl, "_iteration_limit", None)
-                if lim is not None and ctl._itcount + 1 >= lim:
-                    return True
-                if ctl_rows[j][0] == _native.CTL_GRADNORM:
-                    return False
-                e = ehist[j]
-                if len(e) < 3 or ctl._ccount + 1 < ctl._convergence_level:
-                    return False
-                d1, d2 = abs(e[-1] - e[-2]), abs(e[-2] - e[-3])
-                pred = d1 * d1 / d2 if d2 > 0 else 0.0
-                if ctl_rows[j][0] == _native.CTL_DELTA:
-                    pred /= max(abs(e[-1]), 1e-300)
-                return pred < 2.0 * ctl_rows[j][1]
-
-            inflight = collections.deque()
-            while active:
-                if not inflight:
-                    inflight.append(enqueue())
-                if len(inflight) < 2 and not all(likely_last(j) for j in active):
-                    inflight.append(enqueue())   # speculative: queued before this step is read
-                    STATS["pipelined_spec"] += 1
-                process(inflight.popleft())
-                if active and can_compact and _worth_compacting(self.controllers, active, len(rows)):
-                    while inflight and active:
-                        process(inflight.popleft())
-                    inflight.clear()  # steps behind the last live RHS change nothing
-                    if active and _worth_compacting(self.controllers, active, len(rows)):
-                        keep = sorted(pos[j] for j in active)
-                        compact()
-                        CTL = CTL.index_select(0, torch.tensor(keep, device=dev))
-                        new_ring(len(rows))
-                        self.compactions += 1
-                        STATS["compactions"] += 1
-            STATS["pipelined_iters"] += self.niter
-            active.clear()
         while active:
             if chunkable and graph is not None and ii + 2 < self.nreset:
                 m = min(min(self.controllers[j]._iteration_limit - self.controllers[j]._itcount for j in active),

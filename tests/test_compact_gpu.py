@@ -115,60 +115,3 @@ def test_compacted_newton_directions_bitwise(ift, monkeypatch):
     assert ncomp.get(True, 0) >= 1 and ncomp.get(False, 0) == 0
     for a, b in zip(res[False], res[True]):
         assert np.array_equal(a, b)
-
-
-@pytest.mark.parametrize("which", ["los", "gauss"])
-def test_pipelined_value_controllers_bitwise(ift, which, monkeypatch):
-    """value-driven controllers checked on the device (nft_cg_check_batched)
-    while the host queues the next step (fused_cg.PIPELINE): bitwise the
-    synchronous loop, with the same checks, statuses and iteration counts,
-    with and without compaction, across the nreset = 20 residual refresh"""
-    from nifty_amd.minimization import fused_cg
-    cf, A, (core, W, shift) = _metric(ift, which)
-    es = _energies(ift, cf, A, 4, 9)
-    ctls = [ift.AbsDeltaEnergyController(d, iteration_limit=m)
-            for d, m in ((1e-1, 40), (1e-3, 7), (1e-6, 26), (1e-9, 30))] + \
-        [ift.GradientNormController(iteration_limit=12, name="counted")]
-    es = es + _energies(ift, cf, A, 1, 10)
-    for comp in (False, True):
-        monkeypatch.setattr(fused_cg, "COMPACT", comp)
-        out = {}
-        for on in (False, True):
-            monkeypatch.setattr(fused_cg, "PIPELINE", on)
-            cs = [copy.deepcopy(c) for c in ctls]
-            n0 = fused_cg.STATS["pipelined_iters"]
-            cg = fused_cg.FusedCGBatch(core, W, shift, cs)
-            out[on] = (cg.run(es), [c._itcount for c in cs], [getattr(c, "_ccount", None) for c in cs], cg.niter,
-                       fused_cg.STATS["pipelined_iters"] - n0, cg.path)
-        assert out[True][4] > 0 and out[False][4] == 0, (out[True][4:], out[False][4:])
-        assert "+pipeline" in out[True][5]
-        assert out[True][1] == out[False][1] and out[True][2] == out[False][2]
-        assert out[True][3] == out[False][3]
-        assert len(set(out[True][1])) > 1
-        for (e1, s1), (e2, s2) in zip(out[False][0], out[True][0]):
-            assert s1 == s2
-            for key in cf.domain.keys():
-                assert torch.equal(e1.position[key].val, e2.position[key].val), key
-                assert torch.equal(e1.gradient[key].val, e2.gradient[key].val), key
-
-
-def test_pipelined_newton_directions_bitwise(ift, monkeypatch):
-    """batched geoVI refinement with the demo's controllers (AbsDelta sampling
-    CG and NewtonCG directions, per-sample metrics): the pipelined loop gives
-    bitwise the samples of the synchronous one"""
-    from nifty_amd.minimization import fused_cg
-    cf, lh, pos = _problem(ift, "los")
-    res = {}
-    for on in (False, True):
-        monkeypatch.setattr(fused_cg, "PIPELINE", on)
-        n0 = fused_cg.STATS["pipelined_iters"]
-        H = ift.StandardHamiltonian(lh, ift.AbsDeltaEnergyController(deltaE=0.05, iteration_limit=30))
-        mini = ift.NewtonCG(ift.AbsDeltaEnergyController(deltaE=0.5, convergence_level=2, iteration_limit=4))
-        ift.random.push_sseq_from_seed(22)
-        sl = ift.draw_samples(pos, H, mini, 2, True)
-        ift.random.pop_sseq()
-        res[on] = ([np.concatenate([np.ravel(r[k].val.cpu().numpy()) for k in cf.domain.keys()]) for r in sl._r],
-                   fused_cg.STATS["pipelined_iters"] - n0)
-    assert res[True][1] > 0 and res[False][1] == 0
-    for a, b in zip(res[False][0], res[True][0]):
-        assert np.array_equal(a, b)
