@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-pairs", type=int, default=1, help="mirrored pairs in the timed CPU oracle draw")
     p.add_argument("--cpu-lin-iters", type=int, default=None,
-                   help="C2/C4/C5: linear-CG iterations of the timed CPU oracle run (default 3; C4 1)")
+                   help="C2/C4/C5: linear-CG iterations of the timed CPU oracle run (default C2 200, C5 15, C4 2)")
     p.add_argument("--no-demo", action="store_true", help="skip the demo-controller line")
     p.add_argument("--deterministic-allreduce", action="store_true")
     p.add_argument("--backend", choices=["nccl", "gloo", "none"], default=None,
@@ -79,7 +79,9 @@ def parse():
     if a.samples_per_gpu is None:
         a.samples_per_gpu = cfg["pairs"]
     if a.cpu_lin_iters is None:
-        a.cpu_lin_iters = 1 if len(cfg["shape"]) == 3 else 3
+        # about 10 s of host work on the GPU box's cores (C2 ~23, C5 ~1.3,
+        # C4 ~0.15 oracle CG iterations per second there)
+        a.cpu_lin_iters = {"C2": 200, "C5": 15, "C4": 2}.get(a.config, 3)
     return a
 
 
