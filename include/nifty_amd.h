@@ -447,6 +447,15 @@ int nft_cg_direction_dd2_batched(void* d, const void* r, int64_t n1, int64_t o2,
                                  int64_t pstride, hipStream_t stream);
 int nft_fold_partials(const double* part, int nb, int nrhs, double* out, int64_t out_stride,
                       hipStream_t stream);
+/* nft_los_adjoint_batched and nft_fold_partials(fold_part, fold_nb,
+ * fold_nrhs, fold_out, fold_ostride) in ONE launch (the fold runs as the first
+ * fold_nrhs workgroups of the adjoint's grid, bitwise the separate call): the
+ * carried CG's curvature, needed only by the adjoint transform's last pass,
+ * without a launch of its own between the two LOS passes and the transform. */
+int nft_los_adjoint_fold(const nft_los_plan* plan, const void* y, const void* colscale,
+                         const void* rowscale, void* out, int dtype, double scale, int nvec,
+                         int64_t y_stride, int64_t out_stride, const double* fold_part, int fold_nb,
+                         int fold_nrhs, double* fold_out, int64_t fold_ostride, hipStream_t stream);
 /* The CG update split over segments of the packed vectors (pointers offset by
  * the caller), so that the update of one segment can run while another
  * segment's q is still being formed (the amplitude keys' VJP on a second

@@ -57,6 +57,7 @@ SIGNATURES = {
     "nft_los_adjoint": (_i, [_p, _p, _p, _p, _p, _i, _d, _p]),
     "nft_los_forward_batched": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p]),
     "nft_los_adjoint_batched": (_i, [_p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p]),
+    "nft_los_adjoint_fold": (_i, [_p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p, _i, _i, _p, _i64, _p]),
     "nft_los_quad_blocks": (_i, [_p]),
     "nft_los_forward_quad_batched": (_i, [_p, _p, _p, _p, _p, _p, _i, _d, _i, _i64, _i64, _p, _i64, _p]),
     "nft_los_forward_ex": (_i, [_p, _p, _p, _i64, _p, _p, _p, _i, _d, _i, _i64, _i64, _p, _i64, _p]),
@@ -545,11 +546,21 @@ def los_forward_quad_batched(plan, x, y, qpart, colscale=None, rowscale=None, sc
     return y
 
 
-def los_adjoint_batched(plan, y, out, colscale=None, rowscale=None, scale=1.0):
-    """out[b] = scale * rowscale * R^T (colscale * y[b])."""
+def los_adjoint_batched(plan, y, out, colscale=None, rowscale=None, scale=1.0, fold=None):
+    """out[b] = scale * rowscale * R^T (colscale * y[b]).  fold: (part, nb,
+    nrhs, out_address, out_stride) of an nft_fold_partials call carried by the
+    same launch (nft_los_adjoint_fold)."""
     lib = load()
     require_device(y, out, colscale, rowscale)
     k = y.shape[0]
+    if fold is not None:
+        part, nb, nrhs, faddr, fstride = fold
+        require_device(part)
+        _check(lib.nft_los_adjoint_fold(ctypes.byref(plan), ptr(y), ptr(colscale), ptr(rowscale), ptr(out),
+                                        dtype_code(y.dtype), float(scale), k, y[0].numel(), out[0].numel(),
+                                        ptr(part), int(nb), int(nrhs), ctypes.c_void_p(faddr), int(fstride),
+                                        stream_ptr()))
+        return out
     _check(lib.nft_los_adjoint_batched(ctypes.byref(plan), ptr(y), ptr(colscale), ptr(rowscale), ptr(out),
                                        dtype_code(y.dtype), float(scale), k, y[0].numel(), out[0].numel(),
                                        stream_ptr()))

@@ -359,6 +359,42 @@ __global__ __launch_bounds__(256) void los_fwd_reduce(nft_los_plan p, const doub
   }
 }
 
+// The CG curvature fold (nft_fold_partials) carried by an adjoint launch as
+// its first nrhs workgroups (nft_los_adjoint_fold): out[r * ostride] = the sum
+// of part[r * nb + b] over b < nb in fold_wide's order -- 1024 thread-strided
+// sums (here virtual thread q * 256 + t, q < 4), the 16 waves' shuffle trees,
+// the wave totals in order -- so bitwise the separate launch.
+struct LosFold {
+  const double* part;
+  double* out;
+  long long ostride;
+  int nb, nrhs;
+};
+__device__ __forceinline__ void los_fold_rhs(const LosFold& f, int r, double* sh) {
+  const double* part = f.part + (long long)r * f.nb;
+  const int t = threadIdx.x;
+  double v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = 0.0;
+    for (int b = q * 256 + t; b < f.nb; b += 1024) v[q] += part[b];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[q] += __shfl_down(v[q], off, 64);
+  if ((t & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sh[q * 4 + (t >> 6)] = v[q];
+  }
+  __syncthreads();
+  if (t == 0) {
+    double s = 0.0;
+    for (int w = 0; w < 16; ++w) s += sh[w];
+    f.out[(long long)r * f.ostride] = s;
+  }
+}
+
 // Batched over K vectors (template): the chunk's entries (line index +
 // fp32 weight) are staged in LDS once; every pixel thread sums its run for
 // all K vectors in registers from the per-vector line tables.  Per vector the
@@ -367,7 +403,8 @@ template <typename T, typename IDX, int K, bool VEC = false>
 __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* __restrict__ lidx,
                                                      const T* __restrict__ yv, const T* __restrict__ cs,
                                                      const T* __restrict__ rs, T* __restrict__ out, double scale,
-                                                     long long ys, long long os, long long rss, int kv) {
+                                                     long long ys, long long os, long long rss, int kv,
+                                                     LosFold fold) {
 #pragma clang fp contract(off)
   constexpr int PER = LOS_CH_A / 256;
   // line table: 256 lines per vector cover every box of an 8-bit-index plan
@@ -379,7 +416,11 @@ __global__ __launch_bounds__(256) void los_adj_boxes(nft_los_plan p, const IDX* 
   __shared__ __align__(16) float ew[K == 1 ? 2 * LOS_CH_A : LOS_CH_A];
   __shared__ __align__(16) IDX el[K == 1 ? 1 : LOS_CH_A];
   const BoxGeom g{p.H, p.W, p.bh, p.bw, p.nby, p.nbx};
-  const int box = (int)blockIdx.x, t = threadIdx.x;
+  if ((int)blockIdx.x < fold.nrhs) {  // the carried curvature fold (first workgroups)
+    los_fold_rhs(fold, (int)blockIdx.x, yl);
+    return;
+  }
+  const int box = (int)blockIdx.x - fold.nrhs, t = threadIdx.x;
   if (box >= p.nbox) return;
   const int l0 = p.box_lptr[box], nl = p.box_lptr[box + 1] - l0;
   // 16-entry chunks with 16-byte loads (box runs padded, box_ent_adj)
@@ -538,17 +579,18 @@ static void fwd_items_k(const nft_los_plan* p, const T* x, const T* cs, double* 
 
 template <typename T, typename IDX, int K>
 static void adj_boxes_k(const nft_los_plan* p, const IDX* li, const T* y, const T* cs, const T* rs, T* out,
-                        double scale, long long ys, long long os, long long rss, int kv, hipStream_t s) {
-  const dim3 grid((unsigned)p->nbox);
+                        double scale, long long ys, long long os, long long rss, int kv, hipStream_t s,
+                        const LosFold& fold) {
+  const dim3 grid((unsigned)(p->nbox + fold.nrhs));
   if constexpr (K > 1 && sizeof(IDX) == 1) {
     if (p->box_ent_adj) {
       hipLaunchKernelGGL((los_adj_boxes<T, IDX, K, true>), grid, dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys, os,
-                         rss, kv);
+                         rss, kv, fold);
       return;
     }
   }
   hipLaunchKernelGGL((los_adj_boxes<T, IDX, K>), grid, dim3(256), 0, s, *p, li, y, cs, rs, out, scale, ys, os, rss,
-                     kv);
+                     kv, fold);
 }
 
 // vectors are processed in groups of 8 / 4 / 2 / 1 (template sizes); a
@@ -603,17 +645,19 @@ static int los_forward_t(const nft_los_plan* p, const void* x, const void* cs, c
 template <typename T, typename IDX>
 static void los_adjoint_idx(const nft_los_plan* p, const IDX* li, const void* y, const void* cs, const void* rs,
                             void* out, double scale, int K, long long ys, long long os, hipStream_t s,
-                            long long rss = 0) {
+                            long long rss = 0, const LosFold* fold = nullptr) {
+  const LosFold none{nullptr, nullptr, 0, 0, 0};
   for (int v = 0; v < K;) {
     const int g = kgroup(K - v), kv = std::min(g, K - v);
     const T* yv = (const T*)y + v * ys;
     const T* rv = rs ? (const T*)rs + v * rss : nullptr;
     T* ov = (T*)out + v * os;
+    const LosFold& fv = (v == 0 && fold) ? *fold : none;  // the first launch carries it
     switch (g) {
-      case 8: adj_boxes_k<T, IDX, 8>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s); break;
-      case 4: adj_boxes_k<T, IDX, 4>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s); break;
-      case 2: adj_boxes_k<T, IDX, 2>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s); break;
-      default: adj_boxes_k<T, IDX, 1>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, 1, s); break;
+      case 8: adj_boxes_k<T, IDX, 8>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s, fv); break;
+      case 4: adj_boxes_k<T, IDX, 4>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s, fv); break;
+      case 2: adj_boxes_k<T, IDX, 2>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, kv, s, fv); break;
+      default: adj_boxes_k<T, IDX, 1>(p, li, yv, (const T*)cs, rv, ov, scale, ys, os, rss, 1, s, fv); break;
     }
     v += kv;
   }
@@ -621,14 +665,16 @@ static void los_adjoint_idx(const nft_los_plan* p, const IDX* li, const void* y,
 
 template <typename T>
 static int los_adjoint_t(const nft_los_plan* p, const void* y, const void* cs, const void* rs, void* out, double scale,
-                         int K, long long ys, long long os, hipStream_t s, long long rss = 0) {
+                         int K, long long ys, long long os, hipStream_t s, long long rss = 0,
+                         const LosFold* fold = nullptr) {
   if (p->nbox <= 0) return NFT_OK;
   prof_mark(s, "los_adj_boxes");
   if (p->lidx8)
-    los_adjoint_idx<T, unsigned char>(p, (const unsigned char*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s, rss);
+    los_adjoint_idx<T, unsigned char>(p, (const unsigned char*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s, rss,
+                                      fold);
   else
     los_adjoint_idx<T, unsigned short>(p, (const unsigned short*)p->ent_lidx, y, cs, rs, out, scale, K, ys, os, s,
-                                       rss);
+                                       rss, fold);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }
@@ -706,6 +752,26 @@ int nft_los_adjoint_batched(const nft_los_plan* p, const void* y, const void* co
   if (dtype == 1)
     return los_adjoint_t<float>(p, y, colscale, rowscale, out, scale, nvec, y_stride, out_stride, stream);
   set_last_error("nft_los_adjoint: bad dtype %d", dtype);
+  return NFT_ERR_ARG;
+}
+
+int nft_los_adjoint_fold(const nft_los_plan* p, const void* y, const void* colscale, const void* rowscale, void* out,
+                         int dtype, double scale, int nvec, int64_t y_stride, int64_t out_stride,
+                         const double* fold_part, int fold_nb, int fold_nrhs, double* fold_out, int64_t fold_ostride,
+                         hipStream_t stream) {
+  int st = check_plan(p);
+  if (st != NFT_OK) return st;
+  if (nvec < 1 || nvec > LOS_KMAX || p->nbox <= 0 || !fold_part || !fold_out || fold_nb < 1 || fold_nrhs < 1 ||
+      fold_ostride < 1) {
+    set_last_error("nft_los_adjoint_fold: 1 <= nvec <= %d, a non-empty plan and fold partials / output", LOS_KMAX);
+    return NFT_ERR_ARG;
+  }
+  const LosFold f{fold_part, fold_out, (long long)fold_ostride, fold_nb, fold_nrhs};
+  if (dtype == 0)
+    return los_adjoint_t<double>(p, y, colscale, rowscale, out, scale, nvec, y_stride, out_stride, stream, 0, &f);
+  if (dtype == 1)
+    return los_adjoint_t<float>(p, y, colscale, rowscale, out, scale, nvec, y_stride, out_stride, stream, 0, &f);
+  set_last_error("nft_los_adjoint_fold: bad dtype %d", dtype);
   return NFT_ERR_ARG;
 }
 

@@ -853,7 +853,13 @@ class CFJacobian(LinearOperator):
             g = s
         else:
             _native.hartley_fused(s, axes, m.c_h, pro=pro, convention=conv, shape=s.shape, batch=bt)
-            g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
+            fspec = getattr(after_w, "spec", None)
+            if fspec is not None and qpart is not None and callable(W) and getattr(W, "supports_fold", False):
+                # the fold rides in W's last launch (it needs only W's partials)
+                g = W(s, qpart=qpart, fold=fspec)
+                after_w = None
+            else:
+                g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
             g = g.contiguous()
         if after_w is not None:
             after_w()

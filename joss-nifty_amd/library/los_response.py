@@ -137,6 +137,9 @@ def los_coo(shape, distances, starts, ends, sigmas=None, truncation=3.):
 
 LOS_CAP_F = 2048   # entries per forward work item (csrc/nft_los.hip)
 LOS_KMAX = 8       # vectors per batched LOS launch (csrc/nft_los.hip)
+# the carried CG's curvature fold inside the LOS adjoint launch
+# (nft_los_adjoint_fold); NFT_LOS_FOLD=0: its own launch (A/B, tests)
+_FOLD_IN_ADJ = os.environ.get("NFT_LOS_FOLD", "1") != "0"
 BOX = 256
 
 
@@ -368,9 +371,12 @@ class LOSResponse(LinearOperator):
                 cast[dt] = (None if drf is None else drf.to(dt), None if cv is None else cv.to(dt))
             return cast[dt]
 
-        def middle(s, qpart=None):
+        def middle(s, qpart=None, fold=None):
             """qpart (optional, (k, >= quad_blocks) fp64): per-block partials of
-            the quadratic form s . middle(s), from the data space"""
+            the quadratic form s . middle(s), from the data space.  fold
+            (optional, with qpart): an nft_fold_partials call (part, nb, nrhs,
+            out address, out stride) that needs those partials, carried by
+            the last adjoint launch (nft_los_adjoint_fold)"""
             drf, cv = scales(s.dtype)
             if qpart is not None:
                 k = s.shape[0] if s.dim() > len(shape) else 1
@@ -381,7 +387,8 @@ class LOSResponse(LinearOperator):
                     b = min(k, a + LOS_KMAX)
                     _native.los_forward_quad_batched(plan, v[a:b], y[a:b], qpart[a:b], colscale=drf, rowscale=cv,
                                                      scale=scale)
-                    _native.los_adjoint_batched(plan, y[a:b], out[a:b].view(b - a, npix), rowscale=drf)
+                    _native.los_adjoint_batched(plan, y[a:b], out[a:b].view(b - a, npix), rowscale=drf,
+                                                fold=fold if b == k else None)
                 return out if s.dim() > len(shape) else out[0]
             if s.dim() > len(shape):
                 # batch of right-hand sides along a leading axis (batched CG):
@@ -403,6 +410,7 @@ class LOSResponse(LinearOperator):
             return out
         middle.supports_batch = True
         middle.supports_fp32 = True
+        middle.supports_fold = _FOLD_IN_ADJ
         middle.quad_blocks = int(_native.load().nft_los_quad_blocks(ctypes.byref(plan)))
         return middle
 

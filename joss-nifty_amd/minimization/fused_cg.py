@@ -383,6 +383,8 @@ class _CarryIteration:
             _native._check(lib.nft_fold_partials(_native.ptr(self.PQ), pstride, k,
                                                  ctypes.c_void_p(SC.data_ptr() + _native.CG_CURV * 8),
                                                  _native.CG_NSCALARS, _native.stream_ptr()))
+        # the same call as arguments, for a W that carries it in its own launch
+        fold.spec = (self.PQ, pstride, k, SC.data_ptr() + _native.CG_CURV * 8, _native.CG_NSCALARS)
         cg = dict(x=X[0, g0:], r=Rr[0, g0:], d=D[0, g0:], sc=SC, part=self.GP, stride=n, shift=self.shift,
                   nbtot=self.tiles, blk0=0)
         w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbd:], after_w=fold, cg=cg,
@@ -421,6 +423,7 @@ class _CarryIteration:
             _native._check(lib.nft_fold_partials(P(self.PQ), self.nbd + self.nq, k,
                                                  ctypes.c_void_p(SC.data_ptr() + _native.CG_CURV * 8),
                                                  _native.CG_NSCALARS, _native.stream_ptr()))
+        fold.spec = (self.PQ, self.nbd + self.nq, k, SC.data_ptr() + _native.CG_CURV * 8, _native.CG_NSCALARS)
         g0 = self.g0
         cg = dict(x=X[0, g0:], r=Rr[0, g0:], d=D[0, g0:], sc=SC, part=self.UP, stride=n, shift=self.shift,
                   nbtot=self.nbtot, blk0=self.tiles_blk0)

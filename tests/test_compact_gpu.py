@@ -115,3 +115,33 @@ def test_compacted_newton_directions_bitwise(ift, monkeypatch):
     assert ncomp.get(True, 0) >= 1 and ncomp.get(False, 0) == 0
     for a, b in zip(res[False], res[True]):
         assert np.array_equal(a, b)
+
+
+def test_fold_in_los_adjoint_bitwise(ift, monkeypatch):
+    """the carried iteration's curvature fold inside the LOS adjoint launch
+    (nft_los_adjoint_fold) gives bitwise the separate nft_fold_partials"""
+    from nifty_amd import _native
+    from nifty_amd.minimization.fused_cg import FusedCGBatch
+    cf, A, (core, W, shift) = _metric(ift, "los")
+    assert getattr(W, "supports_fold", False)
+    es = _energies(ift, cf, A, 3, 5)
+    lims = [6, 9, 23]
+    calls = []
+    orig = _native.los_adjoint_batched
+
+    def spy(*a, **kw):
+        calls.append(kw.get("fold") is not None)
+        return orig(*a, **kw)
+    monkeypatch.setattr(_native, "los_adjoint_batched", spy)
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(W, "supports_fold", on)
+        calls.clear()
+        cg = FusedCGBatch(core, W, shift, [ift.GradientNormController(iteration_limit=m) for m in lims])
+        out[on] = cg.run(es)
+        assert cg.path.startswith("carry"), cg.path
+        assert any(calls) == on
+    for (e1, s1), (e2, s2) in zip(out[True], out[False]):
+        assert s1 == s2
+        for key in cf.domain.keys():
+            assert torch.equal(e1.position[key].val, e2.position[key].val), key
