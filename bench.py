@@ -280,6 +280,59 @@ def cg_iteration_wall(lib, core, W, shift, bufs, k, reps=20):
     return t0.elapsed_time(t1) * 1e3 / reps
 
 
+def lazy_spec(core, k, n, dtype, nreset=20):
+    """the deferred-iterate buffers of FusedCGBatch's count-only chunks
+    (fused_cg.LAZY) for the probe's carried iteration, or None where the
+    timed loop does not defer x"""
+    from nifty_amd.minimization import fused_cg
+    it = _CARRY_CACHE.get((id(core), k, n))
+    if not (fused_cg.LAZY and it is not None and it.na and getattr(core, "lazy_ok", lambda k: False)(k)):
+        return None
+    ring = torch.empty((nreset, k, n), dtype=dtype, device=core.device)
+    alpha = torch.empty((k, nreset), dtype=torch.float64, device=core.device)
+    return dict(ring=ring[0, 0, it.g0:], sstride=k * n, alpha=alpha, nslot=nreset, buf=ring, g0=it.g0,
+                ng=core.grid_size())
+
+
+def cg_iteration_lazy_wall(lib, core, W, shift, bufs, k, lz, m=19):
+    """Wall time per iteration of a count-only chunk as FusedCGBatch runs it
+    with the deferred iterate: m replays of the captured iteration body
+    (directions into ring slots, x untouched) and the flush that brings x up
+    to date, between two events, divided by m (nreset = 20: chunks of 19)."""
+    from nifty_amd import _native
+    from nifty_amd.minimization import fused_cg
+    X, R, D, Q, SC, ws = bufs
+    n = X.shape[1]
+    it = _CARRY_CACHE[(id(core), k, n)]
+    SC0 = SC.clone()
+
+    def body():
+        it(X, R, D, Q, SC, lz)
+
+    def flush(steps):
+        g0 = lz["g0"]
+        _native.cg_lazy_flush(X[0, g0:], D[0, g0:], lz["ring"], lz["sstride"], lz["alpha"], lz["nslot"], steps,
+                              lz["ng"], n, k)
+    SC[:, _native.CG_LAZY] = 0.0
+    body()
+    flush(1)
+    torch.cuda.synchronize()
+    g = fused_cg._capture(body)
+    SC[:, _native.CG_LAZY] = 0.0
+    torch.cuda.synchronize()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(m):
+        g.replay()
+    flush(m)
+    t1.record()
+    torch.cuda.synchronize()
+    if float(SC[:, _native.CG_DONE].abs().sum()) != 0.0:
+        raise RuntimeError("cg_iteration_lazy_wall: a right-hand side froze during the replays")
+    SC.copy_(SC0)
+    return t0.elapsed_time(t1) * 1e3 / m
+
+
 def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False, s=8):
     """Algorithmic bytes per launch (every operand array counted once per
     launch; arrays shared by the k right-hand sides -- amplitude, xi0, pindex,
@@ -401,13 +454,25 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
         tot_us += tot * 1e3 / reps
         tot_b += (by or 0) * (cnt // reps)
     wall_us = cg_iteration_wall(lib, core, W, shift, bufs, k)
+    timing = "HIP graph replay of the iteration body"
+    eager_x_us = None
+    lz = lazy_spec(core, k, n_lat, X.dtype)
+    if lz is not None:
+        # the timed loop's count-only chunks defer x (fused_cg.LAZY): their
+        # per-iteration time, flush included
+        eager_x_us = wall_us
+        wall_us = cg_iteration_lazy_wall(lib, core, W, shift, bufs, k, lz)
+        timing = ("HIP graph replay of a 19-iteration count-only chunk with the deferred iterate and its flush "
+                  "(as the timed loop runs it), per iteration")
     # the per-launch byte model of the kernel table (every operand array once
     # per launch), over the same iteration time -- a bandwidth, not a second
     # roofline fraction: the line's fraction is roofline.frac (SURVEY §8(d)
     # bytes) beside roofline.traffic_frac (PMC bytes)
-    it = {"rhs": k, "us_per_iteration": round(wall_us, 1), "timing": "HIP graph replay of the iteration body",
+    it = {"rhs": k, "us_per_iteration": round(wall_us, 1), "timing": timing,
           "us_sum_of_launches": round(tot_us, 1), "launch_model_bytes": tot_b,
           "launch_model_gbs": round(tot_b / (wall_us * 1e-6) / 1e9, 1)}
+    if eager_x_us is not None:
+        it["us_per_iteration_x_every_step"] = round(eager_x_us, 1)
     return out, it
 
 

@@ -73,6 +73,9 @@ extern "C" {
                        * steps between reads) */
 #define NFT_CG_AUTO 10 /* set by the host while it queues several steps: a zero, negative or
                         * NaN new gamma freezes the RHS too (DONE = 2; the guard always does) */
+#define NFT_CG_LAZY 11 /* deferred-iterate CG (nft_hartley_fuse.lazy_*): the ring slot of this
+                        * step's previous direction; set by the host, advanced by the
+                        * carried iteration's finalize */
 #define NFT_CG_NSCALARS 16
 
 
@@ -309,6 +312,23 @@ typedef struct nft_hartley_fuse {
   double* quad_part;
   int64_t quad_pstride;
   int32_t quad_blk0, quad_pad;
+  /* deferred iterate of the carried CG (lazy_ring != NULL; the row-staged
+   * prologue's direction and the CG epilogue, count-only solves): step s =
+   * dir_sc / cg_sc[b * NFT_CG_NSCALARS + NFT_CG_LAZY] of item b reads its
+   * previous direction from ring slot s (slot 0: pro_x itself) and the
+   * prologue writes the new one to slot s + 1, at lazy_ring + s *
+   * lazy_sstride (rows x_bstride / cg_stride apart, as pro_x / cg_d), also
+   * for a stopped item (its direction copied); the CG epilogue reads d from
+   * that slot, leaves x as it is (x.r partial 0) and records the step's
+   * alpha (NaN where the guards leave x unchanged) at lazy_alpha[b *
+   * lazy_nslot + s].  nft_cg_lazy_flush then applies the recorded steps to x
+   * in order -- bitwise the per-step update -- and copies the last
+   * direction back: per step one 8-byte read of d in place of x's 16-byte
+   * read and write. */
+  void* lazy_ring;
+  int64_t lazy_sstride;
+  double* lazy_alpha;
+  int64_t lazy_nslot;
 } nft_hartley_fuse;
 
 /* Partial blocks per item of the CG-carrying epilogue for a batched
@@ -447,6 +467,13 @@ int nft_cg_direction_dd2_batched(void* d, const void* r, int64_t n1, int64_t o2,
                                  int64_t pstride, hipStream_t stream);
 int nft_fold_partials(const double* part, int nb, int nrhs, double* out, int64_t out_stride,
                       hipStream_t stream);
+/* The deferred iterate's flush (nft_hartley_fuse.lazy_*): for every row b <
+ * nrhs and element i < n, x[b * vstride + i] -= alpha_t d_t[b * vstride + i]
+ * for the recorded steps t < nsteps in order (alpha_t = alpha[b * nslot + t],
+ * skipped when NaN; d_t = ring slot t + 1 at ring + t * sstride), then d[b *
+ * vstride + i] = slot nsteps (the current direction back in place). */
+int nft_cg_lazy_flush(void* x, void* d, const void* ring, int64_t sstride, const double* alpha, int64_t nslot,
+                      int nsteps, int64_t n, int64_t vstride, int nrhs, int dtype, hipStream_t stream);
 /* nft_los_adjoint_batched and nft_fold_partials(fold_part, fold_nb,
  * fold_nrhs, fold_out, fold_ostride) in ONE launch (the fold runs as the first
  * fold_nrhs workgroups of the adjoint's grid, bitwise the separate call): the

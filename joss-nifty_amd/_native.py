@@ -65,6 +65,7 @@ SIGNATURES = {
     "nft_cg_dd_blocks": (_i, [_i64]),
     "nft_cg_direction_dd_batched": (_i, [_p, _p, _i64, _i64, _i, _i, _p, _d, _p, _i64, _p]),
     "nft_fold_partials": (_i, [_p, _i, _i, _p, _i64, _p]),
+    "nft_cg_lazy_flush": (_i, [_p, _p, _p, _i64, _p, _i64, _i, _i64, _i64, _i, _i, _p]),
     "nft_prof_begin": (_i, [_i]),
     "nft_prof_end": (_i, [_p, _p, _i, ctypes.POINTER(_i)]),
     "nft_prof_label": (ctypes.c_char_p, [_i]),
@@ -108,7 +109,8 @@ class HartleyFuse(ctypes.Structure):
                [(n, _p) for n in ("dir_r", "dir_sc", "dir_part")] + \
                [("dir_pstride", _i64), ("dir_shift", _d), ("dir_blk0", ctypes.c_int32), ("dir_pad", ctypes.c_int32)] + \
                [("epi_out2_pairs", _i64)] + \
-               [("quad_part", _p), ("quad_pstride", _i64), ("quad_blk0", ctypes.c_int32), ("quad_pad", ctypes.c_int32)]
+               [("quad_part", _p), ("quad_pstride", _i64), ("quad_blk0", ctypes.c_int32), ("quad_pad", ctypes.c_int32)] + \
+               [("lazy_ring", _p), ("lazy_sstride", _i64), ("lazy_alpha", _p), ("lazy_nslot", _i64)]
 
 
 class LosPlan(ctypes.Structure):
@@ -141,7 +143,7 @@ class AmpOut(ctypes.Structure):
     _fields_ = [(n, _p) for n in ("fl", "sl", "flex", "asp", "zm", "spec",
                                   "dfl", "dsl", "dflex", "dasp", "dzm", "dspec")] + [("shift", _d)]
 
-CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD, CG_DONE, CG_ITER, CG_AUTO = range(11)
+CG_GAMMA, CG_GPREV, CG_CURV, CG_ALPHA, CG_XR, CG_XB, CG_FLAG, CG_DD, CG_DONE, CG_ITER, CG_AUTO, CG_LAZY = range(12)
 CG_NSCALARS = 16
 AMP2_FALLBACK = 1  # NFT_AMP2_FALLBACK
 
@@ -418,6 +420,26 @@ def hartley_dir_blocks(grid):
     return int(load().nft_hartley_dir_blocks(len(grid), sh))
 
 
+def _set_lazy(f, lz):
+    """nft_hartley_fuse.lazy_*: lz = dict(ring=base of slot 1 (a tensor view
+    laid out like the direction), sstride=elements between slots,
+    alpha=(k, nslot) fp64 rows, nslot=)"""
+    ring, al = lz["ring"], lz["alpha"]
+    if not (ring.is_cuda and al.is_cuda and al.dtype == torch.float64):
+        raise NativeError("lazy iterate: device ring and fp64 device alphas")
+    f.lazy_ring = ring.data_ptr()
+    f.lazy_sstride = int(lz["sstride"])
+    f.lazy_alpha = al.data_ptr()
+    f.lazy_nslot = int(lz["nslot"])
+
+
+def cg_lazy_flush(x, d, ring, sstride, alpha, nslot, nsteps, n, vstride, k):
+    """nft_cg_lazy_flush on the grid segment views x / d / ring (rows vstride
+    apart, ring slot 1 at `ring`)"""
+    _check(load().nft_cg_lazy_flush(ptr(x), ptr(d), ptr(ring), int(sstride), ptr(alpha), int(nslot), int(nsteps),
+                                    int(n), int(vstride), int(k), dtype_code(x.dtype), stream_ptr()))
+
+
 def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None, cg=None,
                   quad=None):
     """out = epilogue(scale * Hartley(prologue)) with
@@ -454,6 +476,8 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
             f.dir_pstride = int(dr["pstride"])
             f.dir_shift = float(dr["shift"])
             f.dir_blk0 = int(dr["blk0"])
+            if dr.get("lazy"):
+                _set_lazy(f, dr["lazy"])
     if epi:
         for k, fld in (("a", "epi_a"), ("d", "epi_d"), ("b", "epi_b"), ("out2", "epi_out2")):
             v = epi.get(k)
@@ -473,6 +497,8 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
         f.cg_shift = float(cg["shift"])
         f.cg_nbtot = int(cg["nbtot"])
         f.cg_blk0 = int(cg["blk0"])
+        if cg.get("lazy"):
+            _set_lazy(f, cg["lazy"])
     if quad:
         # per-tile partials of h * (epi_a * h) (nft_hartley_fuse.quad_*)
         qp = quad["part"]

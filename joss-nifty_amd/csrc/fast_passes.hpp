@@ -68,6 +68,13 @@ struct FuseArgs {
   double* qpart;
   long long qps;
   int qblk0;
+  // deferred iterate (nft_hartley_fuse.lazy_*): direction ring slots 1.. at
+  // lring + (s - 1) * lss, alphas at lalpha[item * lnslot + s]
+  int lazy;
+  void* lring;
+  long long lss;
+  double* lalpha;
+  long long lnslot;
 };
 
 // element index into pc of item-element j: its bin (pidx[j]) or, folded, the
@@ -558,9 +565,15 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         // (same arrays, runtime offsets), which serialised one memory
         // round trip per element
         constexpr int CG_CH = CG_CH_VALUES;
+        // deferred iterate (nft_hartley_fuse.lazy_*): d from the ring slot this
+        // step's prologue wrote, x untouched, the step's alpha recorded
+        const bool lazy = a.f.lazy != 0;
+        const long long sl = lazy ? (long long)scb[NFT_CG_LAZY] : 0;
+        if (lazy && tid == 0 && t - item * a.f.ctr == 0)
+          a.f.lalpha[item * a.f.lnslot + sl] = ok ? alpha : __builtin_nan("");
         const T* __restrict__ ea = (const T*)a.f.ea;
         const T* __restrict__ eb = (const T*)a.f.eb;
-        const T* __restrict__ cd = (const T*)a.f.cd;
+        const T* __restrict__ cd = lazy ? (const T*)a.f.lring + sl * a.f.lss : (const T*)a.f.cd;
         T* __restrict__ cx = (T*)a.f.cx;
         T* __restrict__ cr = (T*)a.f.cr;
 #pragma unroll
@@ -590,7 +603,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
               ev[c][h] = b * a.f.cst + j;
               xv[c][h] = rv_[c][h] = dv[c][h] = qv[c][h] = wv[c][h] = (T)0;
               if (use[c][h]) {
-                xv[c][h] = cx[ev[c][h]];
+                if (!lazy) xv[c][h] = cx[ev[c][h]];
                 rv_[c][h] = cr[ev[c][h]];
                 if (ok) dv[c][h] = cd[ev[c][h]];
                 qv[c][h] = ea ? ea[b * a.f.sea + j] : (T)1;
@@ -610,11 +623,11 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
                 const T di = dv[c][h];
                 xi = xi - al * di;
                 ri = ri - al * (q + shift * di);
-                cx[ev[c][h]] = xi;
+                if (!lazy) cx[ev[c][h]] = xi;
                 cr[ev[c][h]] = ri;
               }
               rr += (double)ri * (double)ri;
-              xr += (double)xi * (double)ri;
+              if (!lazy) xr += (double)xi * (double)ri;
               if (a.f.out2 && !a.f.o2h) ((T*)a.f.out2)[bv[c][h] * a.f.s2 + jv[c][h]] = wv[c][h] * hv[c][h];
             }
             if (a.f.o2h && use[c][0]) {

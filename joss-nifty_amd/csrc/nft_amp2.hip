@@ -1129,6 +1129,7 @@ __device__ __forceinline__ void fin_rhs(const Vjp2Args<VT>& a, int r, double* sh
     btot<2>(f, sh);
     if (tid == 0) {
       double* scb = a.sc + (long long)r * NS_;
+      scb[NFT_CG_LAZY] += 1.0;  // the deferred iterate's ring slot (every step, stopped or not)
       if (scb[NFT_CG_DONE] == 0.0) {
         const double curv = scb[NFT_CG_CURV], gprev = scb[NFT_CG_GAMMA];
         const double alpha = gprev / curv;

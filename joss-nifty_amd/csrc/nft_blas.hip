@@ -423,6 +423,33 @@ __global__ __launch_bounds__(1024) void fold_wide(const double* __restrict__ par
   }
 }
 
+// the deferred iterate's flush (nft_cg_lazy_flush): per element the recorded
+// steps in order, each the CG epilogue's x - alpha d
+template <typename T>
+__global__ __launch_bounds__(256) void lazy_flush_kernel(T* __restrict__ x, T* __restrict__ d,
+                                                         const T* __restrict__ ring, long long ss,
+                                                         const double* __restrict__ alpha, long long nslot, int m,
+                                                         long long n, long long vs) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int b = (int)blockIdx.y;
+  if (i >= n) return;
+  const long long e = (long long)b * vs + i;
+  const double* al = alpha + (long long)b * nslot;
+  T xi = x[e];
+  T dl = d[e];
+  for (int t = 0; t < m; ++t) {
+    const double a = al[t];
+    const T di = ring[(long long)t * ss + e];
+    if (a == a) {
+      const T at = (T)a;
+      xi = xi - at * di;
+    }
+    dl = di;
+  }
+  x[e] = xi;
+  d[e] = dl;
+}
+
 }  // namespace nft
 
 using namespace nft;
@@ -670,6 +697,28 @@ int nft_cg_direction_dd2_batched(void* d, const void* r, int64_t n1, int64_t o2,
     set_last_error("nft_cg_direction_dd2: bad dtype %d", dtype);
     return NFT_ERR_ARG;
   }
+  NFT_HIP_CHECK(hipGetLastError());
+  return NFT_OK;
+}
+
+int nft_cg_lazy_flush(void* x, void* d, const void* ring, int64_t sstride, const double* alpha, int64_t nslot,
+                      int nsteps, int64_t n, int64_t vstride, int nrhs, int dtype, hipStream_t stream) {
+  if (!x || !d || !ring || !alpha || nsteps < 0 || nsteps > nslot || n < 0 || vstride < n || nrhs < 1 ||
+      nrhs > 65535 || sstride < (int64_t)nrhs * vstride || (dtype != 0 && dtype != 1)) {
+    set_last_error("nft_cg_lazy_flush: bad arguments");
+    return NFT_ERR_ARG;
+  }
+  if (n == 0 || nsteps == 0) return NFT_OK;
+  const dim3 grid((unsigned)((n + 255) / 256), (unsigned)nrhs);
+  prof_mark(stream, "cg_lazy_flush");
+  if (dtype == 0)
+    hipLaunchKernelGGL(lazy_flush_kernel<double>, grid, dim3(256), 0, stream, (double*)x, (double*)d,
+                       (const double*)ring, (long long)sstride, alpha, (long long)nslot, nsteps, (long long)n,
+                       (long long)vstride);
+  else
+    hipLaunchKernelGGL(lazy_flush_kernel<float>, grid, dim3(256), 0, stream, (float*)x, (float*)d,
+                       (const float*)ring, (long long)sstride, alpha, (long long)nslot, nsteps, (long long)n,
+                       (long long)vstride);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

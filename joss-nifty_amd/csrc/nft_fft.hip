@@ -940,6 +940,21 @@ __global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __re
   const bool dirc = f.dr != nullptr;
   T* pd = const_cast<T*>(px);
   const T* __restrict__ pr = (const T*)f.dr;
+  // deferred iterate: item b's previous direction in ring slot s (0: px), the
+  // new one into slot s + 1
+  const bool lazy = dirc && f.lazy;
+  const T* pxs[NBM];
+  T* pds[NBM];
+#pragma unroll
+  for (int b = 0; b < NBM; ++b) {
+    pxs[b] = px;
+    pds[b] = pd;
+    if (lazy && b < nb) {
+      const long long sl = (long long)f.dsc[b * NFT_CG_NSCALARS + NFT_CG_LAZY];
+      pxs[b] = sl == 0 ? px : (const T*)f.lring + (sl - 1) * f.lss;
+      pds[b] = (T*)f.lring + sl * f.lss;
+    }
+  }
   T bt[NBM];
   bool live[NBM];
   double dd[NBM];
@@ -1043,7 +1058,7 @@ __global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __re
         for (int b = 0; b < NBM; ++b) {
           xv[i][b] = rv[i][b] = (T)0;
           if (ok[i] && b < nb) {
-            xv[i][b] = px[b * f.sx + j];
+            xv[i][b] = pxs[b][b * f.sx + j];
             if (dirc && live[b]) rv[i][b] = pr[b * f.sx + j];
           }
         }
@@ -1060,8 +1075,10 @@ __global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __re
           T v = xv[i][b];
           if (dirc && live[b]) {
             v = bt[b] * v + rv[i][b];
-            pd[b * f.sx + j] = v;
+            pds[b][b * f.sx + j] = v;
             dd[b] += (double)v * (double)v;
+          } else if (lazy) {
+            pds[b][b * f.sx + j] = v;  // a stopped item's direction carried to the next slot
           }
           if (pa) v *= av[i][PI ? b : 0];
           v += bv[i][PI ? b : 0] * cvs[c1 * NBM + b];
@@ -1192,6 +1209,10 @@ static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out
       prof_mark(s, f.dr ? "pro_fold+dir" : "pro_fold");
       const bool rows = pro_rows_ok(f.fnd, f.fn[f.fnd - 1]) && f.nb <= 8;
       const bool pi = f.sa != 0 || f.sb != 0;
+      if (f.lazy && f.dr && !(rows && f.fnd >= 2)) {
+        set_last_error("nft_hartley_fused: the deferred iterate needs the row-staged prologue");
+        return NFT_ERR_UNSUPPORTED;
+      }
       int pst = NFT_OK;
       if (rows && f.fnd == 2)
         pst = pi ? launch_pro_rows<T, 2, true>(f, u, s) : launch_pro_rows<T, 2, false>(f, u, s);
@@ -1471,6 +1492,19 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
       f.qpart = fz->quad_part;
       f.qps = fz->quad_pstride;
       f.qblk0 = fz->quad_blk0;
+    }
+    f.lazy = 0;
+    if (fz->lazy_ring) {
+      if (!fz->lazy_alpha || fz->lazy_nslot < 1 || fz->lazy_sstride < 1 || !(f.dr || f.cg)) {
+        set_last_error("nft_hartley_fused: the deferred iterate needs its alphas, slots and the carried "
+                       "direction or CG epilogue");
+        return NFT_ERR_ARG;
+      }
+      f.lazy = 1;
+      f.lring = fz->lazy_ring;
+      f.lss = fz->lazy_sstride;
+      f.lalpha = fz->lazy_alpha;
+      f.lnslot = fz->lazy_nslot;
     }
   }
   const int sigma = convention == 0 ? 1 : -1;

@@ -228,7 +228,7 @@ int pro_r2c_try(const fast::FuseArgs& f, int dtype, int nd, const long long* sha
                 void* ws, size_t hws, hipStream_t s, bool* done) {
   *done = false;
   const int mode = pro_r2c_mode();
-  if (mode == 0 || !f.dr || f.fnd != 2 || f.sa != 0 || f.sb != 0 || !f.pb || !f.pidx || f.nb < 1)
+  if (mode == 0 || !f.dr || f.lazy || f.fnd != 2 || f.sa != 0 || f.sb != 0 || !f.pb || !f.pidx || f.nb < 1)
     return NFT_OK;
   if (nd != 3 || naxes != 2 || ax[0] != 1 || ax[1] != 2 || shape[0] != f.nb) return NFT_OK;
   const long long n0 = shape[1], n1 = shape[2];

@@ -303,6 +303,11 @@ _SEG2 = os.environ.get("NFT_CG_SEG2", "1") != "0"
 # with the VJP in the two-phase amplitude kernels (NFT_CG_AMP2=0: the
 # separate direction / update / finalize launches)
 _AMP2 = os.environ.get("NFT_CG_AMP2", "1") != "0"
+# deferred iterate inside queued chunks of count-only solves
+# (nft_hartley_fuse.lazy_*): the grid segment's directions go to ring slots,
+# x is brought up to date once per chunk (nft_cg_lazy_flush, bitwise the
+# per-step update); NFT_CG_LAZY=0: x updated every step
+LAZY = os.environ.get("NFT_CG_LAZY", "1") != "0"
 
 
 class _CarryIteration:
@@ -372,12 +377,13 @@ class _CarryIteration:
         return (dtype == torch.float32 and _AMP2 and _CARRY_DIR and hasattr(core, "amp2_tiles")
                 and core.amp2_tiles(k) > 0 and hasattr(core, "dir_blocks") and core.dir_blocks(k) > 0)
 
-    def _call_amp2(self, X, Rr, D, Q, SC):
+    def _call_amp2(self, X, Rr, D, Q, SC, lazy=None):
         core, lib = self.core, self.lib
         n, k, g0 = self.n, self.k, self.g0
         pstride = self.nbd + self.nq
         da = core.mv_amp_jvp_dir(D, Rr, SC, self.PQ, pstride, self.shift)
-        pro_dir = dict(r=Rr[0, g0:], sc=SC, part=self.PQ, pstride=pstride, shift=self.shift, blk0=self.pro_blk0)
+        pro_dir = dict(r=Rr[0, g0:], sc=SC, part=self.PQ, pstride=pstride, shift=self.shift, blk0=self.pro_blk0,
+                       lazy=lazy)
 
         def fold():
             _native._check(lib.nft_fold_partials(_native.ptr(self.PQ), pstride, k,
@@ -386,15 +392,17 @@ class _CarryIteration:
         # the same call as arguments, for a W that carries it in its own launch
         fold.spec = (self.PQ, pstride, k, SC.data_ptr() + _native.CG_CURV * 8, _native.CG_NSCALARS)
         cg = dict(x=X[0, g0:], r=Rr[0, g0:], d=D[0, g0:], sc=SC, part=self.GP, stride=n, shift=self.shift,
-                  nbtot=self.tiles, blk0=0)
+                  nbtot=self.tiles, blk0=0, lazy=lazy)
         w = core.mv_grid(D, da, Q, self.W, 0.0, qpart=self.PQ[:, self.nbd:], after_w=fold, cg=cg,
                          pro_dir=pro_dir)
         core.mv_amp_vjp_cg(X, Rr, D, w, SC, self.UP, 2 * self.na, self.GP, 3 * self.tiles, self.tiles, self.tiles,
                            self.shift)
 
-    def __call__(self, X, Rr, D, Q, SC):
+    def __call__(self, X, Rr, D, Q, SC, lazy=None):
         if self.na:
-            return self._call_amp2(X, Rr, D, Q, SC)
+            return self._call_amp2(X, Rr, D, Q, SC, lazy)
+        if lazy is not None:
+            raise RuntimeError("the deferred iterate needs the two-phase amplitude kernels")
         core, lib = self.core, self.lib
         P = _native.ptr
         s_ = _native.stream_ptr()
@@ -581,6 +589,19 @@ class FusedCGBatch(FusedCG):
                 st["PQ"] = torch.empty((k, st["nbd"] + nq), dtype=torch.float64, device=dev)
                 if carry:
                     st["split"] = _CarryIteration(lib, core, self.W, n, k, nq, sh)
+            # the deferred iterate: count-only chunks of the carried iteration
+            # with the two-phase amplitude kernels (nothing reads x.r or x
+            # between the chunk's host reads)
+            st["lazy"] = None
+            spl = st["split"]
+            if (LAZY and chunkable0 and HIST is None and not need_value and isinstance(spl, _CarryIteration)
+                    and spl.na and getattr(core, "lazy_ok", lambda k: False)(k)):
+                g0 = spl.g0
+                ring = torch.empty((self.nreset, k, n), dtype=X.dtype, device=dev)
+                alpha = torch.empty((k, self.nreset), dtype=torch.float64, device=dev)
+                st["lazy"] = dict(ring=ring[0, 0, g0:], sstride=k * n, alpha=alpha, nslot=self.nreset,
+                                  buf=ring, g0=g0, ng=core.grid_size())
+        chunkable0 = CHUNK and all(_count_silent(self.controllers[j]) for j in active)
         setup(k0)
 
         def record():
@@ -595,7 +616,7 @@ class FusedCGBatch(FusedCG):
             cur = HIST[rows, idx]
             HIST[rows, idx] = torch.where(live, SC.index_select(1, hsel), cur)
 
-        def body(with_dir):
+        def body(with_dir, lazy=False):
             s_ = _native.stream_ptr()
             k = X.shape[0]
             split, Q, Bu = st["split"], st["Q"], st["Bu"]
@@ -604,7 +625,7 @@ class FusedCGBatch(FusedCG):
                 # it streams b for x.b
                 Bu = Bv
             if with_dir and isinstance(split, _CarryIteration):
-                split(X, Rr, D, Q, SC)
+                split(X, Rr, D, Q, SC, st["lazy"] if lazy else None)
                 if st["xbdot"]:
                     chk(lib.nft_dot_batched(P(X), P(Bv), n, n, k, dt, P(SC[:, _native.CG_XB:]), NS, P(ws), s_))
                 record()
@@ -626,7 +647,7 @@ class FusedCGBatch(FusedCG):
 
         def compact():
             """restrict the buffers, the scalars and the metric to the live RHS"""
-            nonlocal X, Rr, Bv, D, SC, host, core, rows, pos, graph, eager, iter_seen, HIST
+            nonlocal X, Rr, Bv, D, SC, host, core, rows, pos, graph, lgraph, eager, iter_seen, HIST
             keep = sorted(pos[j] for j in active)
             if X is not full_X:
                 idx = torch.tensor(rows, device=dev)
@@ -650,12 +671,14 @@ class FusedCGBatch(FusedCG):
             # one eager iteration warms the new batch size's caches, then the
             # loop body is captured again
             graph = None
+            lgraph = None
             eager = 1
 
         # a core without `subset` applies one metric to every row; a per-RHS
         # metric compacts only if it can restrict itself (subset not None)
         can_compact = COMPACT and getattr(core, "subset", _shared) is not None
         graph = None
+        lgraph = None
         eager = 0
         ii = 0
         first = True
@@ -678,7 +701,21 @@ class FusedCGBatch(FusedCG):
                 m = min(min(self.controllers[j]._iteration_limit - self.controllers[j]._itcount for j in active),
                         self.nreset - 1 - ii)
                 if m > 1:
-                    iter_seen = self._chunk(graph, m, SC, host, iter_seen, active, finish, pos, HIST)
+                    lz = st["lazy"]
+                    if lz is not None:
+                        # the chunk with the deferred iterate: ring slots from 0,
+                        # x brought up to date before the host read
+                        if lgraph is None:
+                            lgraph = _capture(lambda: body(True, lazy=True))
+                        SC[:, _native.CG_LAZY] = 0.0
+
+                        def flush(m=m, lz=lz):
+                            g0 = lz["g0"]
+                            _native.cg_lazy_flush(X[0, g0:], D[0, g0:], lz["ring"], lz["sstride"], lz["alpha"],
+                                                  lz["nslot"], m, lz["ng"], n, X.shape[0])
+                        iter_seen = self._chunk(lgraph, m, SC, host, iter_seen, active, finish, pos, HIST, flush)
+                    else:
+                        iter_seen = self._chunk(graph, m, SC, host, iter_seen, active, finish, pos, HIST)
                     STATS["chunks"] += 1
                     STATS["chunk_iters"] += m
                     if isinstance(st["split"], _CarryIteration):
@@ -796,7 +833,7 @@ class FusedCGBatch(FusedCG):
             full_Rr.index_copy_(0, idx, Rr)
         return full_X, results
 
-    def _chunk(self, graph, m, SC, host, iter_seen, active, finish, pos, HIST=None):
+    def _chunk(self, graph, m, SC, host, iter_seen, active, finish, pos, HIST=None, flush=None):
         """m queued iterations (graph replays) and one host read.  A terminal
         step (guard tripped, gamma zero / negative / NaN) freezes its RHS on
         the device (NFT_CG_DONE = 2, with NFT_CG_AUTO set); every RHS's
@@ -806,6 +843,8 @@ class FusedCGBatch(FusedCG):
         SC[:, NS.CG_AUTO] = 1.0
         for _ in range(m):
             graph.replay()
+        if flush is not None:
+            flush()
         SC[:, NS.CG_AUTO] = 0.0
         self.niter += m
         host.copy_(SC, non_blocking=True)

@@ -145,3 +145,39 @@ def test_fold_in_los_adjoint_bitwise(ift, monkeypatch):
         assert s1 == s2
         for key in cf.domain.keys():
             assert torch.equal(e1.position[key].val, e2.position[key].val), key
+
+
+@pytest.mark.parametrize("which", ["los", "gauss"])
+def test_lazy_iterate_bitwise(ift, which, monkeypatch):
+    """the deferred iterate of count-only chunks (directions in ring slots, x
+    brought up to date once per chunk, nft_cg_lazy_flush) gives bitwise the
+    per-step update -- across the residual refreshes and a compaction"""
+    from nifty_amd import _native
+    from nifty_amd.minimization import fused_cg
+    # these small 2-D grids take the fused prologue + R2C pass, which keeps
+    # its direction in place: the row-staged prologue here
+    monkeypatch.setenv("NFT_PRO_R2C", "0")
+    cf, A, (core, W, shift) = _metric(ift, which)
+    es = _energies(ift, cf, A, 4, 9)
+    lims = [7, 13, 30, 45]
+    flushes = []
+    orig = _native.cg_lazy_flush
+
+    def spy(*a, **kw):
+        flushes.append(a[6])
+        return orig(*a, **kw)
+    monkeypatch.setattr(_native, "cg_lazy_flush", spy)
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(fused_cg, "LAZY", on)
+        flushes.clear()
+        cg = fused_cg.FusedCGBatch(core, W, shift, [ift.GradientNormController(iteration_limit=m) for m in lims])
+        out[on] = cg.run(es)
+        assert cg.path == "carry+chunk", cg.path
+        assert bool(flushes) == on
+        if on:
+            assert cg.compactions >= 1 and sum(flushes) >= 30
+    for (e1, s1), (e2, s2) in zip(out[True], out[False]):
+        assert s1 == s2
+        for key in cf.domain.keys():
+            assert torch.equal(e1.position[key].val, e2.position[key].val), key
