@@ -294,7 +294,24 @@ def lazy_spec(core, k, n, dtype, nreset=20):
                 ng=core.grid_size())
 
 
-def cg_iteration_lazy_wall(lib, core, W, shift, bufs, k, lz, m=19):
+LAZY_CHUNK = 19   # count-only chunk length between residual refreshes (nreset 20)
+
+
+def lazy_chunk(lib, core, W, shift, bufs, k, lz, m):
+    """m eager steps of the carried iteration with the deferred iterate from
+    ring slot 0, then the flush (the chunk of the timed loop, uncaptured)"""
+    from nifty_amd import _native
+    X, R, D, Q, SC, ws = bufs
+    n = X.shape[1]
+    it = _CARRY_CACHE[(id(core), k, n)]
+    SC[:, _native.CG_LAZY] = 0.0
+    for _ in range(m):
+        it(X, R, D, Q, SC, lz)
+    g0 = lz["g0"]
+    _native.cg_lazy_flush(X[0, g0:], D[0, g0:], lz["ring"], lz["sstride"], lz["alpha"], lz["nslot"], m, lz["ng"], n, k)
+
+
+def cg_iteration_lazy_wall(lib, core, W, shift, bufs, k, lz, m=LAZY_CHUNK):
     """Wall time per iteration of a count-only chunk as FusedCGBatch runs it
     with the deferred iterate: m replays of the captured iteration body
     (directions into ring slots, x untouched) and the flush that brings x up
@@ -333,7 +350,7 @@ def cg_iteration_lazy_wall(lib, core, W, shift, bufs, k, lz, m=19):
     return t0.elapsed_time(t1) * 1e3 / m
 
 
-def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False, s=8):
+def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False, s=8, lazy_m=0):
     """Algorithmic bytes per launch (every operand array counted once per
     launch; arrays shared by the k right-hand sides -- amplitude, xi0, pindex,
     the LOS matrix and its scales -- once).  s: bytes per value of the CG
@@ -399,8 +416,13 @@ def byte_model(cf, R, k, n_lat, dir_carried=False, pairs=False, s=8):
         "cg_update_seg2": 6 * s * k * (n_lat - N),
         "cg_dir_dd2": 3 * s * k * (n_lat - N),
         # unpack + the grid segment's CG update: half spectrum (k), A, xi0;
-        # x, r, d in (k), x, r and w = xi0*v out (k) -- q is not stored
-        "fft_unpack+cg": 2 * s * k * Hh + 2 * s * N + 5 * s * k * N + s * k * (Hh if pairs else N),
+        # x, r, d in (k), x, r and w = xi0*v out (k) -- q is not stored;
+        # with the deferred iterate (lazy_m steps per chunk) r, d in and r
+        # out: x is left to the flush
+        "fft_unpack+cg": 2 * s * k * Hh + 2 * s * N + (3 if lazy_m else 5) * s * k * N + s * k * (Hh if pairs else N),
+        # the flush of a chunk: its lazy_m direction slots and x in, x and
+        # the last direction out (k)
+        "cg_lazy_flush": (lazy_m + 3) * s * k * N,
     }
 
 
@@ -428,12 +450,20 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
     for _ in range(3):
         cg_iteration(lib, core, W, shift, bufs, k)
     torch.cuda.synchronize()
+    lz = lazy_spec(core, k, n_lat, X.dtype)
     # keep the GPU busy while the probe launches are queued, so that the
     # events bracket kernels and not host enqueue gaps
     torch.cuda._sleep(200_000_000)
+    lazy_m = 0
     with _native.LaunchProfile() as prof:
-        for _ in range(reps):
-            cg_iteration(lib, core, W, shift, bufs, k)
+        if lz is None:
+            for _ in range(reps):
+                cg_iteration(lib, core, W, shift, bufs, k)
+        else:
+            # the timed loop's count-only chunk: 19 steps with the deferred
+            # iterate, then its flush (launches per iteration: 1 / 19 for it)
+            lazy_m = reps = LAZY_CHUNK
+            lazy_chunk(lib, core, W, shift, bufs, k, lz, lazy_m)
     acc = {}
     for lab, ms in prof.records:
         a = acc.setdefault(lab, [0, 0.0])
@@ -443,20 +473,20 @@ def kernel_probe(ift, cf, R, lh, pos, k, reps=10):
     dcar = bool(fused_cg._CARRY and fused_cg._CARRY_DIR and getattr(core, "dir_blocks", lambda k: 0)(k) > 0
                 and _CARRY_CACHE)
     model = byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(getattr(core, "_pairs", lambda k: 0)(k)),
-                       s=X.element_size())
+                       s=X.element_size(), lazy_m=lazy_m)
     out = {}
     tot_us, tot_b = 0.0, 0
     for lab, (cnt, tot) in acc.items():
         avg = tot / cnt * 1e3
         by = model.get(lab)
-        out[lab] = {"launches": cnt // reps, "avg_us": round(avg, 2), "bytes": by,
+        per = cnt // reps if cnt % reps == 0 else round(cnt / reps, 4)
+        out[lab] = {"launches": per, "avg_us": round(avg, 2), "bytes": by,
                     "gbs": round(by / (avg * 1e-6) / 1e9, 1) if by else None}
         tot_us += tot * 1e3 / reps
-        tot_b += (by or 0) * (cnt // reps)
+        tot_b += (by or 0) * per
     wall_us = cg_iteration_wall(lib, core, W, shift, bufs, k)
     timing = "HIP graph replay of the iteration body"
     eager_x_us = None
-    lz = lazy_spec(core, k, n_lat, X.dtype)
     if lz is not None:
         # the timed loop's count-only chunks defer x (fused_cg.LAZY): their
         # per-iteration time, flush included

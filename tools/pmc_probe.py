@@ -54,13 +54,24 @@ def main(config="C3", reps=3):
         _native._check(lib.nft_scale(_native.ptr(cal), cal_n, _native.dtype_code(X.dtype), 1.0000001,
                                      _native.stream_ptr()))
     torch.cuda.synchronize()
+    for _ in range(2):
+        bench.cg_iteration(lib, core, W, shift, bufs, k)
+    torch.cuda.synchronize()
+    # the timed loop's count-only chunk when it defers x (bench.lazy_spec):
+    # 19 steps and the flush, as bench.kernel_probe labels them
+    lz = bench.lazy_spec(core, k, n_lat, X.dtype)
+    lazy_m = bench.LAZY_CHUNK if lz is not None else 0
     with _native.LaunchProfile(capacity=4096) as p:
-        for _ in range(reps):
-            bench.cg_iteration(lib, core, W, shift, bufs, k)
+        if lz is None:
+            for _ in range(reps):
+                bench.cg_iteration(lib, core, W, shift, bufs, k)
+        else:
+            bench.lazy_chunk(lib, core, W, shift, bufs, k, lz, lazy_m)
     torch.cuda.synchronize()
     from nifty_amd.minimization import fused_cg
     dcar = bool(fused_cg._CARRY and fused_cg._CARRY_DIR and core.dir_blocks(k) > 0 and bench._CARRY_CACHE)
-    model = bench.byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(core._pairs(k)), s=X.element_size())
+    model = bench.byte_model(cf, R, k, n_lat, dir_carried=dcar, pairs=bool(core._pairs(k)), s=X.element_size(),
+                             lazy_m=lazy_m)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "pmc_labels.json"), "w") as f:
         json.dump({"labels": [lab for lab, _ in p.records], "calibration_bytes": X.element_size() * cal_n,

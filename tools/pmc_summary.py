@@ -65,8 +65,10 @@ def main(out_dir):
                         "traffic_bytes": round(tr), "algorithmic_bytes": alg,
                         "traffic_over_algorithmic": round(tr / alg, 3) if alg else None}
     config = meta.get("config", "C3")
+    what = ("a 19-step count-only chunk with the deferred iterate and its flush (cg_lazy_flush: launches "
+            "per iteration 1/19)" if "cg_lazy_flush" in acc else "batched CG iteration")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/pmc_probe.py, "
-                     f"batched CG iteration of the bench problem ({config}), {meta['rhs']} RHS",
+                     f"{what} of the bench problem ({config}), {meta['rhs']} RHS",
            "calibration": {"kernel": "nft::scale_kernel over 1 GiB in the run's storage type",
                            "known_bytes_each_way": known,
                            "fetch_size_bytes": round(fcal), "write_size_bytes": round(wcal),
