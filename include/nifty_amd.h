@@ -312,8 +312,9 @@ typedef struct nft_hartley_fuse {
   double* quad_part;
   int64_t quad_pstride;
   int32_t quad_blk0, quad_pad;
-  /* deferred iterate of the carried CG (lazy_ring != NULL; the row-staged
-   * prologue's direction and the CG epilogue, count-only solves): step s =
+  /* deferred iterate of the carried CG (lazy_ring != NULL; the direction of
+   * the row-staged or R2C-fused prologue and the CG epilogue, count-only
+   * solves): step s =
    * dir_sc / cg_sc[b * NFT_CG_NSCALARS + NFT_CG_LAZY] of item b reads its
    * previous direction from ring slot s (slot 0: pro_x itself) and the
    * prologue writes the new one to slot s + 1, at lazy_ring + s *

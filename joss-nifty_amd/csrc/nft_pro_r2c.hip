@@ -65,6 +65,15 @@ __global__ __launch_bounds__(N / 8) void pro_r2c_kernel(fast::FuseArgs f, const 
   const T bt = (T)beta;
   const long long jA = (long long)rowA * N, jB = (long long)rowB * N;
   const long long ib = (long long)b * f.sx, ic = (long long)b * f.sc;
+  // deferred iterate (nft_hartley_fuse.lazy_*): the previous direction from
+  // ring slot s (0: px), the new one (a stopped item's copied) into slot s + 1
+  const T* pxs = px;
+  T* pds = pd;
+  if (f.lazy) {
+    const long long sl = (long long)scb[NFT_CG_LAZY];
+    pxs = sl == 0 ? px : (const T*)f.lring + (sl - 1) * f.lss;
+    pds = (T*)f.lring + sl * f.lss;
+  }
   double dA = 0.0;
   T vbk[VP];  // d of row B, summed after every position of row A
   // two halves of the thread's positions, each with every load of both rows
@@ -77,8 +86,8 @@ __global__ __launch_bounds__(N / 8) void pro_r2c_kernel(fast::FuseArgs f, const 
     for (int i = 0; i < HV; ++i) {
       const int p = tid + (h * HV + i) * NT;
       const int c1 = p == 0 ? 0 : (p <= N - p ? p : N - p);
-      xa[i] = px[ib + jA + p];
-      xb[i] = px[ib + jB + p];
+      xa[i] = pxs[ib + jA + p];
+      xb[i] = pxs[ib + jB + p];
       ra[i] = rb[i] = (T)0;
       if (live) {
         ra[i] = pr[ib + jA + p];
@@ -101,9 +110,12 @@ __global__ __launch_bounds__(N / 8) void pro_r2c_kernel(fast::FuseArgs f, const 
       if (live) {
         va = bt * va + ra[i];
         vb = bt * vb + rb[i];
-        pd[ib + jA + p] = va;
-        pd[ib + jB + p] = vb;
+        pds[ib + jA + p] = va;
+        pds[ib + jB + p] = vb;
         dA += (double)va * (double)va;
+      } else if (f.lazy) {
+        pds[ib + jA + p] = va;
+        pds[ib + jB + p] = vb;
       }
       vbk[h * HV + i] = vb;
       if (pa) {
@@ -228,7 +240,7 @@ int pro_r2c_try(const fast::FuseArgs& f, int dtype, int nd, const long long* sha
                 void* ws, size_t hws, hipStream_t s, bool* done) {
   *done = false;
   const int mode = pro_r2c_mode();
-  if (mode == 0 || !f.dr || f.lazy || f.fnd != 2 || f.sa != 0 || f.sb != 0 || !f.pb || !f.pidx || f.nb < 1)
+  if (mode == 0 || !f.dr || f.fnd != 2 || f.sa != 0 || f.sb != 0 || !f.pb || !f.pidx || f.nb < 1)
     return NFT_OK;
   if (nd != 3 || naxes != 2 || ax[0] != 1 || ax[1] != 2 || shape[0] != f.nb) return NFT_OK;
   const long long n0 = shape[1], n1 = shape[2];

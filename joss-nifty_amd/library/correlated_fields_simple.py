@@ -817,10 +817,7 @@ class CFJacobian(LinearOperator):
         """the carried iteration can defer its iterate (nft_hartley_fuse.lazy_*):
         the direction is carried by the row-staged prologue"""
         grid = tuple(self._afull.shape)
-        # not where the prologue runs fused with the R2C pass (nft_pro_r2c: 2-D
-        # rows <= 1024), which keeps its direction in place
-        fused_r2c = len(grid) == 2 and grid[-1] <= 1024 and os.environ.get("NFT_PRO_R2C", "1") != "0"
-        return self.dir_blocks(k) > 0 and 2 <= len(grid) <= 3 and grid[-1] // 2 + 1 <= 2556 and not fused_r2c
+        return self.dir_blocks(k) > 0 and 2 <= len(grid) <= 3 and grid[-1] // 2 + 1 <= 2556
 
     def grid_size(self):
         """elements of the grid key (the grid segment without its padding)"""

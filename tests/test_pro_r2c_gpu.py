@@ -119,3 +119,37 @@ def test_pro_r2c_fp32(ift, monkeypatch):
         a = torch.cat([e1.position[k].val.reshape(-1) for k in cf.domain.keys()])
         b = torch.cat([e2.position[k].val.reshape(-1) for k in cf.domain.keys()])
         assert _rel(a, b) < 1e-4
+
+
+@pytest.mark.parametrize("shape,kind", [((512, 512), "los"), ((256, 1024), "gauss")])
+def test_pro_r2c_lazy_iterate_bitwise(ift, shape, kind, monkeypatch):
+    """the fused pass with the deferred iterate of count-only chunks (its
+    directions in ring slots, nft_cg_lazy_flush) gives bitwise the per-step
+    update, across the residual refreshes and a compaction"""
+    from nifty_amd import _native
+    from nifty_amd.minimization import fused_cg
+    cf, A = _problem(ift, shape, kind)
+    es = _energies(ift, cf, A, 3)
+    flushes = []
+    orig = _native.cg_lazy_flush
+
+    def spy(*a, **kw):
+        flushes.append(a[6])
+        return orig(*a, **kw)
+    monkeypatch.setattr(_native, "cg_lazy_flush", spy)
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(fused_cg, "LAZY", on)
+        flushes.clear()
+        monkeypatch.setenv("NFT_PRO_R2C", "2")
+        from nifty_amd.minimization.fused_cg import fusable_metric
+        core, W, shift = fusable_metric(A)
+        cg = fused_cg.FusedCGBatch(core, W, shift, [ift.GradientNormController(iteration_limit=m)
+                                                    for m in (9, 24, 31)])
+        out[on] = cg.run(es)
+        assert cg.path == "carry+chunk", cg.path
+        assert bool(flushes) == on
+    for (e1, s1), (e2, s2) in zip(out[True], out[False]):
+        assert s1 == s2
+        for key in cf.domain.keys():
+            assert torch.equal(e1.position[key].val, e2.position[key].val), key
