@@ -19,6 +19,11 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/replay_$tag -o run -- python3 $R/tools/replay_probe.py > $R/gpurun_out/replay_$tag.log 2>&1 || exit $?
 cd $R
 python3 tools/trace_labels.py gpurun_out/replay_$tag/run_kernel_trace.csv 20 > gpurun_out/trace_labels_$tag.json || exit $?
+# the count-only chunk with the deferred iterate (19 replays, then the flush)
+cd /tmp
+LAZY_CHUNK=1 REPLAYS=19 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/replayl_$tag -o run -- python3 $R/tools/replay_probe.py > $R/gpurun_out/replayl_$tag.log 2>&1 || exit $?
+cd $R
+python3 tools/trace_labels.py gpurun_out/replayl_$tag/run_kernel_trace.csv 19 > gpurun_out/trace_labels_lazy_$tag.json || exit $?
 cd /tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$tag -o run -- python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/bench_${tag}_under_rocprof.json 2> $R/gpurun_out/prof_$tag.err
 echo "done rc=$?"

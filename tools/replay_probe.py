@@ -36,6 +36,14 @@ def main():
     for _ in range(3):
         body()
     torch.cuda.synchronize()
+    lz = bench.lazy_spec(core, k, X.shape[1], X.dtype) if os.environ.get("LAZY_CHUNK") == "1" else None
+    if lz is not None:
+        # the timed loop's count-only chunk: REPLAYS (19) steps with the
+        # deferred iterate from slot 0, then the flush (the trace's trailing
+        # dispatch, outside the periodic tail tools/trace_labels.py reads)
+        wall = bench.cg_iteration_lazy_wall(lib, core, W, shift, bufs, k, lz, int(os.environ.get("REPLAYS", "19")))
+        print(f"lazy chunk: {wall:.1f} us per iteration, flush included", flush=True)
+        return
     g = fused_cg._capture(body)
     g.replay()
     torch.cuda.synchronize()
