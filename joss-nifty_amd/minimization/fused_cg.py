@@ -594,8 +594,10 @@ class FusedCGBatch(FusedCG):
             # between the chunk's host reads)
             st["lazy"] = None
             spl = st["split"]
+            ring_bytes = self.nreset * k * n * X.element_size()
             if (LAZY and chunkable0 and HIST is None and not need_value and isinstance(spl, _CarryIteration)
-                    and spl.na and getattr(core, "lazy_ok", lambda k: False)(k)):
+                    and spl.na and getattr(core, "lazy_ok", lambda k: False)(k)
+                    and ring_bytes <= 0.5 * torch.cuda.mem_get_info(dev)[0]):
                 g0 = spl.g0
                 ring = torch.empty((self.nreset, k, n), dtype=X.dtype, device=dev)
                 alpha = torch.empty((k, self.nreset), dtype=torch.float64, device=dev)
