@@ -4,7 +4,7 @@
 # short bench runs (no CPU baseline, no demo line)
 var=$1; vals=$2; shift 2
 mkdir -p gpurun_out
-for i in 1 2; do
+for i in ${ROUNDS:-1 2}; do
   for v in $vals; do
     env $var=$v timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-demo "$@" > gpurun_out/abb_$v.$i.json 2> gpurun_out/abb_$v.$i.err || exit $?
     python3 -c "
