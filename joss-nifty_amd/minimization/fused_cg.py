@@ -755,7 +755,9 @@ class FusedCGBatch(FusedCG):
                 k = X.shape[0]
                 Q, Bu = st["Q"], st["Bu"]
                 split = st["split"]
-                if REFRESH_CARRY and not first and isinstance(split, _CarryIteration) and not st["xbdot"]:
+                # (x.r and x.b of the step come from the residual pass below,
+                # traced or not: the same path either way)
+                if REFRESH_CARRY and not first and isinstance(split, _CarryIteration):
                     # the residual refresh's step itself as the carried
                     # iteration (direction, q, curvature, x / r update; its
                     # finalize leaves GPREV = the step's gamma), then r
