@@ -308,10 +308,6 @@ _AMP2 = os.environ.get("NFT_CG_AMP2", "1") != "0"
 # x is brought up to date once per chunk (nft_cg_lazy_flush, bitwise the
 # per-step update); NFT_CG_LAZY=0: x updated every step
 LAZY = os.environ.get("NFT_CG_LAZY", "1") != "0"
-# the residual refresh's step (every nreset-th) as the carried iteration,
-# then r = A x - b as before (NFT_CG_REFRESH_CARRY=0: the separate direction,
-# metric, curvature d.q and update passes for that step)
-REFRESH_CARRY = os.environ.get("NFT_CG_REFRESH_CARRY", "1") != "0"
 
 
 class _CarryIteration:
@@ -754,27 +750,13 @@ class FusedCGBatch(FusedCG):
             else:
                 k = X.shape[0]
                 Q, Bu = st["Q"], st["Bu"]
-                split = st["split"]
-                # (x.r and x.b of the step come from the residual pass below,
-                # traced or not: the same path either way)
-                if REFRESH_CARRY and not first and isinstance(split, _CarryIteration):
-                    # the residual refresh's step itself as the carried
-                    # iteration (direction, q, curvature, x / r update; its
-                    # finalize leaves GPREV = the step's gamma), then r
-                    # recomputed from x below
-                    split(X, Rr, D, Q, SC)
-                    if isinstance(split, _CarryIteration):
-                        STATS["carry_iters"] += 1
-                    gp = SC[:, _native.CG_GPREV].clone()
-                else:
-                    if not first:
-                        chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), sp))
-                    core.metric_flat_batch(D, Q, self.W, 0.0)
-                    chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), sp))
-                    gp = SC[:, _native.CG_GAMMA].clone()
-                    chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws),
-                                                  sp))
+                if not first:
+                    chk(lib.nft_cg_direction_batched(P(D), P(Rr), n, n, k, dt, P(SC), sp))
                 first = False
+                core.metric_flat_batch(D, Q, self.W, 0.0)
+                chk(lib.nft_cg_curv_batched(P(D), P(Q), n, n, k, dt, sh, P(SC), P(ws), sp))
+                gp = SC[:, _native.CG_GAMMA].clone()
+                chk(lib.nft_cg_update_batched(P(X), P(Rr), P(D), P(Q), P(Bu), n, n, k, dt, sh, P(SC), P(ws), sp))
                 if st["AX"] is None:
                     st["AX"] = torch.zeros_like(X)
                 AX = st["AX"]
