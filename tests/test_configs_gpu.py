@@ -269,3 +269,39 @@ def test_c5_geovi_draw_4096_fp32(ift):
     d = float(np.mean(v32) - np.mean(v64))
     assert abs(d - pred) <= 0.05 * abs(pred) + 1e-9 * abs(np.mean(v64)), (d, pred)
     assert abs(out["fp32"].value - float(np.mean(v32))) <= 1e-12 * abs(out["fp32"].value)
+
+
+def test_c5_fp32_lazy_iterate_bitwise(ift, monkeypatch):
+    """C5's fp32 storage with the deferred iterate of count-only chunks (fp32
+    ring slots, the flush's fp32 x - alpha d): bitwise the per-step update"""
+    from nifty_amd import _native, config
+    from nifty_amd.minimization import fused_cg
+    cf, lh, pos = _gauss_problem(ift, (256, 256))
+    met, _ = _metric(ift, lh, pos)
+    flushes = []
+    orig = _native.cg_lazy_flush
+
+    def spy(*a, **kw):
+        flushes.append(a[6])
+        return orig(*a, **kw)
+    monkeypatch.setattr(_native, "cg_lazy_flush", spy)
+    with ift.random.Context(6):
+        es = [ift.QuadraticEnergy(0 * ift.from_random(cf.domain, "normal"), met, ift.from_random(cf.domain, "normal"))
+              for _ in range(2)]
+    out = {}
+    config.set_cg_precision("fp32")
+    try:
+        core, W, shift = fused_cg.fusable_metric(met)
+        for on in (True, False):
+            monkeypatch.setattr(fused_cg, "LAZY", on)
+            flushes.clear()
+            cg = fused_cg.FusedCGBatch(core, W, shift, [ift.GradientNormController(iteration_limit=m) for m in (12, 27)])
+            out[on] = cg.run(es)
+            assert cg.path == "carry+chunk", cg.path
+            assert bool(flushes) == on
+    finally:
+        config.set_cg_precision("fp64")
+    for (e1, s1), (e2, s2) in zip(out[True], out[False]):
+        assert s1 == s2
+        for k in cf.domain.keys():
+            assert torch.equal(e1.position[k].val, e2.position[k].val), k
