@@ -568,7 +568,8 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
         // deferred iterate (nft_hartley_fuse.lazy_*): d from the ring slot this
         // step's prologue wrote, x untouched, the step's alpha recorded
         const bool lazy = a.f.lazy != 0;
-        const long long sl = lazy ? (long long)scb[NFT_CG_LAZY] : 0;
+        // (clamped: a counter out of range never addresses outside the ring)
+        const long long sl = lazy ? min(max((long long)scb[NFT_CG_LAZY], 0LL), a.f.lnslot - 1) : 0;
         if (lazy && tid == 0 && t - item * a.f.ctr == 0)
           a.f.lalpha[item * a.f.lnslot + sl] = ok ? alpha : __builtin_nan("");
         const T* __restrict__ ea = (const T*)a.f.ea;

@@ -950,7 +950,8 @@ __global__ __launch_bounds__(256) void pro_rows_kernel(fast::FuseArgs f, T* __re
     pxs[b] = px;
     pds[b] = pd;
     if (lazy && b < nb) {
-      const long long sl = (long long)f.dsc[b * NFT_CG_NSCALARS + NFT_CG_LAZY];
+      // (clamped: a counter out of range never addresses outside the ring)
+      const long long sl = min(max((long long)f.dsc[b * NFT_CG_NSCALARS + NFT_CG_LAZY], 0LL), f.lnslot - 1);
       pxs[b] = sl == 0 ? px : (const T*)f.lring + (sl - 1) * f.lss;
       pds[b] = (T*)f.lring + sl * f.lss;
     }

@@ -70,7 +70,8 @@ __global__ __launch_bounds__(N / 8) void pro_r2c_kernel(fast::FuseArgs f, const 
   const T* pxs = px;
   T* pds = pd;
   if (f.lazy) {
-    const long long sl = (long long)scb[NFT_CG_LAZY];
+    // (clamped: a counter out of range never addresses outside the ring)
+    const long long sl = min(max((long long)scb[NFT_CG_LAZY], 0LL), f.lnslot - 1);
     pxs = sl == 0 ? px : (const T*)f.lring + (sl - 1) * f.lss;
     pds = (T*)f.lring + sl * f.lss;
   }
