@@ -330,6 +330,18 @@ typedef struct nft_hartley_fuse {
   int64_t lazy_sstride;
   double* lazy_alpha;
   int64_t lazy_nslot;
+  /* curvature fold carried by the transform (fold_nrhs > 0): fold_out[r *
+   * fold_ostride] = the sum of fold_part[r * fold_nb + b] over b < fold_nb
+   * for r < fold_nrhs, bitwise nft_fold_partials, formed by the first
+   * workgroups of the R2C row pass (any other geometry, or with a prologue:
+   * by nft_fold_partials launched first).  It lets the adjoint transform of
+   * a sampling metric with a pointwise W fold the quad_part partials of the
+   * forward one on its way (conjugate_gradient.py:101's d.q). */
+  const double* fold_part;
+  int64_t fold_nb;
+  double* fold_out;
+  int64_t fold_ostride;
+  int64_t fold_nrhs;
 } nft_hartley_fuse;
 
 /* Partial blocks per item of the CG-carrying epilogue for a batched

@@ -110,7 +110,8 @@ class HartleyFuse(ctypes.Structure):
                [("dir_pstride", _i64), ("dir_shift", _d), ("dir_blk0", ctypes.c_int32), ("dir_pad", ctypes.c_int32)] + \
                [("epi_out2_pairs", _i64)] + \
                [("quad_part", _p), ("quad_pstride", _i64), ("quad_blk0", ctypes.c_int32), ("quad_pad", ctypes.c_int32)] + \
-               [("lazy_ring", _p), ("lazy_sstride", _i64), ("lazy_alpha", _p), ("lazy_nslot", _i64)]
+               [("lazy_ring", _p), ("lazy_sstride", _i64), ("lazy_alpha", _p), ("lazy_nslot", _i64)] + \
+               [("fold_part", _p), ("fold_nb", _i64), ("fold_out", _p), ("fold_ostride", _i64), ("fold_nrhs", _i64)]
 
 
 class LosPlan(ctypes.Structure):
@@ -441,7 +442,7 @@ def cg_lazy_flush(x, d, ring, sstride, alpha, nslot, nsteps, n, vstride, k):
 
 
 def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0, shape=None, batch=None, cg=None,
-                  quad=None):
+                  quad=None, fold=None):
     """out = epilogue(scale * Hartley(prologue)) with
     pro = dict(a=, x=, b=, c=, index=) (or fold=True and c per fundamental
     cell instead of index, nft_hartley_fuse.pro_folded) and
@@ -449,7 +450,9 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
     (nft_hartley_fused); `x` is the plain input when no prologue is given.
     Batched transforms: `shape` = (k, *grid), axes over the grid, and
     batch = dict(period=, x=, c=, out=, d=, out2=) with the per-item strides
-    of the operands (elements); `out` may then be a strided base pointer."""
+    of the operands (elements); `out` may then be a strided base pointer.
+    fold: (part, nb, nrhs, out_address, out_stride) of an nft_fold_partials
+    call carried by the transform's R2C row pass (nft_hartley_fuse.fold_*)."""
     lib = load()
     f = HartleyFuse()
     if batch:
@@ -507,6 +510,15 @@ def hartley_fused(out, axes, scale=1.0, x=None, pro=None, epi=None, convention=0
         f.quad_part = qp.data_ptr()
         f.quad_pstride = int(quad["pstride"])
         f.quad_blk0 = int(quad.get("blk0", 0))
+    if fold is not None:
+        part, nb, nrhs, faddr, fstride = fold
+        if not (part.is_cuda and part.dtype == torch.float64):
+            raise NativeError("carried fold: fp64 device partials")
+        f.fold_part = part.data_ptr()
+        f.fold_nb = int(nb)
+        f.fold_out = int(faddr)
+        f.fold_ostride = int(fstride)
+        f.fold_nrhs = int(nrhs)
     if batch:
         for t in tens:
             if t is not None and not t.is_cuda:

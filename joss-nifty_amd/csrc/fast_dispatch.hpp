@@ -98,6 +98,12 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     set_last_error("out2 pair sums: only the strided unpack pass stores them");
     return NFT_ERR_UNSUPPORTED;
   }
+  // the carried curvature fold: extra leading workgroups of the R2C row pass
+  const int nfold = KIND == K_R2C ? a.f.fnrhs : 0;
+  if (a.f.fnrhs > 0 && (KIND != K_R2C || !a.f.fpart || !a.f.fout || a.f.fnb < 1 || a.f.fnrhs > 65535)) {
+    set_last_error("carried curvature fold: only the R2C row pass carries it (partials, output, nb >= 1)");
+    return NFT_ERR_UNSUPPORTED;
+  }
   if (a.f.cg || a.f.quad) {
     // the CG update / the quadratic-form partials ride only in the strided
     // unpack pass, one item per tile
@@ -142,7 +148,7 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
   bool launched = false;
   if constexpr (persist_ok<N, NT, KIND, VP>()) {
     if (!launched && !a.f.pro) {
-      const long long grid = std::min<long long>(ntiles, (long long)ncu * std::max(1, per_cu));
+      const long long grid = std::min<long long>(ntiles, (long long)ncu * std::max(1, per_cu)) + nfold;
       hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, true, 0, VP>), dim3((unsigned)grid), dim3(NT), lds, s, b);
       launched = true;
     }
@@ -158,7 +164,8 @@ static int launch_one(const FastArgs<T>& a, hipStream_t s) {
     }
   }
   if (!launched)
-    hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 0, VP>), dim3((unsigned)ntiles), dim3(NT), lds, s, b);
+    hipLaunchKernelGGL((fast_kernel<T, N, NT, KIND, ROWS, false, 0, VP>), dim3((unsigned)(ntiles + nfold)), dim3(NT),
+                       lds, s, b);
   NFT_HIP_CHECK(hipGetLastError());
   return NFT_OK;
 }

@@ -75,7 +75,46 @@ struct FuseArgs {
   long long lss;
   double* lalpha;
   long long lnslot;
+  // CG curvature fold carried by the R2C row pass (nft_hartley_fuse.fold_*):
+  // its first fnrhs workgroups write fout[r * fos] = the sum of
+  // fpart[r * fnb + b] over b < fnb, before the pass's own tiles
+  const double* fpart;
+  double* fout;
+  long long fos;
+  int fnb, fnrhs;
 };
+
+// One RHS of the carried fold in nft_fold_partials' order (fold_wide: 1024
+// thread-strided sums, the 16 waves' shuffle trees, the wave totals in order)
+// by an NT-thread workgroup: virtual thread q * NT + t (q < 1024 / NT) keeps
+// its own sum, so the result is bitwise the separate launch's.
+template <int NT>
+__device__ __forceinline__ void cg_fold_rhs(const FuseArgs& f, int r, double* sh) {
+  static_assert(NT >= 64 && NT <= 1024 && 1024 % NT == 0, "cg_fold_rhs: NT divides 1024");
+  constexpr int V = 1024 / NT, WPB = NT / 64;
+  const double* part = f.fpart + (long long)r * f.fnb;
+  const int t = threadIdx.x;
+  double v[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) {
+    v[q] = 0.0;
+    for (int b = q * NT + t; b < f.fnb; b += 1024) v[q] += part[b];
+  }
+#pragma unroll
+  for (int q = 0; q < V; ++q)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[q] += __shfl_down(v[q], off, 64);
+  if ((t & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < V; ++q) sh[q * WPB + (t >> 6)] = v[q];
+  }
+  __syncthreads();
+  if (t == 0) {
+    double s = 0.0;
+    for (int w = 0; w < 16; ++w) s += sh[w];
+    f.fout[(long long)r * f.fos] = s;
+  }
+}
 
 // element index into pc of item-element j: its bin (pidx[j]) or, folded, the
 // bin of its fundamental cell (pidx[cell(j)]), times the element stride
@@ -281,6 +320,15 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   constexpr int SHN = ilog2(N), SHL = ilog2(L);
   extern __shared__ __align__(16) unsigned char smem[];
   C* lds = (C*)smem;
+  // the carried curvature fold: the first workgroups of the R2C row pass
+  int nfold = 0;
+  if constexpr (KIND == K_R2C) {
+    nfold = a.f.fnrhs;
+    if ((int)blockIdx.x < nfold) {
+      cg_fold_rhs<NT>(a.f, (int)blockIdx.x, (double*)smem);
+      return;
+    }
+  }
   C* twq = (C*)(smem + tw_lds_offset<T, N, NT, KIND, ROWS, VP>());
   for (int r = threadIdx.x; r < N / 4; r += NT) twq[r] = ((const C*)a.tw)[r];  // synced before the first stage
   const int tid = threadIdx.x;
@@ -361,7 +409,8 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
   constexpr bool PERSIST = PF;
   constexpr bool prefetch = PF;  // launched persistent only without a prologue
   C rv[VP];
-  long long t = blockIdx.x;
+  long long t = (long long)blockIdx.x - nfold;
+  const long long gstride = (long long)gridDim.x - nfold;
   if constexpr (!PERSIST) {
     if (a.bgroup > 1) t = a.bmode == 2 ? batch_tile_contig(t, ntiles, a.bgroup) : batch_tile(t, ntiles, a.bgroup);
   }
@@ -375,7 +424,7 @@ __global__ __launch_bounds__(NT) void fast_kernel(FastArgs<T> a) {
       lds[l * PITCH + padx<PS>(x)] = rv[r];
     }
     __syncthreads();
-    const long long tn = PERSIST ? t + gridDim.x : ntiles;
+    const long long tn = PERSIST ? t + gstride : ntiles;
     if (prefetch && tn < ntiles) load(tn, rv);  // in flight during the FFT and the stores
     fft<T, N, NT, L, PITCH, PS>(lds, twq, tid);
     long long o, m, i0;

@@ -473,7 +473,19 @@ static LineDesc make_desc(const Geo& g, const long long* cs, const std::vector<i
   return d;
 }
 
-// geometry covered by hartley_v2's multi-axis path
+// geometry covered by hartley_v2's multi-axis path (its first launch is the
+// R2C row pass along the last axis)
+static bool v2_multi_ok(const Geo& g, const std::vector<int>& ax) {
+  using namespace fast;
+  const int m = (int)ax.size();
+  if (m < 2) return false;
+  const int h = ax[m - 1];
+  if (h != g.nd - 1 || !rows_supported((int)g.shape[h])) return false;
+  for (int k = 1; k < m - 1; ++k)
+    if (!strided_supported((int)g.shape[ax[k]])) return false;
+  const int N0 = (int)g.shape[ax[0]];
+  return strided_supported(N0) || fourstep_supported(N0);
+}
 
 // r2c_done: the R2C row pass has already written the half spectra to ws
 template <typename T>
@@ -582,6 +594,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
       if (fz) {
         a.f = *fz;
         a.f.pro = 0;
+        a.f.fnrhs = 0;  // the fold rides in the R2C pass
       }
       return launch<T>(K_UNPACK, false, N, a, s);
     }
@@ -628,6 +641,7 @@ static int hartley_v2(const void* in, void* out, const Geo& g, const std::vector
       if (fz) {
         a.f = *fz;
         a.f.pro = 0;
+        a.f.fnrhs = 0;  // the fold rides in the R2C pass
       }
       return launch<T>(K_UNPACK, false, N2, a, s);
     }
@@ -1159,6 +1173,15 @@ template <typename T>
 static int hartley_fused_impl(const fast::FuseArgs& f, const void* in, void* out, const Geo& g,
                               const std::vector<int>& ax, int sigma, double scale, void* ws, size_t ws_bytes,
                               size_t hws, hipStream_t s) {
+  if (f.fnrhs > 0 && (f.pro || !v2_multi_ok(g, ax))) {
+    // the carried curvature fold needs the plain R2C row pass of engine v2:
+    // otherwise it runs as its own launch first (the same sums)
+    int st = nft_fold_partials(f.fpart, f.fnb, f.fnrhs, f.fout, f.fos, s);
+    if (st != NFT_OK) return st;
+    fast::FuseArgs f1 = f;
+    f1.fnrhs = 0;
+    return hartley_fused_impl<T>(f1, in, out, g, ax, sigma, scale, ws, ws_bytes, hws, s);
+  }
   const long long ntot = prod(g.shape, 0, g.nd);
   if (f.dr && !(f.fnd > 0 && f.pb && f.sa == 0 && f.sb == 0 && f.P > 0 &&
                 (long long)f.nb * f.P == ntot && ws_bytes >= align256(hws) + (size_t)ntot * sizeof(T))) {
@@ -1506,6 +1529,20 @@ int nft_hartley_fused(const nft_hartley_fuse* fz, const void* in, void* out, int
       f.lss = fz->lazy_sstride;
       f.lalpha = fz->lazy_alpha;
       f.lnslot = fz->lazy_nslot;
+    }
+    f.fnrhs = 0;
+    if (fz->fold_nrhs > 0) {
+      if (!fz->fold_part || !fz->fold_out || fz->fold_nb < 1 || fz->fold_nb > 0x7fffffffLL ||
+          fz->fold_nrhs > 65535) {
+        set_last_error("nft_hartley_fused: the carried fold needs its partials, output, 1 <= fold_nb and "
+                       "fold_nrhs <= 65535");
+        return NFT_ERR_ARG;
+      }
+      f.fpart = fz->fold_part;
+      f.fout = fz->fold_out;
+      f.fos = fz->fold_ostride;
+      f.fnb = (int)fz->fold_nb;
+      f.fnrhs = (int)fz->fold_nrhs;
     }
   }
   const int sigma = convention == 0 ? 1 : -1;

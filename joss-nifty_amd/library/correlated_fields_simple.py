@@ -63,6 +63,11 @@ _AMP_NATIVE_FWD = os.environ.get("NFT_AMP_NATIVE_FWD", "1") != "0"
 # folded prologue gather (NFT_PRO_FOLD=0 restores the per-pixel pindex gather)
 _PRO_FOLD = os.environ.get("NFT_PRO_FOLD", "1") != "0"
 
+# the CG curvature fold carried by the adjoint transform's R2C row pass
+# (nft_hartley_fuse.fold_*; NFT_FOLD_R2C=0: its own launch between W and the
+# adjoint)
+_FOLD_R2C = os.environ.get("NFT_FOLD_R2C", "1") != "0"
+
 # constant-scan tables for the two-phase amplitude kernels (nft_amp2_prepare:
 # bitwise the same results with fewer scans); tests switch it off for A/B
 AMP2_TABLE = True
@@ -871,8 +876,11 @@ class CFJacobian(LinearOperator):
             else:
                 g = (W(s, qpart=qpart) if qpart is not None else W(s)) if callable(W) else s * W
             g = g.contiguous()
+        fold = None
         if after_w is not None:
-            after_w()
+            fold = getattr(after_w, "spec", None) if _FOLD_R2C else None
+            if fold is None:
+                after_w()
         w = bufs["w"]
         pairs = self._pairs(k)
         epi = dict(a=afull, b=xi0, out2=w, pairs=pairs)
@@ -881,7 +889,7 @@ class CFJacobian(LinearOperator):
             epi.update(d=D[0, xo:], shift=shift)
             bt["d"] = size
         _native.hartley_fused(Q[0, xo:], axes, m.c_h, x=g, epi=epi, convention=conv, shape=(k,) + grid, batch=bt,
-                              cg=cg)
+                              cg=cg, fold=fold)
         return w
 
     def mv_fold(self, w):

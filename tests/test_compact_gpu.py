@@ -181,3 +181,61 @@ def test_lazy_iterate_bitwise(ift, which, monkeypatch):
         assert s1 == s2
         for key in cf.domain.keys():
             assert torch.equal(e1.position[key].val, e2.position[key].val), key
+
+
+def test_fold_in_adjoint_r2c_bitwise(ift, monkeypatch):
+    """the carried iteration's curvature fold inside the adjoint transform's
+    R2C row pass (nft_hartley_fuse.fold_*, pointwise W) gives bitwise the
+    separate nft_fold_partials"""
+    from nifty_amd import _native
+    from nifty_amd.library import correlated_fields_simple as cfs
+    from nifty_amd.minimization.fused_cg import FusedCGBatch
+    cf, A, (core, W, shift) = _metric(ift, "gauss")
+    assert torch.is_tensor(W)
+    es = _energies(ift, cf, A, 3, 5)
+    lims = [6, 9, 23]
+    calls = []
+    orig = _native.hartley_fused
+
+    def spy(*a, **kw):
+        calls.append(kw.get("fold") is not None)
+        return orig(*a, **kw)
+    monkeypatch.setattr(_native, "hartley_fused", spy)
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(cfs, "_FOLD_R2C", on)
+        calls.clear()
+        cg = FusedCGBatch(core, W, shift, [ift.GradientNormController(iteration_limit=m) for m in lims])
+        out[on] = cg.run(es)
+        assert cg.path.startswith("carry"), cg.path
+        assert any(calls) == on
+    for (e1, s1), (e2, s2) in zip(out[True], out[False]):
+        assert s1 == s2
+        for key in cf.domain.keys():
+            assert torch.equal(e1.position[key].val, e2.position[key].val), key
+
+
+@pytest.mark.parametrize("shape", [(16, 256), (8, 2048), (8, 4096), (4, 8192), (8, 16, 64), (4, 96)])
+def test_hartley_carried_fold_direct(shape):
+    """nft_hartley_fuse.fold_*: the sums bitwise nft_fold_partials' for every
+    R2C workgroup size (256 / 512 / 1024 threads), the transform unchanged; a
+    geometry without the engine-v2 R2C pass (4 x 96) folds in its own launch"""
+    from nifty_amd import _native
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randn(shape, generator=g, dtype=torch.float64).to(dev)
+    axes = tuple(range(len(shape)))
+    nrhs, nb = 3, 2311
+    part = torch.randn((nrhs, nb), generator=g, dtype=torch.float64).to(dev)
+    ref = torch.full((nrhs, 5), -1.0, dtype=torch.float64, device=dev)
+    _native._check(_native.load().nft_fold_partials(_native.ptr(part), nb, nrhs, _native.ptr(ref), 5,
+                                                    _native.stream_ptr()))
+    got = torch.full((nrhs, 5), -1.0, dtype=torch.float64, device=dev)
+    h0 = torch.empty_like(x)
+    h1 = torch.empty_like(x)
+    _native.hartley_fused(h0, axes, 1.0, x=x)
+    _native.hartley_fused(h1, axes, 1.0, x=x, fold=(part, nb, nrhs, got.data_ptr(), 5))
+    torch.cuda.synchronize()
+    assert torch.equal(h0, h1)
+    assert torch.equal(got, ref)
+    assert torch.equal(got[:, 1:], torch.full_like(got[:, 1:], -1.0))

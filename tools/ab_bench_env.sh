@@ -10,7 +10,7 @@ for i in ${ROUNDS:-1 2}; do
     python3 -c "
 import json
 d=json.loads(open('gpurun_out/abb_$v.$i.json').read().strip().splitlines()[-1])
-print('$var=$v', d['value'], d['ms_per_step'], d.get('cg_iter_per_s'))
+print('$var=$v', d['value'], d['ms_per_step'], d.get('cg_iter_per_s'), (d.get('cg_iteration') or {}).get('us_per_iteration'))
 "
   done
 done
