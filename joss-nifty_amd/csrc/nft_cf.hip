@@ -442,6 +442,88 @@ __global__ __launch_bounds__(256) void bin_fold_half_sorted(const T* __restrict_
   }
 }
 
+// bin_fold_half_sorted over the flat cell index: one cell per thread, the
+// cell row decoded per thread.  A row-per-workgroup launch runs ~2 rounds of
+// its loads per row (h = n/2 + 1 cells: the last round for one cell) at 2
+// workgroups per CU for 1024^2; here every thread issues its loads once and
+// the grid holds n/2 + 1 times more threads.  Same sums in the same order,
+// same stores (bitwise).
+template <typename T, int PRE>
+__global__ __launch_bounds__(256) void bin_fold_half_flat(const T* __restrict__ in, T* __restrict__ out,
+                                                          const int* __restrict__ cpos, FoldShape fs,
+                                                          unsigned ncell, long long nhalf, int pre) {
+  const unsigned e = blockIdx.x * 256u + threadIdx.x;
+  if (e >= ncell) return;
+  const int D = fs.d;
+  const unsigned hl = (unsigned)fs.h[D - 1];
+  const unsigned o = e / hl, x = e - o * hl;
+  unsigned r = o;
+  long long q[FOLD_MAXD], m[FOLD_MAXD];
+  bool two[FOLD_MAXD];
+#pragma unroll
+  for (int a = FOLD_MAXD - 1; a >= 0; --a) {
+    q[a] = m[a] = 0;
+    two[a] = false;
+    if (a < D - 1) {
+      const unsigned h = (unsigned)fs.h[a];
+      const unsigned qq = r % h;
+      r /= h;
+      q[a] = qq;
+      m[a] = fs.n[a] - q[a];
+      two[a] = q[a] != 0 && m[a] != q[a];
+    }
+  }
+  constexpr int NS = 1 << (FOLD_MAXD - 1);
+  long long roff[NS];
+  bool rok[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    bool ok = true;
+    long long idx = 0;
+#pragma unroll
+    for (int a = 0; a < FOLD_MAXD - 1; ++a) {
+      if (a >= D - 1) continue;
+      const bool hi = (s >> (FOLD_MAXD - 2 - a)) & 1;
+      ok = ok && (!hi || two[a]);
+      idx = idx * fs.n[a] + (hi ? m[a] : q[a]);
+    }
+    for (int a = D - 1; a < FOLD_MAXD - 1; ++a) ok = ok && !((s >> (FOLD_MAXD - 2 - a)) & 1);
+    rok[s] = ok;
+    roff[s] = idx * (long long)hl;
+  }
+  T v[PRE][NS];
+#pragma unroll
+  for (int p = 0; p < PRE; ++p)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) v[p][s] = (p < pre && rok[s]) ? in[p * nhalf + roff[s] + x] : (T)0;
+  const long long dpos = (cpos ? (long long)cpos[e] : (long long)e) * pre;
+  T accs[PRE];
+#pragma unroll
+  for (int p = 0; p < PRE; ++p) {
+    T acc = (T)0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (rok[s]) acc += v[p][s];
+    accs[p] = acc;
+  }
+  if (PRE % 2 == 0 && pre == PRE) {
+    typedef T V2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < PRE; p += 2) {
+      V2 w;
+      w.x = accs[p];
+      w.y = accs[p + 1];
+      *(V2*)(out + dpos + p) = w;
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) {
+      if (p >= pre) break;
+      out[dpos + p] = accs[p];
+    }
+  }
+}
+
 // The bin sums of the fold in cell order with the items interleaved
 // (bin_fold_half_sorted with cpos = NULL: in[cell * PRE + p]): chunks of CH
 // bin-sorted positions as in bin_scatter_chunk, one 8 PRE-byte gather per
@@ -793,10 +875,21 @@ int nft_bin_fold_half_sorted(const void* in, void* out, const int* cpos, int64_t
   }
   const long long nrows = fs.nout / fs.h[ndim - 1];
   const unsigned grid = (unsigned)std::min<long long>(nrows, 1LL << 20);
+  // the flat launch (NFT_FOLD_FLAT=0: one workgroup per cell row)
+  const char* fenv = getenv("NFT_FOLD_FLAT");
+  const bool flat_knob = !(fenv && fenv[0] == '0');
+  const bool flat = flat_knob && fs.nout < (1LL << 31) - 256;
+  const unsigned fgrid = (unsigned)((fs.nout + 255) / 256);
   prof_mark(stream, "bin_fold");
-#define NFT_FS(TT, PP)                                                                                     \
-  hipLaunchKernelGGL((bin_fold_half_sorted<TT, PP>), dim3(grid), dim3(256), 0, stream, (const TT*)in, (TT*)out, \
-                     cpos, fs, nrows, nhalf, (int)pre)
+#define NFT_FS(TT, PP)                                                                                          \
+  do {                                                                                                          \
+    if (flat)                                                                                                   \
+      hipLaunchKernelGGL((bin_fold_half_flat<TT, PP>), dim3(fgrid), dim3(256), 0, stream, (const TT*)in,        \
+                         (TT*)out, cpos, fs, (unsigned)fs.nout, nhalf, (int)pre);                               \
+    else                                                                                                        \
+      hipLaunchKernelGGL((bin_fold_half_sorted<TT, PP>), dim3(grid), dim3(256), 0, stream, (const TT*)in,      \
+                         (TT*)out, cpos, fs, nrows, nhalf, (int)pre);                                           \
+  } while (0)
   if (dtype == 0) {
     if (pre <= 1) NFT_FS(double, 1);
     else if (pre <= 2) NFT_FS(double, 2);
