@@ -349,6 +349,60 @@ __global__ __launch_bounds__(256) void bin_fold_half_rows(const T* __restrict__ 
   }
 }
 
+// bin_fold_half_rows over the flat output index (one output per thread, its
+// row decoded with 32-bit divisions): the row launch spends a second round
+// of loads on each row's last element (h = n/2 + 1 = 4 x 256 + 1 at 2048^2).
+// Same sums in the same order (bitwise).
+template <typename T>
+__global__ __launch_bounds__(256) void bin_fold_half_flat_planar(const T* __restrict__ in, T* __restrict__ out,
+                                                                 FoldShape fs, unsigned tot, long long nhalf) {
+  const unsigned e = blockIdx.x * 256u + threadIdx.x;
+  if (e >= tot) return;
+  const int D = fs.d;
+  const unsigned hl = (unsigned)fs.h[D - 1];
+  const unsigned o = e / hl, x = e - o * hl;
+  unsigned r = o;
+  long long q[FOLD_MAXD], m[FOLD_MAXD];
+  bool two[FOLD_MAXD];
+#pragma unroll
+  for (int a = FOLD_MAXD - 1; a >= 0; --a) {
+    q[a] = m[a] = 0;
+    two[a] = false;
+    if (a < D - 1) {
+      const unsigned h = (unsigned)fs.h[a];
+      const unsigned qq = r % h;
+      r /= h;
+      q[a] = qq;
+      m[a] = fs.n[a] - q[a];
+      two[a] = q[a] != 0 && m[a] != q[a];
+    }
+  }
+  const T* src = in + (long long)r * nhalf + x;  // r: the item
+  constexpr int NS = 1 << (FOLD_MAXD - 1);
+  T v[NS];
+  bool rok[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    bool ok = true;
+    long long idx = 0;
+#pragma unroll
+    for (int a = 0; a < FOLD_MAXD - 1; ++a) {
+      if (a >= D - 1) continue;
+      const bool hi = (s >> (FOLD_MAXD - 2 - a)) & 1;
+      ok = ok && (!hi || two[a]);
+      idx = idx * fs.n[a] + (hi ? m[a] : q[a]);
+    }
+    for (int a = D - 1; a < FOLD_MAXD - 1; ++a) ok = ok && !((s >> (FOLD_MAXD - 2 - a)) & 1);
+    rok[s] = ok;
+    v[s] = ok ? src[idx * (long long)hl] : (T)0;
+  }
+  T acc = (T)0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (rok[s]) acc += v[s];
+  out[e] = acc;
+}
+
 // The half-grid fold written in bin-sorted order, the items of a cell
 // adjacent: out[cpos[cell] * pre + p] (cpos = inverse of the folded index's
 // stable bin -> cell permutation).  One workgroup per cell row, all pre items
@@ -826,11 +880,19 @@ int nft_bin_fold_half(const void* in, void* out, int64_t pre, int ndim, const in
   const long long tot = pre * fs.nout;
   if (tot <= 0) return NFT_OK;
   prof_mark(stream, "bin_fold");
-  // one workgroup per output row
+  // one output per thread (NFT_FOLD_FLAT=0: one workgroup per output row)
+  const char* fenv = getenv("NFT_FOLD_FLAT");
+  const bool flat = !(fenv && fenv[0] == '0') && tot < (1LL << 31) - 256;
   constexpr bool rows = true;
   const long long nouter = tot / fs.h[ndim - 1];
   const unsigned rgrid = (unsigned)std::min<long long>(nouter, 1LL << 20);
-  if (rows && dtype == 0)
+  if (flat && dtype == 0)
+    hipLaunchKernelGGL(bin_fold_half_flat_planar<double>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream,
+                       (const double*)in, (double*)out, fs, (unsigned)tot, nhalf);
+  else if (flat && dtype == 1)
+    hipLaunchKernelGGL(bin_fold_half_flat_planar<float>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream,
+                       (const float*)in, (float*)out, fs, (unsigned)tot, nhalf);
+  else if (rows && dtype == 0)
     hipLaunchKernelGGL(bin_fold_half_rows<double>, dim3(rgrid), dim3(256), 0, stream, (const double*)in,
                        (double*)out, fs, nouter, nhalf);
   else if (rows && dtype == 1)
